@@ -1,0 +1,300 @@
+#!/usr/bin/env python3
+"""Benchmark of the gradient-bucket allreduce engine (BASELINE.json metric:
+"device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X").
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+A step is one pass of the hot path over one bucket resident in HBM:
+  * N = 1 (BASELINE configs[1], "1xMI355X: local reduce kernel only, fp32 bucket sweep"): the
+    per-hop reduce kernel acc += in over a 256 MiB fp32 bucket; value = bucket GiB/s. A sweep
+    4 KiB..1 GiB of the same kernel is reported beside it.
+  * N > 1 (configs[2], ring over xGMI, fp32 256 MiB per rank): one ddl_allreduce (ring
+    reduce-scatter + allgather over RCCL send/recv, HIP reduce kernel); value = N * bucket
+    GiB / max-over-ranks step time (whole job). RCCL's own ncclAllReduce is timed beside it as
+    a comparator.
+rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'experiment-distributed-deep-learning_amd')
+sys.path.insert(0, PKG)
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0     # same doc: 6.29 TB/s measured float4 copy
+XGMI_LINK_GBS = 153.0         # task brief: per-link xGMI, 7 links per GPU
+DT_FLOAT = 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--bucket-mib', type=int, default=256)
+    ap.add_argument('--no-sweep', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--variant', type=int, default=0, help='reduce kernel variant (0 reg, 1 lds, 2 nt)')
+    return ap.parse_args()
+
+
+def pmc_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(n_bytes_sample, seconds):
+    """The oracle's MPI_SUM restatement (oracle/ddl_oracle.c, 1 thread) on a bounded sample of
+    the same workload: acc += in over a fp32 bucket of n_bytes_sample, repeated ~`seconds`."""
+    import numpy as np
+    lib = ctypes.CDLL(os.path.join(ROOT, 'oracle', 'build', 'libddl_oracle.so'))
+    lib.ddlo_reduce_reps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    n = n_bytes_sample // 4
+    rng = np.random.default_rng(1234)
+    acc = rng.uniform(-1, 1, n).astype(np.float32)
+    inp = rng.uniform(-1, 1, n).astype(np.float32)
+    lib.ddlo_reduce_reps(DT_FLOAT, acc.ctypes.data, inp.ctypes.data, n, 1)  # first touch
+    t0 = time.perf_counter()
+    lib.ddlo_reduce_reps(DT_FLOAT, acc.ctypes.data, inp.ctypes.data, n, 1)
+    one = max(time.perf_counter() - t0, 1e-6)
+    reps = max(1, int(seconds / one))
+    t0 = time.perf_counter()
+    lib.ddlo_reduce_reps(DT_FLOAT, acc.ctypes.data, inp.ctypes.data, n, reps)
+    dt = time.perf_counter() - t0
+    return {'value': round(n_bytes_sample * reps / dt / GiB, 3), 'unit': 'GiB/s', 'cores': 1, 'kind': 'port',
+            'sample': f'oracle ddlo_sum2 acc+=in, fp32 {n_bytes_sample >> 20} MiB x {reps} reps '
+                      f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM on the reference data plane'}
+
+
+def single_gpu(args):
+    import torch
+    from ddl.torch.cpp_backend import CPPBackend, check
+    lib = CPPBackend.c_api()
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    S = args.bucket_mib << 20
+    n = S // 4
+    g = torch.Generator(device=dev).manual_seed(1234)
+    acc = torch.rand(n, device=dev, generator=g) * 2 - 1
+    inp = torch.rand(n, device=dev, generator=g) * 2 - 1
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(a=acc, b=inp, m=n, variant=args.variant):
+        check(lib.ddl_reduce_sum2_variant(variant, a.data_ptr(), a.data_ptr(), b.data_ptr(), m, DT_FLOAT, sh),
+              'ddl_reduce_sum2_variant')
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
+    ms_per_step = wall * 1e3 / args.steps
+    value = S / GiB / (ms_per_step / 1e3)
+    achieved = 3.0 * S / (kernel_ms / 1e3) / 1e9
+
+    extra = {}
+    # kernel variants at the same size (interleaved in one process, guide §5.4 rule 24)
+    variants = {}
+    for v in (0, 1, 2):
+        times = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                step(variant=v)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / 10)
+        variants[['reg_stream', 'lds_stage', 'nontemporal'][v]] = round(3.0 * S / (min(times) / 1e3) / 1e9, 1)
+    extra['variants_achieved_GBs'] = variants
+
+    if not args.no_sweep:
+        sweep = []
+        size = 4 << 10
+        while size <= (1 << 30):
+            m = size // 4
+            a = torch.zeros(m, device=dev)
+            b = torch.ones(m, device=dev)
+            reps = int(min(2000, max(5, (64 << 20) // size * 4)))
+            for _ in range(3):
+                step(a, b, m)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                step(a, b, m)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / reps / 1e3
+            sweep.append({'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
+                          'hbm_GBs': round(3 * size / t / 1e9, 1)})
+            del a, b
+            size *= 4
+        extra['sweep_fp32'] = sweep
+
+    traffic = pmc_traffic(f'reduce_fp32_{args.bucket_mib}MiB')
+    out = {
+        'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
+        'value': round(value, 2),
+        'unit': 'GiB/s',
+        'n_gpus': 1,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_per_step, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic U(-1,1) fp32 bucket, resident in HBM',
+        'config': {'workload': 'C2: local reduce kernel acc += in (per-hop ring reduce), fp32, '
+                               f'{args.bucket_mib} MiB bucket, 1xMI355X',
+                   'bucket_bytes': S, 'parallelism': 'none (1 GPU)'},
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                     'kernel': 'k_sum2_vec<float>', 'kernel_ms': round(kernel_ms, 4),
+                     'algorithmic_bytes_per_launch': 3 * S,
+                     'frac_of_measured_copy_peak': round(achieved / HBM_MEASURED_GBS, 4)},
+    }
+    out.update(extra)
+    if not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+def multi_gpu(args):
+    import torch
+    import torch.distributed as dist
+    from ddl.torch.communicator import Communicator
+    from ddl.torch.cpp_backend import CPPBackend, check
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', rank))
+    torch.cuda.set_device(local)
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    comm = Communicator.world()
+    lib = CPPBackend.c_api()
+    dev = torch.device('cuda', local)
+    S = args.bucket_mib << 20
+    n = S // 4
+    g = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+    send = torch.randn(n, device=dev, generator=g)
+    recv = torch.empty_like(send)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(variant=0):
+        check(lib.ddl_allreduce_variant(comm.id, send.data_ptr(), recv.data_ptr(), n, DT_FLOAT, 0,
+                                        stream.cuda_stream, variant), 'ddl_allreduce_variant')
+
+    def timed(variant, steps, warmup):
+        for _ in range(warmup):
+            step(variant)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(variant)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item()
+
+    el = timed(0, args.steps, args.warmup)
+    # reduce-kernel roofline: time every reduce launch on the engine's compute stream
+    check(lib.ddl_kernel_timing(comm.id, 1), 'ddl_kernel_timing')
+    for _ in range(min(args.steps, 10)):
+        step(0)
+    torch.cuda.synchronize()
+    check(lib.ddl_kernel_timing(comm.id, 0), 'ddl_kernel_timing')
+    launches, kbytes, kms = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+    check(lib.ddl_kernel_stats(comm.id, ctypes.byref(launches), ctypes.byref(kbytes), ctypes.byref(kms)),
+          'ddl_kernel_stats')
+    el_rccl = timed(1, max(5, args.steps // 2), 3)
+    # correctness spot check: every rank's sum must match across ranks (checksum of checksums)
+    step(0)
+    torch.cuda.synchronize()
+    cs = torch.tensor([recv.double().sum().item()], dtype=torch.float64)
+    ref = torch.tensor([send.double().sum().item()], dtype=torch.float64)
+    dist.all_reduce(ref)
+    cs_max, cs_min = cs.clone(), cs.clone()
+    dist.all_reduce(cs_max, op=dist.ReduceOp.MAX)
+    dist.all_reduce(cs_min, op=dist.ReduceOp.MIN)
+
+    ms = el * 1e3 / args.steps
+    algbw = S / GiB / (ms / 1e3)
+    busbw = 2 * (world - 1) / world * algbw
+    ms_rccl = el_rccl * 1e3 / max(5, args.steps // 2)
+    link_ceiling = min(HBM_PEAK_GBS * 2 / 7, 7 * XGMI_LINK_GBS)  # SURVEY §8d, L = 7 links
+    avg_kernel_ms = kms.value / max(1, launches.value)
+    achieved = kbytes.value / max(1e-9, kms.value / 1e3) / 1e9
+    if rank == 0:
+        out = {
+            'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
+            'value': round(world * S / GiB / (ms / 1e3), 2),
+            'unit': 'GiB/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(ms, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic N(0,1) fp32 bucket per rank, resident in HBM',
+            'config': {'workload': f'C3: ring allreduce (RS+AG over RCCL send/recv, HIP reduce), fp32 '
+                                   f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
+                       'bucket_bytes': S, 'parallelism': f'dp{world}'},
+            'algbw_GiBs': round(algbw, 2),
+            'busbw_GBs': round(busbw * GiB / 1e9, 2),
+            'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling,
+                              'frac': round(busbw * GiB / 1e9 / link_ceiling, 4)},
+            'rccl_allreduce_comparator': {'ms': round(ms_rccl, 4),
+                                          'busbw_GBs': round(2 * (world - 1) / world * S / (ms_rccl / 1e3) / 1e9, 2)},
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'kernel': 'k_sum2_vec<float> (reduce-scatter step)',
+                         'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
+            'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
+                      'sum_of_inputs': ref.item()},
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    from ddl.torch.communicator import finalize
+    finalize()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', args.gpus))
+    if world <= 1:
+        single_gpu(args)
+    else:
+        multi_gpu(args)
+
+
+if __name__ == '__main__':
+    main()

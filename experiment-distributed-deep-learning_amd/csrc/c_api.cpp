@@ -1,0 +1,470 @@
+// c_api.cpp — extern "C" boundary (include/ddl_amd.h). Every entry point converts internal
+// errors into a status code; no C++ exception crosses the ABI.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "handler.h"
+
+using namespace ddl;
+
+namespace {
+
+template <typename F>
+int guarded(F &&f) {
+    try {
+        f();
+        return DDL_STATUS_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        DDL_LOG(1, "error " << e.status << ": " << e.msg);
+        return e.status;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return DDL_STATUS_ERROR_UNKNOWN;
+    } catch (...) {
+        set_error("unknown error");
+        return DDL_STATUS_ERROR_UNKNOWN;
+    }
+}
+
+hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
+
+int current_device() {
+    int d = 0;
+    DDL_HIP(hipGetDevice(&d));
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ddl_version(void) { return 1; }
+const char *ddl_last_error(void) { return last_error(); }
+const char *ddl_dtype_name(int dtype) { return dtype_name(dtype); }
+size_t ddl_dtype_size(int dtype) { return dtype_size(dtype); }
+
+int ddl_get_unique_id(void *out, size_t len) {
+    return guarded([&] {
+        DDL_REQUIRE(out && len >= sizeof(ncclUniqueId), DDL_STATUS_INVALID_ARGUMENT,
+                    "unique id buffer needs " << sizeof(ncclUniqueId) << " bytes");
+        ncclUniqueId id;
+        rccl_check(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+        std::memcpy(out, &id, sizeof id);
+    });
+}
+
+int ddl_init(int rank, int size, int device, const void *unique_id, size_t len) {
+    return guarded([&] {
+        DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad rank/size " << rank << "/" << size);
+        DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
+        DDL_HIP(hipSetDevice(device));
+        ncclComm_t nc = nullptr;
+        if (size > 1) {
+            DDL_REQUIRE(unique_id && len >= sizeof(ncclUniqueId), DDL_STATUS_INVALID_ARGUMENT,
+                        "unique id of " << sizeof(ncclUniqueId) << " bytes required");
+            ncclUniqueId id;
+            std::memcpy(&id, unique_id, sizeof id);
+            rccl_check(rccl().CommInitRank(&nc, size, id, rank), "ncclCommInitRank");
+        }
+        Registry::get().set_world(std::make_shared<Communicator>(rank, size, device, nc));
+        DDL_LOG(1, "initialized rank " << rank << "/" << size << " on device " << device
+                                       << (size > 1 ? std::string(" rccl=") + rccl().path : ""));
+    });
+}
+
+int ddl_init_single(int device) { return ddl_init(0, 1, device, nullptr, 0); }
+
+int ddl_control_listen(char *endpoint_out, size_t len) {
+    return guarded([&] {
+        std::string ep = world_control().listen();
+        DDL_REQUIRE(endpoint_out && len > ep.size(), DDL_STATUS_INVALID_ARGUMENT, "endpoint buffer too small");
+        std::memcpy(endpoint_out, ep.c_str(), ep.size() + 1);
+    });
+}
+
+int ddl_control_connect(const char *endpoints) {
+    return guarded([&] {
+        DDL_REQUIRE(endpoints, DDL_STATUS_INVALID_ARGUMENT, "null endpoints");
+        auto world = Registry::get().world();
+        std::vector<std::string> eps;
+        std::string s(endpoints);
+        size_t pos = 0;
+        while (pos <= s.size()) {
+            size_t sc = s.find(';', pos);
+            if (sc == std::string::npos) sc = s.size();
+            if (sc > pos) eps.push_back(s.substr(pos, sc - pos));
+            pos = sc + 1;
+        }
+        world_control().connect(world->rank(), world->size(), eps, 120000);
+        world->handler();  // collective: creates the handler's private RCCL communicator now
+    });
+}
+
+int ddl_control_connect_ranked(int rank, int size, const char *endpoints) {
+    return guarded([&] {
+        DDL_REQUIRE(endpoints, DDL_STATUS_INVALID_ARGUMENT, "null endpoints");
+        std::vector<std::string> eps;
+        std::string s(endpoints);
+        size_t pos = 0;
+        while (pos <= s.size()) {
+            size_t sc = s.find(';', pos);
+            if (sc == std::string::npos) sc = s.size();
+            if (sc > pos) eps.push_back(s.substr(pos, sc - pos));
+            pos = sc + 1;
+        }
+        world_control().connect(rank, size, eps, 120000);
+    });
+}
+
+int ddl_control_negotiate(const char *keys, char *out, size_t len) {
+    return guarded([&] {
+        DDL_REQUIRE(keys && out && len > 0, DDL_STATUS_INVALID_ARGUMENT, "bad negotiate args");
+        ControlChannel &ch = world_control();
+        DDL_REQUIRE(ch.connected(), DDL_STATUS_NOT_INITIALIZED, "control channel not connected");
+        std::vector<std::string> mine;
+        std::string s(keys);
+        size_t pos = 0;
+        while (pos < s.size()) {
+            size_t nl = s.find('\n', pos);
+            if (nl == std::string::npos) nl = s.size();
+            if (nl > pos) mine.push_back(s.substr(pos, nl - pos));
+            pos = nl + 1;
+        }
+        std::sort(mine.begin(), mine.end());
+        std::vector<std::string> agreed;
+        if (ch.rank() == 0) {
+            agreed = negotiate_root(ch, mine);
+            negotiate_root_finish(ch);
+        } else {
+            Token t;
+            ch.recv(t, -1);
+            agreed = negotiate_member(ch, t, [&](const std::vector<std::string> &proposed) {
+                std::vector<std::string> both;
+                for (const auto &k : proposed)
+                    if (std::binary_search(mine.begin(), mine.end(), k)) both.push_back(k);
+                return both;
+            });
+        }
+        std::string res;
+        for (const auto &k : agreed) res.append(k).append("\n");
+        DDL_REQUIRE(res.size() < len, DDL_STATUS_INVALID_ARGUMENT, "output buffer too small");
+        std::memcpy(out, res.c_str(), res.size() + 1);
+    });
+}
+
+int ddl_finalize(void) {
+    return guarded([&] {
+        Registry::get().clear();
+        world_control().close_all();
+    });
+}
+
+int ddl_is_initialized(void) { return Registry::get().initialized() ? 1 : 0; }
+
+int ddl_set_config(const char *key, long long value) {
+    return guarded([&] {
+        DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
+        std::string k(key);
+        Config &c = config();
+        if (k == "slice_bytes") c.slice_bytes = value;
+        else if (k == "rings") c.rings = value;
+        else if (k == "max_slices") c.max_slices = value;
+        else if (k == "fusion_threshold_bytes") {
+            DDL_REQUIRE(value > 0, DDL_STATUS_INVALID_ARGUMENT, "fusion threshold must be > 0");
+            c.fusion_threshold_bytes = value;
+        } else if (k == "log_level") c.log_level = value;
+        else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
+    });
+}
+
+long long ddl_get_config(const char *key) {
+    if (!key) return -1;
+    std::string k(key);
+    Config &c = config();
+    if (k == "slice_bytes") return c.slice_bytes;
+    if (k == "rings") return c.rings;
+    if (k == "max_slices") return c.max_slices;
+    if (k == "fusion_threshold_bytes") return c.fusion_threshold_bytes;
+    if (k == "log_level") return c.log_level;
+    return -1;
+}
+
+// ---- reference c_api.h surface (src/cpp/c_api.cc:11-65) ------------------------------------
+int communicator_rank(ddl_communicator_id id) {
+    int r = -1;
+    if (guarded([&] { r = Registry::get().find(id)->rank(); }) != DDL_STATUS_OK) return -1;
+    return r;
+}
+
+int communicator_size(ddl_communicator_id id) {
+    int s = -1;
+    if (guarded([&] { s = Registry::get().find(id)->size(); }) != DDL_STATUS_OK) return -1;
+    return s;
+}
+
+ddl_communicator_id world_communicator(void) {
+    ddl_communicator_id id = 0;
+    if (guarded([&] { id = Registry::get().world()->id(); }) != DDL_STATUS_OK) return 0;
+    return id;
+}
+
+ddl_communicator_id split_communicator(ddl_communicator_id id, int color, int key) {
+    ddl_communicator_id out = 0;
+    int st = guarded([&] {
+        auto c = Registry::get().find(id)->split(color, key);
+        Registry::get().add(c);
+        out = c->id();
+    });
+    return st == DDL_STATUS_OK ? out : 0;
+}
+
+void detach_communicator(ddl_communicator_id id) {
+    (void)guarded([&] { Registry::get().detach(id); });
+}
+
+void py_info(const char *s) { DDL_LOG(1, "[py]: " << (s ? s : "")); }
+void py_debug(const char *s) { DDL_LOG(2, "[py]: " << (s ? s : "")); }
+void py_error(const char *s) { DDL_LOG(0, "[py]: " << (s ? s : "")); }
+
+// ---- data plane ---------------------------------------------------------------------------
+int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,
+                  int op, void *hip_stream) {
+    return guarded([&] { Registry::get().find(id)->allreduce(send, recv, elements, dtype, op, as_stream(hip_stream)); });
+}
+
+int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,
+                          int op, void *hip_stream, int variant) {
+    return guarded([&] {
+        auto c = Registry::get().find(id);
+        if (variant == 0) {
+            c->allreduce(send, recv, elements, dtype, op, as_stream(hip_stream));
+            return;
+        }
+        DDL_REQUIRE(variant == 1, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
+        DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM");
+        DeviceGuard g(c->device());
+        if (c->size() == 1) {
+            if (send != recv) DDL_HIP(hipMemcpyAsync(recv, send, elements * dtype_size(dtype), hipMemcpyDeviceToDevice, as_stream(hip_stream)));
+            return;
+        }
+        ncclDataType_t t;
+        switch (dtype) {
+            case DDL_FLOAT: t = ncclFloat32; break;
+            case DDL_DOUBLE: t = ncclFloat64; break;
+            case DDL_INT32: t = ncclInt32; break;
+            case DDL_INT64: t = ncclInt64; break;
+            case DDL_UINT64: t = ncclUint64; break;
+            case DDL_HALF: t = ncclFloat16; break;
+            case DDL_BFLOAT16: t = ncclBfloat16; break;
+            default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
+        }
+        rccl_check(rccl().AllReduce(send, recv, elements, t, ncclSum, c->nccl(), as_stream(hip_stream)), "ncclAllReduce");
+    });
+}
+
+int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
+                         size_t elements, int dtype, int op, void *hip_stream, ddl_done_fn done,
+                         void *user) {
+    return guarded([&] {
+        DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
+        auto c = Registry::get().find(id);
+        DeviceGuard g(c->device());
+        Request r;
+        r.key = key;
+        r.in = in;
+        r.out = out;
+        r.n = elements;
+        r.dtype = dtype;
+        r.op = op;
+        r.done = done;
+        r.user = user;
+        DDL_HIP(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(r.ready, as_stream(hip_stream));
+        if (e != hipSuccess) {
+            (void)hipEventDestroy(r.ready);
+            DDL_HIP(e);
+        }
+        try {
+            c->handler().submit(r);
+        } catch (...) {
+            (void)hipEventDestroy(r.ready);
+            throw;
+        }
+    });
+}
+
+int ddl_kernel_timing(ddl_communicator_id id, int on) {
+    return guarded([&] {
+        auto c = Registry::get().find(id);
+        std::lock_guard<std::mutex> g(c->mutex());
+        c->executor().set_timing(on != 0);
+    });
+}
+
+int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes, double *ms) {
+    return guarded([&] {
+        DDL_REQUIRE(launches && bytes && ms, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        auto c = Registry::get().find(id);
+        std::lock_guard<std::mutex> g(c->mutex());
+        DeviceGuard dg(c->device());
+        KernelStats s = c->executor().collect_stats();
+        *launches = s.launches;
+        *bytes = s.bytes;
+        *ms = s.ms;
+    });
+}
+
+int ddl_wait_all(ddl_communicator_id id) {
+    return guarded([&] { Registry::get().find(id)->handler().wait_all(); });
+}
+
+// ---- kernels ------------------------------------------------------------------------------
+int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b, size_t elements,
+                            int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(variant >= 0 && variant <= 2, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
+        SegTable t;
+        t.count = 1;
+        t.a[0] = a;
+        t.b[0] = b;
+        t.out[0] = out;
+        t.n[0] = elements;
+        launch_sum2(t, dtype, as_stream(hip_stream), variant);
+    });
+}
+
+int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype, void *hip_stream) {
+    return ddl_reduce_sum2_variant(0, out, a, b, elements, dtype, hip_stream);
+}
+
+int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void *hip_stream) {
+    return ddl_reduce_sum2_variant(0, acc, acc, in, elements, dtype, hip_stream);
+}
+
+int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(count >= 0 && (count == 0 || (dst && srcs && bytes)), DDL_STATUS_INVALID_ARGUMENT, "bad pack args");
+        launch_pack(dst, srcs, bytes, count, as_stream(hip_stream));
+    });
+}
+
+int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int count, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(count >= 0 && (count == 0 || (src && dsts && bytes)), DDL_STATUS_INVALID_ARGUMENT, "bad unpack args");
+        launch_unpack(dsts, src, bytes, count, as_stream(hip_stream));
+    });
+}
+
+int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements,
+                             int dtype, int op, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM");
+        DDL_REQUIRE(sends && recvs, DDL_STATUS_INVALID_ARGUMENT, "null buffer arrays");
+        (void)current_device();
+        local_world(nranks).allreduce(sends, recvs, elements, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
+// ---- schedule introspection -----------------------------------------------------------------
+int ddl_ring_count(int nranks, int max_rings) {
+    if (nranks < 1) return 0;
+    return (int)rings_for(nranks, max_rings).size();
+}
+
+int ddl_ring_perm(int nranks, int max_rings, int ring, int *perm_out) {
+    return guarded([&] {
+        const auto &rings = rings_for(nranks, max_rings);
+        DDL_REQUIRE(ring >= 0 && ring < (int)rings.size() && perm_out, DDL_STATUS_INVALID_ARGUMENT, "bad ring " << ring);
+        for (int p = 0; p < nranks; ++p) perm_out[p] = rings[ring][p];
+    });
+}
+
+int ddl_chunk_range(size_t elements, int dtype, int nranks, int rings, int ring, int chunk, size_t *begin,
+                    size_t *end) {
+    return guarded([&] {
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es && nranks >= 1 && rings >= 1 && ring >= 0 && ring < rings && chunk >= 0 && chunk < nranks &&
+                        begin && end,
+                    DDL_STATUS_INVALID_ARGUMENT, "bad chunk query");
+        Range r = chunk_range(elements, es, nranks, rings, ring, chunk);
+        *begin = r.begin;
+        *end = r.end;
+    });
+}
+
+int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slices) {
+    return guarded([&] {
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es && nranks >= 1 && rings && slices, DDL_STATUS_INVALID_ARGUMENT, "bad shape query");
+        size_t stride;
+        ring_shape(elements, es, nranks, config().ring(), rings, slices, &stride);
+    });
+}
+
+int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out, size_t max_ops,
+                     size_t *nops) {
+    return guarded([&] {
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es && nranks >= 1 && rank >= 0 && rank < nranks && nops, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad program query");
+        // symbolic base addresses: every pointer of the program decodes to (buffer, offset)
+        char *const bases[3] = {(char *)(uintptr_t(1) << 44), (char *)(uintptr_t(2) << 44), (char *)(uintptr_t(3) << 44)};
+        auto decode = [&](const void *p, long long *buf, long long *off) {
+            uintptr_t v = reinterpret_cast<uintptr_t>(p);
+            *buf = (long long)(v >> 44) - 1;
+            *off = (long long)((v & ((uintptr_t(1) << 44) - 1)) / es);
+        };
+        RingProgram prog;
+        build_program(prog, rank, nranks, bases[0], bases[1], bases[2], elements, dtype, config().ring());
+        std::vector<long long> rows;
+        for (size_t t = 0; t < prog.ticks.size(); ++t) {
+            const Tick &tk = prog.ticks[t];
+            for (const P2POp &op : tk.ops) {
+                long long buf, off;
+                decode(op.ptr, &buf, &off);
+                long long row[8] = {(long long)t, op.send ? 0 : 1, op.peer, op.tag, buf, off, (long long)(op.bytes / es), tk.wait_reduce};
+                rows.insert(rows.end(), row, row + 8);
+            }
+            for (int sgi = 0; sgi < tk.reduce.count; ++sgi) {
+                long long obuf, ooff, abuf, aoff, bbuf, boff;
+                decode(tk.reduce.out[sgi], &obuf, &ooff);
+                decode(tk.reduce.a[sgi], &abuf, &aoff);
+                decode(tk.reduce.b[sgi], &bbuf, &boff);
+                DDL_REQUIRE(abuf == 0 && aoff == ooff && bbuf == 2 && obuf == 1, DDL_STATUS_ERROR_UNKNOWN,
+                            "unexpected reduce operands");
+                long long row[8] = {(long long)t, 2, -1, sgi, obuf, ooff, (long long)tk.reduce.n[sgi], boff};
+                rows.insert(rows.end(), row, row + 8);
+            }
+        }
+        *nops = rows.size() / 8;
+        DDL_REQUIRE(*nops <= max_ops && (rows.empty() || ops_out), DDL_STATUS_INVALID_ARGUMENT,
+                    "op buffer too small: need " << *nops);
+        std::copy(rows.begin(), rows.end(), ops_out);
+    });
+}
+
+int ddl_make_plans(const size_t *elements, const size_t *esizes, size_t count, size_t limit, size_t *plans_out,
+                   size_t max_plans, size_t *nplans) {
+    return guarded([&] {
+        DDL_REQUIRE(nplans && (count == 0 || (elements && esizes)), DDL_STATUS_INVALID_ARGUMENT, "bad plan args");
+        std::vector<size_t> e(elements, elements + count), s(esizes, esizes + count);
+        auto plans = make_plans(e, s, limit);
+        *nplans = plans.size();
+        DDL_REQUIRE(plans.size() <= max_plans && (plans.empty() || plans_out), DDL_STATUS_INVALID_ARGUMENT,
+                    "plan buffer too small: need " << plans.size());
+        for (size_t i = 0; i < plans.size(); ++i) {
+            plans_out[4 * i] = plans[i].req_begin;
+            plans_out[4 * i + 1] = plans[i].elem_begin;
+            plans_out[4 * i + 2] = plans[i].req_end;
+            plans_out[4 * i + 3] = plans[i].elem_end;
+        }
+    });
+}
+
+}  // extern "C"

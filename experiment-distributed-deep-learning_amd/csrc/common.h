@@ -1,0 +1,110 @@
+// common.h — shared definitions of the MI355X allreduce engine (host side).
+//
+// dtype numbers and status codes follow the C-ABI (include/ddl_amd.h), which mirrors the
+// reference's tensorflow::DataType use (src/cpp/def.h:10) and StatusCode (def.h:70-74).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <sstream>
+
+#include "ddl_amd.h"
+
+namespace ddl {
+
+inline size_t dtype_size(int dt) {
+    switch (dt) {
+        case DDL_FLOAT: case DDL_INT32: return 4;
+        case DDL_DOUBLE: case DDL_INT64: case DDL_UINT64: return 8;
+        case DDL_HALF: case DDL_BFLOAT16: return 2;
+        default: return 0;
+    }
+}
+
+inline const char *dtype_name(int dt) {
+    switch (dt) {
+        case DDL_FLOAT: return "float32";
+        case DDL_DOUBLE: return "float64";
+        case DDL_INT32: return "int32";
+        case DDL_INT64: return "int64";
+        case DDL_UINT64: return "uint64";
+        case DDL_HALF: return "float16";
+        case DDL_BFLOAT16: return "bfloat16";
+        default: return "unsupported";
+    }
+}
+
+// Thread-local description of the last failure (ddl_last_error).
+void set_error(const std::string &msg);
+const char *last_error();
+
+// Error carried inside the library; converted to a status at the C-ABI (no exception
+// crosses the boundary).
+struct Error {
+    int status;
+    std::string msg;
+};
+
+[[noreturn]] inline void fail(int status, const std::string &msg) { throw Error{status, msg}; }
+
+#define DDL_HIP(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            std::ostringstream _os;                                                         \
+            _os << #expr << " failed: " << hipGetErrorString(_e) << " (" << __FILE__ << ":" \
+                << __LINE__ << ")";                                                         \
+            ::ddl::fail(DDL_STATUS_HIP_ERROR, _os.str());                                   \
+        }                                                                                   \
+    } while (0)
+
+#define DDL_REQUIRE(cond, status, msg)                    \
+    do {                                                  \
+        if (!(cond)) {                                    \
+            std::ostringstream _os;                       \
+            _os << msg;                                   \
+            ::ddl::fail((status), _os.str());             \
+        }                                                 \
+    } while (0)
+
+// Logging (the reference logs per rank to log-<rank>.txt, GlobalLog.cc:17-49; here
+// stderr, gated by the "log_level" config: 0 errors, 1 info, 2 debug).
+int log_level();
+void log_line(int level, const std::string &msg);
+
+#define DDL_LOG(level, msg)                                     \
+    do {                                                        \
+        if (::ddl::log_level() >= (level)) {                    \
+            std::ostringstream _os;                             \
+            _os << msg;                                         \
+            ::ddl::log_line((level), _os.str());                \
+        }                                                       \
+    } while (0)
+
+// ---- kernels (reduce_kernels.hip) ----------------------------------------------------
+constexpr int kMaxSegments = 8;
+
+// Up to kMaxSegments independent out = a + b problems in one launch (one per ring).
+struct SegTable {
+    const void *a[kMaxSegments];
+    const void *b[kMaxSegments];
+    void *out[kMaxSegments];
+    uint64_t n[kMaxSegments];
+    int count;
+};
+
+enum ReduceVariant { kRegStream = 0, kLdsStage = 1, kNonTemporal = 2 };
+
+// out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.
+void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant = kRegStream);
+// Gather/scatter segments into/out of a contiguous fusion buffer.
+void launch_pack(void *dst, const void *const *srcs, const size_t *bytes, int count,
+                 hipStream_t stream);
+void launch_unpack(void *const *dsts, const void *src, const size_t *bytes, int count,
+                   hipStream_t stream);
+int device_cu_count();
+
+}  // namespace ddl

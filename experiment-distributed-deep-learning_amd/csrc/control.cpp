@@ -1,0 +1,195 @@
+// control.cpp — see control.h.
+#include "control.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "common.h"
+
+namespace ddl {
+
+namespace {
+
+void write_all(int fd, const void *p, size_t n) {
+    const char *c = static_cast<const char *>(p);
+    while (n) {
+        ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
+        if (w < 0 && errno == EINTR) continue;
+        DDL_REQUIRE(w > 0, DDL_STATUS_COMM_ERROR, "control channel send failed: " << std::strerror(errno));
+        c += w;
+        n -= (size_t)w;
+    }
+}
+
+void read_all(int fd, void *p, size_t n) {
+    char *c = static_cast<char *>(p);
+    while (n) {
+        ssize_t r = ::recv(fd, c, n, 0);
+        if (r < 0 && errno == EINTR) continue;
+        DDL_REQUIRE(r > 0, DDL_STATUS_COMM_ERROR,
+                    "control channel closed by peer" << (r < 0 ? std::string(": ") + std::strerror(errno) : ""));
+        c += r;
+        n -= (size_t)r;
+    }
+}
+
+void split_endpoint(const std::string &ep, std::string &host, int &port) {
+    size_t c = ep.rfind(':');
+    DDL_REQUIRE(c != std::string::npos, DDL_STATUS_INVALID_ARGUMENT, "bad endpoint '" << ep << "'");
+    host = ep.substr(0, c);
+    port = std::atoi(ep.c_str() + c + 1);
+}
+
+void tune(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+}
+
+}  // namespace
+
+ControlChannel::~ControlChannel() { close_all(); }
+
+void ControlChannel::close_all() {
+    for (int *fd : {&listen_fd_, &send_fd_, &recv_fd_}) {
+        if (*fd >= 0) ::close(*fd);
+        *fd = -1;
+    }
+}
+
+std::string ControlChannel::listen() {
+    DDL_REQUIRE(listen_fd_ < 0, DDL_STATUS_INVALID_ARGUMENT, "control channel already listening");
+    // The token ring is a single-node, same-host channel: it binds to loopback. A deployment
+    // that spans hosts opts in by naming the interface address in $DDL_CONTROL_HOST.
+    const char *env = std::getenv("DDL_CONTROL_HOST");
+    const std::string host = env && *env ? env : "127.0.0.1";
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = 0;
+    DDL_REQUIRE(inet_pton(AF_INET, host.c_str(), &a.sin_addr) == 1, DDL_STATUS_INVALID_ARGUMENT,
+                "DDL_CONTROL_HOST '" << host << "' is not an IPv4 address");
+    listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+    DDL_REQUIRE(listen_fd_ >= 0, DDL_STATUS_COMM_ERROR, "socket: " << std::strerror(errno));
+    DDL_REQUIRE(::bind(listen_fd_, (sockaddr *)&a, sizeof a) == 0, DDL_STATUS_COMM_ERROR,
+                "bind " << host << ": " << std::strerror(errno));
+    DDL_REQUIRE(::listen(listen_fd_, 16) == 0, DDL_STATUS_COMM_ERROR, "listen: " << std::strerror(errno));
+    socklen_t len = sizeof a;
+    getsockname(listen_fd_, (sockaddr *)&a, &len);
+    return host + ":" + std::to_string(ntohs(a.sin_port));
+}
+
+void ControlChannel::connect(int rank, int size, const std::vector<std::string> &eps, int timeout_ms) {
+    DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && (int)eps.size() == size,
+                DDL_STATUS_INVALID_ARGUMENT, "control connect: " << eps.size() << " endpoints for size " << size);
+    rank_ = rank;
+    size_ = size;
+    if (size == 1) return;
+    DDL_REQUIRE(listen_fd_ >= 0, DDL_STATUS_INVALID_ARGUMENT, "ddl_control_listen must come first");
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    // 1) connect to the successor (its listener may not be accepting yet: retry)
+    std::string host;
+    int port = 0;
+    split_endpoint(eps[(rank + 1) % size], host, port);
+    for (;;) {
+        int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        DDL_REQUIRE(fd >= 0, DDL_STATUS_COMM_ERROR, "socket: " << std::strerror(errno));
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons((uint16_t)port);
+        DDL_REQUIRE(inet_pton(AF_INET, host.c_str(), &a.sin_addr) == 1, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad control host '" << host << "'");
+        if (::connect(fd, (sockaddr *)&a, sizeof a) == 0) {
+            tune(fd);
+            int32_t me = rank;
+            write_all(fd, &me, sizeof me);
+            send_fd_ = fd;
+            break;
+        }
+        ::close(fd);
+        DDL_REQUIRE(std::chrono::steady_clock::now() < deadline, DDL_STATUS_COMM_ERROR,
+                    "control connect to " << eps[(rank + 1) % size] << " timed out");
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    // 2) accept the predecessor (a connection announcing any other rank is dropped)
+    const int pred = (rank + size - 1) % size;
+    while (recv_fd_ < 0) {
+        pollfd p{listen_fd_, POLLIN, 0};
+        int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                       deadline - std::chrono::steady_clock::now()).count();
+        DDL_REQUIRE(left > 0, DDL_STATUS_COMM_ERROR, "control accept from rank " << pred << " timed out");
+        if (::poll(&p, 1, left) <= 0) continue;
+        int fd = ::accept(listen_fd_, nullptr, nullptr);
+        if (fd < 0) continue;
+        int32_t who = -1;
+        read_all(fd, &who, sizeof who);
+        if (who == pred) {
+            tune(fd);
+            recv_fd_ = fd;
+        } else {
+            ::close(fd);
+        }
+    }
+    // the ring is complete: no further connections are accepted
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+}
+
+void ControlChannel::send(const Token &t) {
+    unsigned char hdr[10];
+    uint64_t len = t.msg.size();
+    hdr[0] = t.type;
+    hdr[1] = t.request;
+    std::memcpy(hdr + 2, &len, 8);  // host byte order, as the reference's MPI_Pack of size_t
+    write_all(send_fd_, hdr, sizeof hdr);
+    if (len) write_all(send_fd_, t.msg.data(), len);
+}
+
+bool ControlChannel::recv(Token &t, int timeout_ms) {
+    if (timeout_ms >= 0) {
+        pollfd p{recv_fd_, POLLIN, 0};
+        int r = ::poll(&p, 1, timeout_ms);
+        if (r == 0) return false;
+        DDL_REQUIRE(r > 0, DDL_STATUS_COMM_ERROR, "control poll: " << std::strerror(errno));
+    }
+    unsigned char hdr[10];
+    read_all(recv_fd_, hdr, sizeof hdr);
+    uint64_t len;
+    std::memcpy(&len, hdr + 2, 8);
+    DDL_REQUIRE(len < (1ull << 32), DDL_STATUS_COMM_ERROR, "control token too long: " << len);
+    t.type = hdr[0];
+    t.request = hdr[1];
+    t.msg.assign(len, '\0');
+    if (len) read_all(recv_fd_, &t.msg[0], len);
+    return true;
+}
+
+std::string encode_keys(const std::vector<std::string> &keys) {
+    std::string s;
+    for (const auto &k : keys) s.append("Allreduce::").append(k).append("\n");
+    return s;
+}
+
+std::vector<std::string> decode_keys(const std::string &msg) {
+    std::vector<std::string> keys;
+    size_t pos = 0;
+    while (pos < msg.size()) {
+        size_t nl = msg.find('\n', pos);
+        if (nl == std::string::npos) nl = msg.size();
+        std::string item = msg.substr(pos, nl - pos);
+        size_t sep = item.find("::");
+        keys.push_back(sep == std::string::npos ? item : item.substr(sep + 2));
+        pos = nl + 1;
+    }
+    return keys;
+}
+
+}  // namespace ddl

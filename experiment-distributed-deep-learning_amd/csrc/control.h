@@ -1,0 +1,57 @@
+// control.h — host control channel: a ring of TCP links carrying negotiation tokens.
+//
+// Replaces the reference's token transport over MPI point-to-point
+// (communicate/tensor/collective/controller/rtc/mpi/MPIRingTokenCommunication.cc:29-102):
+// every rank sends to rank+1 and receives from rank-1; a token on the wire is the same
+// packed header the reference sends with MPI_Pack — {u8 type, u8 request type, u64 length}
+// (10 bytes, :25,44-53) — followed by `length` bytes of key list.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ddl {
+
+// Token types / request types: reference rtc/Token.h:20-33.
+enum TokenType : uint8_t { TOKEN_READY = 0, TOKEN_SYNC = 1, TOKEN_COMMUNICATE = 2, TOKEN_SHUT_DOWN = 3 };
+enum TokenRequest : uint8_t { TOKEN_REQUEST_SHUTDOWN = 0, TOKEN_REQUEST_ALLREDUCE = 1 };
+
+struct Token {
+    uint8_t type = TOKEN_READY;
+    uint8_t request = TOKEN_REQUEST_ALLREDUCE;
+    std::string msg;
+};
+
+class ControlChannel {
+public:
+    ControlChannel() = default;
+    ~ControlChannel();
+    ControlChannel(const ControlChannel &) = delete;
+    ControlChannel &operator=(const ControlChannel &) = delete;
+
+    // Opens the listening socket; returns "host:port" (host from $DDL_CONTROL_HOST, default
+    // 127.0.0.1 — one node).
+    std::string listen();
+    // Connects to rank+1's endpoint and accepts rank-1's connection.
+    void connect(int rank, int size, const std::vector<std::string> &endpoints, int timeout_ms);
+    bool connected() const { return send_fd_ >= 0 && recv_fd_ >= 0; }
+
+    void send(const Token &t);
+    // Blocks until a token arrives, or returns false after timeout_ms (< 0: forever).
+    bool recv(Token &t, int timeout_ms);
+    int rank() const { return rank_; }
+    int size() const { return size_; }
+    void close_all();
+
+private:
+    int listen_fd_ = -1, send_fd_ = -1, recv_fd_ = -1;
+    int rank_ = 0, size_ = 1;
+};
+
+// "Allreduce::<key>\n" per key — the reference's token message format
+// (RingTokenCommunicateHandler.cc:10-11, 140-147, 412-437).
+std::string encode_keys(const std::vector<std::string> &keys);
+std::vector<std::string> decode_keys(const std::string &msg);
+
+}  // namespace ddl

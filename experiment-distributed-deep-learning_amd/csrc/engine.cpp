@@ -1,0 +1,170 @@
+// engine.cpp — communicators, registry, config, logging, errors.
+#include "engine.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "handler.h"
+
+namespace ddl {
+
+// ---- errors / logging --------------------------------------------------------------------
+namespace {
+thread_local std::string t_last_error;
+}
+
+void set_error(const std::string &msg) { t_last_error = msg; }
+const char *last_error() { return t_last_error.c_str(); }
+
+Config &config() {
+    static Config *c = [] {
+        Config *cfg = new Config();
+        if (const char *e = std::getenv("DDL_SLICE_BYTES")) cfg->slice_bytes = std::atoll(e);
+        if (const char *e = std::getenv("DDL_RINGS")) cfg->rings = std::atoll(e);
+        if (const char *e = std::getenv("DDL_MAX_SLICES")) cfg->max_slices = std::atoll(e);
+        if (const char *e = std::getenv("DDL_FUSION_THRESHOLD")) cfg->fusion_threshold_bytes = std::atoll(e);
+        if (const char *e = std::getenv("DDL_LOG_LEVEL")) cfg->log_level = std::atoll(e);
+        return cfg;
+    }();
+    return *c;
+}
+
+int log_level() { return (int)config().log_level.load(); }
+
+void log_line(int level, const std::string &msg) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    const char *tag = level <= 0 ? "ERROR" : (level == 1 ? "INFO" : "DEBUG");
+    std::fprintf(stderr, "[ddl %s tid=%zu] %s\n", tag,
+                 (size_t)std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000, msg.c_str());
+}
+
+// ---- device guard ---------------------------------------------------------------------------
+DeviceGuard::DeviceGuard(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    if (prev_ != device) DDL_HIP(hipSetDevice(device));
+}
+DeviceGuard::~DeviceGuard() {
+    int cur = -1;
+    if (prev_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev_) (void)hipSetDevice(prev_);
+}
+
+// ---- communicator -----------------------------------------------------------------------------
+Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl)
+    : rank_(rank), size_(size), device_(device), nccl_(nccl) {
+    DeviceGuard g(device_);
+    std::unique_ptr<Transport> t;
+    if (size_ > 1) t.reset(new RcclTransport(nccl_));
+    exec_.reset(new RingExecutor(rank_, size_, device_, std::move(t)));
+}
+
+Communicator::~Communicator() {
+    handler_.reset();
+    exec_.reset();
+    if (nccl_) (void)rccl().CommDestroy(nccl_);
+}
+
+void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream) {
+    DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported (op " << op << ")");
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    exec_->allreduce(send, recv, n, dtype, stream, config().ring());
+}
+
+std::shared_ptr<Communicator> Communicator::split(int color, int key) {
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    if (size_ == 1) return std::make_shared<Communicator>(0, 1, device_, nullptr);
+    ncclComm_t nc = nullptr;
+    rccl_check(rccl().CommSplit(nccl_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr),
+               "ncclCommSplit");
+    DDL_REQUIRE(nc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
+    int r = 0, s = 0;
+    rccl_check(rccl().CommCount(nc, &s), "ncclCommCount");
+    rccl_check(rccl().CommUserRank(nc, &r), "ncclCommUserRank");
+    return std::make_shared<Communicator>(r, s, device_, nc);
+}
+
+RequestHandler &Communicator::handler() {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    if (!handler_) handler_.reset(new RequestHandler(this));
+    return *handler_;
+}
+
+// ---- registry ------------------------------------------------------------------------------
+Registry &Registry::get() {
+    static Registry *r = new Registry();  // leaked on purpose: no static-destruction order issues
+    return *r;
+}
+
+void Registry::add(const std::shared_ptr<Communicator> &c) {
+    std::lock_guard<std::mutex> g(mu_);
+    comms_[c->id()] = c;
+}
+
+std::shared_ptr<Communicator> Registry::find(long long id) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = comms_.find(id);
+    DDL_REQUIRE(it != comms_.end(), DDL_STATUS_INVALID_ARGUMENT, "unknown communicator id " << id);
+    return it->second;
+}
+
+void Registry::detach(long long id) {
+    std::shared_ptr<Communicator> keep;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = comms_.find(id);
+        if (it == comms_.end()) return;
+        if (world_ && world_->id() == id) return;  // the world stays until ddl_finalize
+        keep = it->second;
+        comms_.erase(it);
+    }
+}
+
+std::shared_ptr<Communicator> Registry::world() {
+    std::lock_guard<std::mutex> g(mu_);
+    DDL_REQUIRE(world_ != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_init has not been called");
+    return world_;
+}
+
+void Registry::set_world(const std::shared_ptr<Communicator> &c) {
+    std::lock_guard<std::mutex> g(mu_);
+    DDL_REQUIRE(world_ == nullptr, DDL_STATUS_INVALID_ARGUMENT, "already initialized");
+    world_ = c;
+    comms_[c->id()] = c;
+}
+
+void Registry::clear() {
+    std::map<long long, std::shared_ptr<Communicator>> comms;
+    std::shared_ptr<Communicator> w;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        comms.swap(comms_);
+        w.swap(world_);
+    }
+    comms.clear();
+    w.reset();
+}
+
+bool Registry::initialized() {
+    std::lock_guard<std::mutex> g(mu_);
+    return world_ != nullptr;
+}
+
+LocalWorld &local_world(int nranks) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::unique_ptr<LocalWorld>> worlds;
+    int dev = 0;
+    DDL_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(mu);
+    auto key = std::make_pair(nranks, dev);
+    auto it = worlds.find(key);
+    if (it == worlds.end()) it = worlds.emplace(key, std::unique_ptr<LocalWorld>(new LocalWorld(nranks, dev))).first;
+    return *it->second;
+}
+
+}  // namespace ddl

@@ -1,0 +1,96 @@
+// engine.h — communicators, configuration and the process-wide registry.
+//
+// Mirrors the reference's Global singleton wiring (src/cpp/global/Global.cc:10-34,
+// initialize.cc:25-112) and its Communicator (communicate/backend/Communicator.h:18-118),
+// MI355X-first: one process per GPU, one RCCL communicator per Communicator, the id is the
+// address of the Communicator object (the reference uses the MPI_Comm* address,
+// MPICommunicator.cc:107-109).
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "executor.h"
+
+namespace ddl {
+
+class RequestHandler;  // keyed requests (handler.h)
+
+struct Config {
+    std::atomic<long long> slice_bytes{2ll << 20};
+    std::atomic<long long> rings{kMaxRings};
+    std::atomic<long long> max_slices{8};
+    // fusion plan cap; the reference uses MAX_MPI_BUFFER_SIZE = 2^31 - 1 (MPIBackend.h:12)
+    std::atomic<long long> fusion_threshold_bytes{(1ll << 31) - 1};
+    std::atomic<long long> log_level{0};
+    RingConfig ring() const {
+        RingConfig c;
+        c.rings = (int)rings.load();
+        c.slice_bytes = (size_t)slice_bytes.load();
+        c.max_slices = (int)max_slices.load();
+        return c;
+    }
+};
+Config &config();
+
+class Communicator : public std::enable_shared_from_this<Communicator> {
+public:
+    Communicator(int rank, int size, int device, ncclComm_t nccl);
+    ~Communicator();
+
+    long long id() const { return reinterpret_cast<long long>(this); }
+    int rank() const { return rank_; }
+    int size() const { return size_; }
+    int device() const { return device_; }
+    ncclComm_t nccl() const { return nccl_; }
+
+    // Communicator::allreduce (reference Communicator.h:45-48), device buffers, stream-ordered.
+    void allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream);
+    std::shared_ptr<Communicator> split(int color, int key);
+
+    RequestHandler &handler();
+    RingExecutor &executor() { return *exec_; }
+    std::mutex &mutex() { return mu_; }
+
+private:
+    int rank_, size_, device_;
+    ncclComm_t nccl_;
+    std::mutex mu_;  // one collective at a time per communicator (RCCL ordering)
+    std::unique_ptr<RingExecutor> exec_;
+    std::unique_ptr<RequestHandler> handler_;
+    std::mutex handler_mu_;
+};
+
+class Registry {
+public:
+    static Registry &get();
+    void add(const std::shared_ptr<Communicator> &c);
+    std::shared_ptr<Communicator> find(long long id);  // throws if unknown
+    void detach(long long id);
+    std::shared_ptr<Communicator> world();              // throws if not initialized
+    void set_world(const std::shared_ptr<Communicator> &c);
+    void clear();
+    bool initialized();
+
+private:
+    std::mutex mu_;
+    std::map<long long, std::shared_ptr<Communicator>> comms_;
+    std::shared_ptr<Communicator> world_;
+};
+
+// Current-device guard: sets `device` for the scope, restores the previous one.
+class DeviceGuard {
+public:
+    explicit DeviceGuard(int device);
+    ~DeviceGuard();
+
+private:
+    int prev_ = -1;
+};
+
+LocalWorld &local_world(int nranks);
+
+}  // namespace ddl

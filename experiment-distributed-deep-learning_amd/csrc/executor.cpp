@@ -1,0 +1,234 @@
+// executor.cpp — see executor.h.
+#include "executor.h"
+
+namespace ddl {
+
+void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
+    if (ops.empty()) return;
+    const RcclApi &api = rccl();
+    rccl_check(api.GroupStart(), "ncclGroupStart");
+    ncclResult_t first_err = ncclSuccess;
+    for (const P2POp &op : ops) {
+        ncclResult_t r = op.send ? api.Send(op.ptr, op.bytes, ncclInt8, op.peer, comm_, stream)
+                                 : api.Recv(op.ptr, op.bytes, ncclInt8, op.peer, comm_, stream);
+        if (r != ncclSuccess && first_err == ncclSuccess) first_err = r;
+    }
+    ncclResult_t e = api.GroupEnd();
+    rccl_check(first_err, "ncclSend/ncclRecv");
+    rccl_check(e, "ncclGroupEnd");
+}
+
+RankResources::RankResources(int dev) : device(dev) {
+    DDL_HIP(hipStreamCreateWithFlags(&comm, hipStreamNonBlocking));
+    DDL_HIP(hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));
+    DDL_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    DDL_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+}
+
+RankResources::~RankResources() {
+    // best effort: called at teardown, errors are ignored
+    for (auto *v : {&comm_ev, &red_ev, &pre_ev, &post_ev})
+        for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+    if (comm) (void)hipStreamDestroy(comm);
+    if (compute) (void)hipStreamDestroy(compute);
+    if (staging_) (void)hipFree(staging_);
+}
+
+void RankResources::ensure_events(size_t ticks) {
+    for (auto *v : {&comm_ev, &red_ev, &pre_ev, &post_ev}) {
+        while (v->size() < ticks) {
+            hipEvent_t e;
+            DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            v->push_back(e);
+        }
+    }
+}
+
+void *RankResources::ensure_staging(size_t bytes) {
+    if (bytes > staging_bytes_) {
+        if (staging_) {
+            // a previous call may still read it on the device
+            DDL_HIP(hipStreamSynchronize(comm));
+            DDL_HIP(hipStreamSynchronize(compute));
+            DDL_HIP(hipFree(staging_));
+            staging_ = nullptr;
+        }
+        size_t sz = bytes + bytes / 4;  // grow with headroom (the reference grows x1.5, MPIRTC.cc:13)
+        DDL_HIP(hipMalloc(&staging_, sz));
+        staging_bytes_ = sz;
+    }
+    return staging_;
+}
+
+int last_reduce_at_or_before(const RingProgram &p, int w) {
+    for (int t = w; t >= 0; --t)
+        if (p.ticks[t].has_reduce) return t;
+    return -1;
+}
+
+RingExecutor::RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport)
+    : rank_(rank), size_(size), transport_(std::move(transport)), res_(device) {}
+
+RingExecutor::~RingExecutor() {
+    for (auto *v : {&timed_, &free_pairs_})
+        for (auto &p : *v) {
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+}
+
+void RingExecutor::set_timing(bool on) { timing_ = on; }
+
+KernelStats RingExecutor::collect_stats() {
+    KernelStats s;
+    for (size_t i = 0; i < timed_.size(); ++i) {
+        DDL_HIP(hipEventSynchronize(timed_[i].second));
+        float ms = 0;
+        DDL_HIP(hipEventElapsedTime(&ms, timed_[i].first, timed_[i].second));
+        s.ms += ms;
+        s.bytes += timed_bytes_[i];
+        s.launches += 1;
+        free_pairs_.push_back(timed_[i]);
+    }
+    timed_.clear();
+    timed_bytes_.clear();
+    return s;
+}
+
+void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hipStream_t user,
+                             const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (n == 0) return;
+    if (size_ == 1) {  // P = 1: out = in (the reference never completes here)
+        if (in != out) DDL_HIP(hipMemcpyAsync(out, in, n * es, hipMemcpyDeviceToDevice, user));
+        return;
+    }
+    int R, K;
+    size_t stride;
+    ring_shape(n, es, size_, cfg, &R, &K, &stride);
+    void *staging = res_.ensure_staging((size_t)R * stride * es);
+    build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
+    res_.ensure_events(prog_.ticks.size());
+
+    DDL_HIP(hipEventRecord(res_.fork_ev, user));
+    DDL_HIP(hipStreamWaitEvent(res_.comm, res_.fork_ev, 0));
+    DDL_HIP(hipStreamWaitEvent(res_.compute, res_.fork_ev, 0));
+    for (size_t t = 0; t < prog_.ticks.size(); ++t) {
+        const Tick &tk = prog_.ticks[t];
+        if (tk.wait_reduce >= 0) {
+            int w = last_reduce_at_or_before(prog_, tk.wait_reduce);
+            if (w >= 0) DDL_HIP(hipStreamWaitEvent(res_.comm, res_.red_ev[w], 0));
+        }
+        transport_->group(tk.ops, res_.comm);
+        if (tk.has_reduce) {
+            DDL_HIP(hipEventRecord(res_.comm_ev[t], res_.comm));
+            DDL_HIP(hipStreamWaitEvent(res_.compute, res_.comm_ev[t], 0));
+            std::pair<hipEvent_t, hipEvent_t> tp{nullptr, nullptr};
+            if (timing_) {
+                if (free_pairs_.empty()) {
+                    DDL_HIP(hipEventCreate(&tp.first));
+                    DDL_HIP(hipEventCreate(&tp.second));
+                } else {
+                    tp = free_pairs_.back();
+                    free_pairs_.pop_back();
+                }
+                DDL_HIP(hipEventRecord(tp.first, res_.compute));
+            }
+            launch_sum2(tk.reduce, dtype, res_.compute);
+            if (timing_) {
+                DDL_HIP(hipEventRecord(tp.second, res_.compute));
+                double elems = 0;
+                for (int sgi = 0; sgi < tk.reduce.count; ++sgi) elems += (double)tk.reduce.n[sgi];
+                timed_.push_back(tp);
+                timed_bytes_.push_back(3.0 * elems * (double)es);
+            }
+            DDL_HIP(hipEventRecord(res_.red_ev[t], res_.compute));
+        }
+    }
+    // the allgather waited for the last reduce, so the comm stream's tail covers everything
+    DDL_HIP(hipEventRecord(res_.join_ev, res_.comm));
+    DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
+}
+
+LocalWorld::LocalWorld(int nranks, int device) : P_(nranks) {
+    for (int r = 0; r < nranks; ++r) res_.emplace_back(new RankResources(device));
+    progs_.resize(nranks);
+}
+
+void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, int dtype,
+                           hipStream_t user, const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (n == 0) return;
+    if (P_ == 1) {
+        if (in[0] != out[0]) DDL_HIP(hipMemcpyAsync(out[0], in[0], n * es, hipMemcpyDeviceToDevice, user));
+        return;
+    }
+    int R, K;
+    size_t stride;
+    ring_shape(n, es, P_, cfg, &R, &K, &stride);
+    for (int r = 0; r < P_; ++r) {
+        void *st = res_[r]->ensure_staging((size_t)R * stride * es);
+        build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
+        res_[r]->ensure_events(progs_[r].ticks.size());
+    }
+    hipEvent_t fork = res_[0]->fork_ev;
+    DDL_HIP(hipEventRecord(fork, user));
+    for (int r = 0; r < P_; ++r) {
+        DDL_HIP(hipStreamWaitEvent(res_[r]->comm, fork, 0));
+        DDL_HIP(hipStreamWaitEvent(res_[r]->compute, fork, 0));
+    }
+    const size_t T = progs_[0].ticks.size();
+    for (size_t t = 0; t < T; ++t) {
+        // 1) each rank's comm stream reaches the tick (after its reduce dependency)
+        for (int r = 0; r < P_; ++r) {
+            const Tick &tk = progs_[r].ticks[t];
+            RankResources &rr = *res_[r];
+            if (tk.wait_reduce >= 0) {
+                int w = last_reduce_at_or_before(progs_[r], tk.wait_reduce);
+                if (w >= 0) DDL_HIP(hipStreamWaitEvent(rr.comm, rr.red_ev[w], 0));
+            }
+            DDL_HIP(hipEventRecord(rr.pre_ev[t], rr.comm));
+        }
+        // 2) receives: copy from the matching send of the peer, once the peer reached the tick
+        for (int r = 0; r < P_; ++r) {
+            RankResources &rr = *res_[r];
+            for (const P2POp &op : progs_[r].ticks[t].ops) {
+                if (op.send) continue;
+                const P2POp *match = nullptr;
+                for (const P2POp &o : progs_[op.peer].ticks[t].ops)
+                    if (o.send && o.peer == r && o.tag == op.tag) { match = &o; break; }
+                DDL_REQUIRE(match && match->bytes == op.bytes, DDL_STATUS_ERROR_UNKNOWN,
+                            "local ring: unmatched recv rank " << r << " tick " << t << " ring " << op.tag);
+                DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->pre_ev[t], 0));
+                DDL_HIP(hipMemcpyAsync(op.ptr, match->ptr, op.bytes, hipMemcpyDeviceToDevice, rr.comm));
+            }
+            DDL_HIP(hipEventRecord(rr.post_ev[t], rr.comm));
+        }
+        // 3) a group completes for the sender only once its receivers have the data
+        for (int r = 0; r < P_; ++r) {
+            RankResources &rr = *res_[r];
+            for (const P2POp &op : progs_[r].ticks[t].ops)
+                if (op.send) DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->post_ev[t], 0));
+        }
+        // 4) reduce of the received slices
+        for (int r = 0; r < P_; ++r) {
+            const Tick &tk = progs_[r].ticks[t];
+            RankResources &rr = *res_[r];
+            if (!tk.has_reduce) continue;
+            DDL_HIP(hipEventRecord(rr.comm_ev[t], rr.comm));
+            DDL_HIP(hipStreamWaitEvent(rr.compute, rr.comm_ev[t], 0));
+            launch_sum2(tk.reduce, dtype, rr.compute);
+            DDL_HIP(hipEventRecord(rr.red_ev[t], rr.compute));
+        }
+    }
+    for (int r = 0; r < P_; ++r) {
+        DDL_HIP(hipEventRecord(res_[r]->join_ev, res_[r]->comm));
+        DDL_HIP(hipStreamWaitEvent(user, res_[r]->join_ev, 0));
+    }
+}
+
+}  // namespace ddl

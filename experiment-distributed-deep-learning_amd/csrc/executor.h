@@ -1,0 +1,105 @@
+// executor.h — runs a ring program on HIP streams: recv -> reduce -> send overlap.
+//
+// Per rank two non-blocking streams: `comm` posts the send/recv groups of each tick (RCCL
+// kernels), `compute` runs the reduce kernel of each reduce-scatter tick. Events chain them:
+// reduce(s,k) waits for group(s,k); group(s+1,k) waits for reduce(s,k) (it forwards what that
+// reduce produced). With K slices per chunk the group of slice k+1 overlaps the reduce of
+// slice k. The caller's stream is forked into both and joined back — no host
+// synchronisation anywhere on the path.
+#pragma once
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "rccl_api.h"
+#include "schedule.h"
+
+namespace ddl {
+
+class Transport {
+public:
+    virtual ~Transport() = default;
+    // Post one tick's sends and recvs as one group on `stream`.
+    virtual void group(const std::vector<P2POp> &ops, hipStream_t stream) = 0;
+};
+
+class RcclTransport : public Transport {
+public:
+    explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
+    void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
+
+private:
+    ncclComm_t comm_;
+};
+
+// Streams, events and staging memory of one rank (reused across calls).
+class RankResources {
+public:
+    explicit RankResources(int device);
+    ~RankResources();
+    RankResources(const RankResources &) = delete;
+    RankResources &operator=(const RankResources &) = delete;
+
+    void ensure_events(size_t ticks);
+    void *ensure_staging(size_t bytes);
+
+    int device;
+    hipStream_t comm = nullptr, compute = nullptr;
+    std::vector<hipEvent_t> comm_ev, red_ev, pre_ev, post_ev;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+
+private:
+    void *staging_ = nullptr;
+    size_t staging_bytes_ = 0;
+};
+
+// Optional timing of the reduce kernels on the compute stream (bench.py's roofline leg):
+// timing events bracket every reduce launch while enabled; totals are read on demand.
+struct KernelStats {
+    long long launches = 0;
+    double bytes = 0;  // algorithmic HBM bytes: 3 * elements * sizeof(T) per launch
+    double ms = 0;
+};
+
+// Single-rank executor over a Transport (RCCL in production).
+class RingExecutor {
+public:
+    RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport);
+    ~RingExecutor();
+    void allreduce(const void *in, void *out, size_t n, int dtype, hipStream_t user,
+                   const RingConfig &cfg);
+    int rank() const { return rank_; }
+    int size() const { return size_; }
+    void set_timing(bool on);
+    KernelStats collect_stats();  // synchronises the recorded timing events, then resets
+
+private:
+    int rank_, size_;
+    std::unique_ptr<Transport> transport_;
+    RankResources res_;
+    RingProgram prog_;
+    bool timing_ = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed_;  // recorded, not yet collected
+    std::vector<double> timed_bytes_;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_pairs_;
+};
+
+// P virtual ranks in one process on one GPU: the same per-rank programs, with
+// device-to-device copies standing in for RCCL send/recv (matched by peer and ring tag).
+class LocalWorld {
+public:
+    LocalWorld(int nranks, int device);
+    void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
+                   const RingConfig &cfg);
+
+private:
+    int P_;
+    std::vector<std::unique_ptr<RankResources>> res_;
+    std::vector<RingProgram> progs_;
+};
+
+// Most recent tick <= w that launched a reduce (-1 if none).
+int last_reduce_at_or_before(const RingProgram &p, int w);
+
+}  // namespace ddl

@@ -1,0 +1,362 @@
+// handler.cpp — see handler.h.
+#include "handler.h"
+
+#include <algorithm>
+#include <chrono>
+#include <set>
+
+namespace ddl {
+
+std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vector<size_t> &esize,
+                             size_t limit) {
+    std::vector<Plan> plans;
+    const size_t nreq = elements.size();
+    if (nreq == 0) return plans;
+    DDL_REQUIRE(limit > 0, DDL_STATUS_INVALID_ARGUMENT, "fusion threshold must be > 0");
+    std::vector<size_t> begins(nreq);
+    size_t all = 0;
+    for (size_t i = 0; i < nreq; ++i) {
+        begins[i] = all;
+        all += elements[i] * esize[i];
+    }
+    size_t byte_size = 0, pb = 0, pbe = 0;
+    while (byte_size < all) {
+        size_t pe = nreq - 1, pe_elem = elements[nreq - 1];
+        byte_size += limit;
+        if (byte_size < all) {
+            for (size_t i = pb; i < nreq; ++i) {
+                if (i == nreq - 1 || (begins[i] < byte_size && byte_size <= begins[i + 1])) {
+                    pe = i;
+                    pe_elem = (byte_size - begins[i]) / esize[i];
+                    break;
+                }
+            }
+        }
+        // a plan must make progress: if the cap is below one element, take one element
+        if (pe == pb && pe_elem <= pbe) pe_elem = pbe + 1;
+        plans.push_back(Plan{pb, pbe, pe, pe_elem});
+        if (pe_elem == elements[pe]) {
+            pb = pe + 1;
+            pbe = 0;
+        } else {
+            pb = pe;
+            pbe = pe_elem;
+        }
+        byte_size = begins[pe] + esize[pe] * pe_elem;
+    }
+    return plans;
+}
+
+ControlChannel &world_control() {
+    static ControlChannel *ch = new ControlChannel();
+    return *ch;
+}
+
+RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
+    DeviceGuard g(owner_->device());
+    if (owner_->size() > 1) {
+        DDL_REQUIRE(world_control().connected() && world_control().size() == owner_->size() &&
+                        world_control().rank() == owner_->rank(),
+                    DDL_STATUS_NOT_INITIALIZED,
+                    "keyed requests at size > 1 need the control channel (ddl_control_connect)");
+        // private RCCL communicator for the data plane (collective: created on every rank
+        // inside ddl_control_connect)
+        data_ = owner_->split(0, owner_->rank());
+    } else {
+        data_ = owner_->shared_from_this();
+    }
+    DDL_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    thread_ = std::thread(&RequestHandler::main_, this);
+}
+
+RequestHandler::~RequestHandler() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    if (thread_.joinable()) thread_.join();
+    fail_all_(DDL_STATUS_COMM_ERROR);
+    for (hipEvent_t e : plan_events_) (void)hipEventDestroy(e);
+    if (fusion_) (void)hipFree(fusion_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void RequestHandler::submit(Request r) {
+    DDL_REQUIRE(dtype_size(r.dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << r.dtype);
+    DDL_REQUIRE(r.op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported");
+    DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
+        DDL_REQUIRE(pending_.find(r.key) == pending_.end(), DDL_STATUS_DUPLICATE_KEY,
+                    "a request with key '" << r.key << "' is already pending");
+        pending_.emplace(r.key, r);
+    }
+    cv_.notify_all();
+}
+
+void RequestHandler::wait_all() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_cv_.wait(lk, [this] { return (pending_.empty() && inflight_ == 0) || stop_; });
+}
+
+void RequestHandler::fail_all_(int status) {
+    std::map<std::string, Request> left;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        left.swap(pending_);
+    }
+    for (auto &kv : left) {
+        if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
+        if (kv.second.done) kv.second.done(status, kv.second.user);
+    }
+    idle_cv_.notify_all();
+}
+
+void RequestHandler::main_() {
+    try {
+        DDL_HIP(hipSetDevice(owner_->device()));
+        ControlChannel &ch = world_control();
+        const int P = owner_->size(), rank = owner_->rank();
+        for (;;) {
+            if (P == 1 || rank == 0) {
+                std::vector<std::string> keys;
+                {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
+                    if (stop_) break;
+                    for (auto &kv : pending_) keys.push_back(kv.first);
+                }
+                if (P == 1) execute_(keys);
+                else root_round_();
+            } else {
+                Token t;
+                bool got = ch.recv(t, 50);
+                if (!got) {
+                    std::lock_guard<std::mutex> g(mu_);
+                    if (stop_ && pending_.empty()) {
+                        // rank 0 shuts the ring down; keep listening a little for it
+                        Token s;
+                        if (ch.recv(s, 5000) && s.type == TOKEN_SHUT_DOWN) ch.send(s);
+                        break;
+                    }
+                    continue;
+                }
+                if (t.type == TOKEN_SHUT_DOWN) {
+                    ch.send(t);
+                    break;
+                }
+                member_round_(t);
+            }
+        }
+        if (P > 1 && rank == 0) {  // SHUT_DOWN lap (RingTokenCommunicateHandler.cc:34-48)
+            Token s;
+            s.type = TOKEN_SHUT_DOWN;
+            s.request = TOKEN_REQUEST_SHUTDOWN;
+            s.msg = "shut down";
+            ch.send(s);
+            Token back;
+            while (ch.recv(back, 5000) && back.type != TOKEN_SHUT_DOWN) {
+            }
+        }
+    } catch (const Error &e) {
+        DDL_LOG(0, "request handler stopped: " << e.msg);
+        fail_all_(e.status);
+    }
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    idle_cv_.notify_all();
+}
+
+std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine) {
+    Token t;
+    t.type = TOKEN_SYNC;
+    t.msg = encode_keys(mine);
+    ch.send(t);
+    Token back;
+    ch.recv(back, -1);
+    DDL_REQUIRE(back.type == TOKEN_SYNC, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)back.type);
+    Token c;
+    c.type = TOKEN_COMMUNICATE;
+    c.msg = back.msg;
+    ch.send(c);
+    return decode_keys(back.msg);
+}
+
+void negotiate_root_finish(ControlChannel &ch) {
+    Token drain;
+    ch.recv(drain, -1);
+    DDL_REQUIRE(drain.type == TOKEN_COMMUNICATE, DDL_STATUS_COMM_ERROR,
+                "token protocol: expected COMMUNICATE, got " << (int)drain.type);
+}
+
+std::vector<std::string> negotiate_member(
+    ControlChannel &ch, const Token &sync,
+    const std::function<std::vector<std::string>(const std::vector<std::string> &)> &intersect) {
+    DDL_REQUIRE(sync.type == TOKEN_SYNC, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)sync.type);
+    Token s;
+    s.type = TOKEN_SYNC;
+    s.msg = encode_keys(intersect(decode_keys(sync.msg)));
+    ch.send(s);
+    Token c;
+    ch.recv(c, -1);
+    DDL_REQUIRE(c.type == TOKEN_COMMUNICATE, DDL_STATUS_COMM_ERROR,
+                "token protocol: expected COMMUNICATE, got " << (int)c.type);
+    ch.send(c);  // forward first, then communicate (RingTokenCommunicateHandler.cc:302-310)
+    return decode_keys(c.msg);
+}
+
+// Rank 0: propose every registered key (lap 1, SYNC — each rank intersects), then announce
+// the agreed set (lap 2, COMMUNICATE) and run it.
+void RequestHandler::root_round_() {
+    ControlChannel &ch = world_control();
+    std::vector<std::string> mine;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto &kv : pending_) mine.push_back(kv.first);
+    }
+    std::vector<std::string> agreed = negotiate_root(ch, mine);
+    execute_(agreed);
+    negotiate_root_finish(ch);
+}
+
+// Other ranks: join the SYNC lap once the first proposed key is registered here (the
+// reference parks the READY token the same way, RingTokenCommunicateHandler.cc:225-250),
+// forward the intersection, then forward COMMUNICATE and run the agreed set (:302-310).
+void RequestHandler::member_round_(Token &t) {
+    std::vector<std::string> agreed = negotiate_member(world_control(), t, [this](const std::vector<std::string> &keys) {
+        std::vector<std::string> mine;
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!keys.empty()) cv_.wait(lk, [&] { return stop_ || pending_.count(keys.front()) > 0; });
+        for (const auto &k : keys)
+            if (pending_.count(k)) mine.push_back(k);
+        return mine;
+    });
+    execute_(agreed);
+}
+
+void RequestHandler::execute_(const std::vector<std::string> &keys) {
+    if (keys.empty()) return;
+    std::vector<Request> reqs;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (const auto &k : keys) {
+            auto it = pending_.find(k);
+            DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed key '" << k << "' is not registered");
+            reqs.push_back(it->second);
+            pending_.erase(it);
+        }
+        inflight_ += reqs.size();
+    }
+    // dtype groups in ascending enum order, keys lexicographic inside (std::map / sorted keys)
+    std::map<int, std::vector<size_t>> groups;
+    std::vector<size_t> empties;  // zero-element requests: nothing to reduce, done at once
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        if (reqs[i].n == 0) empties.push_back(i);
+        else groups[reqs[i].dtype].push_back(i);
+    }
+    const size_t kNoPlan = (size_t)-1;
+
+    struct Done {
+        size_t plan;
+        size_t req;
+        int status;
+    };
+    std::vector<Done> dones;
+    size_t nplans = 0;
+    std::set<size_t> waited;
+    int status = DDL_STATUS_OK;
+    try {
+        for (auto &g : groups) {
+            const int dt = g.first;
+            const size_t es = dtype_size(dt);
+            std::vector<size_t> elems, esz;
+            for (size_t i : g.second) {
+                elems.push_back(reqs[i].n);
+                esz.push_back(es);
+            }
+            std::vector<Plan> plans = make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load());
+            for (const Plan &p : plans) {
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    if (r.ready && waited.insert(g.second[q]).second)
+                        DDL_HIP(hipStreamWaitEvent(stream_, r.ready, 0));
+                }
+                if (p.req_begin == p.req_end) {
+                    const Request &r = reqs[g.second[p.req_begin]];
+                    const size_t cnt = p.elem_end - p.elem_begin;
+                    data_->allreduce(static_cast<const char *>(r.in) + p.elem_begin * es,
+                                     static_cast<char *>(r.out) + p.elem_begin * es, cnt, dt, r.op, stream_);
+                } else {
+                    std::vector<const void *> srcs;
+                    std::vector<void *> dsts;
+                    std::vector<size_t> bytes;
+                    size_t total = 0;
+                    for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                        const Request &r = reqs[g.second[q]];
+                        const size_t b = q == p.req_begin ? p.elem_begin : 0;
+                        const size_t e = q == p.req_end ? p.elem_end : r.n;
+                        srcs.push_back(static_cast<const char *>(r.in) + b * es);
+                        dsts.push_back(static_cast<char *>(r.out) + b * es);
+                        bytes.push_back((e - b) * es);
+                        total += ((e - b) * es + 255) & ~size_t(255);
+                    }
+                    if (total > fusion_bytes_) {
+                        if (fusion_) {
+                            DDL_HIP(hipStreamSynchronize(stream_));
+                            DDL_HIP(hipFree(fusion_));
+                            fusion_ = nullptr;
+                        }
+                        fusion_bytes_ = total + total / 2;  // x1.5 growth (MPIRTC.cc:13, 480)
+                        DDL_HIP(hipMalloc(&fusion_, fusion_bytes_));
+                    }
+                    launch_pack(fusion_, srcs.data(), bytes.data(), (int)srcs.size(), stream_);
+                    data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+                    launch_unpack(dsts.data(), fusion_, bytes.data(), (int)dsts.size(), stream_);
+                }
+                if (plan_events_.size() <= nplans) {
+                    hipEvent_t e;
+                    DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    plan_events_.push_back(e);
+                }
+                DDL_HIP(hipEventRecord(plan_events_[nplans], stream_));
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    const size_t e = q == p.req_end ? p.elem_end : r.n;
+                    if (e == r.n) dones.push_back(Done{nplans, g.second[q], DDL_STATUS_OK});
+                }
+                ++nplans;
+            }
+        }
+        for (size_t i : empties) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});
+    } catch (const Error &e) {
+        DDL_LOG(0, "allreduce of agreed requests failed: " << e.msg);
+        status = e.status;
+    }
+    // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725)
+    std::vector<char> fired(reqs.size(), 0);
+    for (const Done &d : dones) {
+        if (status == DDL_STATUS_OK && d.plan != kNoPlan) {
+            hipError_t he = hipEventSynchronize(plan_events_[d.plan]);
+            if (he != hipSuccess) status = DDL_STATUS_HIP_ERROR;
+        }
+        const Request &r = reqs[d.req];
+        fired[d.req] = 1;
+        if (r.done) r.done(status == DDL_STATUS_OK ? d.status : status, r.user);
+    }
+    for (size_t i = 0; i < reqs.size(); ++i)
+        if (!fired[i] && reqs[i].done) reqs[i].done(status == DDL_STATUS_OK ? DDL_STATUS_ERROR_UNKNOWN : status, reqs[i].user);
+    for (const Request &r : reqs)
+        if (r.ready) (void)hipEventDestroy(r.ready);
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        inflight_ -= reqs.size();
+    }
+    idle_cv_.notify_all();
+    if (status != DDL_STATUS_OK) fail(status, "keyed allreduce failed");
+}
+
+}  // namespace ddl

@@ -1,0 +1,102 @@
+// handler.h — keyed asynchronous allreduce requests with cross-rank negotiation and fusion.
+//
+// Replaces the reference's request path below the TF op:
+//   TensorAllreduceRequest (collective/request/TensorAllreduceRequest.h:13-41)
+//   RingTokenCommunicateHandler (controller/rtc/RingTokenCommunicateHandler.cc:13-410):
+//     per-communicator background thread, ring-token negotiation of which keys every rank
+//     has registered, communication of the agreed set in lexicographic (type, key) order;
+//   MPIRingTokenCommunication::allreduceRequests (rtc/mpi/MPIRingTokenCommunication.cc:105-157,
+//     495-749): dtype classification (ascending enum), plans capped at the fusion threshold,
+//     memcpy in -> MPI_Allreduce -> memcpy out, done() as each tensor's last element lands.
+//
+// MI355X-first changes: the token makes 2 laps instead of 3 (READY+SYNC merged: a rank joins
+// the lap once it has the first key of the proposed set, then intersects); one-request plans
+// run the ring directly on the tensor (no staging copy); multi-request plans are packed by
+// one gather kernel into an HBM fusion buffer and scattered by one kernel; the data plane
+// runs on a private RCCL communicator so user-level ddl_allreduce calls never interleave.
+#pragma once
+
+#include <condition_variable>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "control.h"
+#include "engine.h"
+
+namespace ddl {
+
+struct Request {
+    std::string key;
+    const void *in = nullptr;
+    void *out = nullptr;
+    size_t n = 0;
+    int dtype = 0;
+    int op = 0;
+    hipEvent_t ready = nullptr;  // input ready on the submitter's stream
+    ddl_done_fn done = nullptr;
+    void *user = nullptr;
+};
+
+struct Plan {  // makeCollectiveCommunicatePlan's (requestBegin, elementBegin, requestEnd, elementEnd)
+    size_t req_begin, elem_begin, req_end, elem_end;
+};
+
+// Plans over requests (in order) capped at `limit` bytes. Same walk as the reference
+// (MPIRingTokenCommunication.cc:495-546) except that a plan ending exactly on a request
+// boundary advances to requestEnd + 1 (the reference advances requestBegin by one, which
+// re-plans requests when a multi-request plan ends on a boundary; unreachable with its odd
+// 2^31-1 cap and even element sizes, reachable with a configurable cap).
+std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vector<size_t> &esize,
+                             size_t limit);
+
+// Global control channel of the world communicator (ddl_control_listen/connect).
+ControlChannel &world_control();
+
+// One negotiation round of the 2-lap token protocol.
+//   root:   SYNC(mine) -> ... -> SYNC(intersection) back; COMMUNICATE(agreed) sent.
+//           After running the agreed set, negotiate_root_finish() drains COMMUNICATE.
+//   member: receives SYNC, `intersect` (may block until the first key is registered)
+//           forwards the intersection, then receives and forwards COMMUNICATE.
+std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine);
+void negotiate_root_finish(ControlChannel &ch);
+std::vector<std::string> negotiate_member(
+    ControlChannel &ch, const Token &sync,
+    const std::function<std::vector<std::string>(const std::vector<std::string> &)> &intersect);
+
+class RequestHandler {
+public:
+    explicit RequestHandler(Communicator *owner);
+    ~RequestHandler();
+
+    void submit(Request r);
+    void wait_all();
+
+private:
+    void main_();
+    void root_round_();
+    void member_round_(Token &first);
+    void execute_(const std::vector<std::string> &keys);
+    void fail_all_(int status);
+
+    Communicator *owner_;
+    std::shared_ptr<Communicator> data_;  // private data-plane communicator
+    hipStream_t stream_ = nullptr;
+    void *fusion_ = nullptr;
+    size_t fusion_bytes_ = 0;
+    std::vector<hipEvent_t> plan_events_;
+
+    std::mutex mu_;
+    std::condition_variable cv_;       // new registrations / stop
+    std::condition_variable idle_cv_;  // completions
+    std::map<std::string, Request> pending_;  // sorted: lexicographic key order
+    size_t inflight_ = 0;
+    bool stop_ = false;
+    std::thread thread_;
+};
+
+}  // namespace ddl

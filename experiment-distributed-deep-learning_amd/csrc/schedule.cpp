@@ -1,0 +1,227 @@
+// schedule.cpp — ring construction, bucket partition and per-rank tick lists.
+#include "schedule.h"
+
+#include <map>
+#include <mutex>
+
+namespace ddl {
+
+namespace {
+
+struct RingSearch {
+    int P;
+    std::vector<std::vector<char>> used;  // used[u][v]: directed edge u->v taken
+    std::vector<std::vector<int>> cycles;
+    int want;
+
+    bool next_cycle(std::vector<int> &path, std::vector<char> &visited, std::vector<int> &out) {
+        // first Hamiltonian cycle (DFS, ascending vertex order) avoiding used edges
+        if ((int)path.size() == P) {
+            if (!used[path.back()][path[0]]) { out = path; return true; }
+            return false;
+        }
+        for (int v = 0; v < P; ++v) {
+            if (visited[v] || used[path.back()][v]) continue;
+            visited[v] = 1;
+            path.push_back(v);
+            if (next_cycle(path, visited, out)) return true;
+            path.pop_back();
+            visited[v] = 0;
+        }
+        return false;
+    }
+
+    // Enumerate candidate cycles in DFS order and backtrack over them.
+    void all_cycles(std::vector<int> &path, std::vector<char> &visited,
+                    std::vector<std::vector<int>> &res) {
+        if ((int)path.size() == P) {
+            if (!used[path.back()][path[0]]) res.push_back(path);
+            return;
+        }
+        for (int v = 0; v < P; ++v) {
+            if (visited[v] || used[path.back()][v]) continue;
+            visited[v] = 1;
+            path.push_back(v);
+            all_cycles(path, visited, res);
+            path.pop_back();
+            visited[v] = 0;
+        }
+    }
+
+    void mark(const std::vector<int> &c, char val) {
+        for (int i = 0; i < P; ++i) used[c[i]][c[(i + 1) % P]] = val;
+    }
+
+    bool rec(std::vector<std::vector<int>> &best) {
+        if ((int)cycles.size() == want) return true;
+        if (cycles.size() > best.size()) best = cycles;
+        std::vector<int> path{0};
+        std::vector<char> visited(P, 0);
+        visited[0] = 1;
+        std::vector<std::vector<int>> cands;
+        all_cycles(path, visited, cands);
+        for (const auto &c : cands) {
+            mark(c, 1);
+            cycles.push_back(c);
+            if (rec(best)) return true;
+            cycles.pop_back();
+            mark(c, 0);
+        }
+        return false;
+    }
+};
+
+std::vector<std::vector<int>> search_rings(int P, int max_rings) {
+    std::vector<std::vector<int>> res;
+    std::vector<int> nat(P);
+    for (int i = 0; i < P; ++i) nat[i] = i;
+    res.push_back(nat);
+    if (P <= 2 || max_rings <= 1) return res;
+    RingSearch s;
+    s.P = P;
+    s.used.assign(P, std::vector<char>(P, 0));
+    s.want = std::min(P - 1, max_rings);
+    s.mark(nat, 1);
+    s.cycles.push_back(nat);
+    std::vector<std::vector<int>> best = s.cycles;
+    if (s.rec(best)) return s.cycles;
+    return best;
+}
+
+}  // namespace
+
+const std::vector<std::vector<int>> &rings_for(int P, int max_rings) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::vector<std::vector<int>>> cache;
+    if (P < 1) P = 1;
+    if (max_rings < 1) max_rings = 1;
+    if (max_rings > kMaxRings) max_rings = kMaxRings;
+    std::lock_guard<std::mutex> g(mu);
+    auto key = std::make_pair(P, max_rings);
+    auto it = cache.find(key);
+    if (it == cache.end()) it = cache.emplace(key, search_rings(P, max_rings)).first;
+    return it->second;
+}
+
+Range chunk_range(size_t n, size_t esize, int P, int R, int ring, int chunk) {
+    const size_t G = kGranuleBytes / esize;
+    const size_t ng = (n + G - 1) / G;
+    const size_t parts = (size_t)R * (size_t)P;
+    const size_t q = (size_t)ring * (size_t)P + (size_t)chunk;
+    const size_t gb = (size_t)(((unsigned __int128)ng * q) / parts);
+    const size_t ge = (size_t)(((unsigned __int128)ng * (q + 1)) / parts);
+    Range r;
+    r.begin = gb * G < n ? gb * G : n;
+    r.end = ge * G < n ? ge * G : n;
+    return r;
+}
+
+Range slice_range(const Range &chunk, size_t esize, int K, int k) {
+    const size_t G = kGranuleBytes / esize;
+    const size_t len = chunk.size();
+    const size_t ng = (len + G - 1) / G;
+    const size_t gb = ng * (size_t)k / (size_t)K, ge = ng * (size_t)(k + 1) / (size_t)K;
+    Range r;
+    r.begin = chunk.begin + (gb * G < len ? gb * G : len);
+    r.end = chunk.begin + (ge * G < len ? ge * G : len);
+    return r;
+}
+
+void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
+                size_t *staging_stride) {
+    const auto &rings = rings_for(P, cfg.rings);
+    int r = (int)rings.size();
+    // Small buckets: fewer rings so every message stays >= 64 KiB (latency-bound regime).
+    const size_t bytes = n * esize;
+    while (r > 1 && bytes / ((size_t)r * (size_t)P) < (64u << 10)) --r;
+    size_t max_chunk = 0;
+    for (int j = 0; j < r; ++j)
+        for (int c = 0; c < P; ++c) {
+            size_t s = chunk_range(n, esize, P, r, j, c).size();
+            max_chunk = s > max_chunk ? s : max_chunk;
+        }
+    int k = 1;
+    if (cfg.slice_bytes > 0) {
+        size_t want = (max_chunk * esize + cfg.slice_bytes - 1) / cfg.slice_bytes;
+        k = (int)(want < 1 ? 1 : want);
+    }
+    if (k > cfg.max_slices) k = cfg.max_slices;
+    if (k < 1) k = 1;
+    *R = r;
+    *K = k;
+    *staging_stride = (max_chunk + 63) & ~size_t(63);
+}
+
+void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
+                   size_t n, int dtype, const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    prog.P = P;
+    prog.rank = rank;
+    prog.n = n;
+    prog.esize = es;
+    prog.ticks.clear();
+    ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
+    if (P <= 1 || n == 0) return;
+    const int R = prog.R, K = prog.K;
+    const auto &rings = rings_for(P, cfg.rings);
+    std::vector<int> pos(R), succ(R), pred(R);
+    for (int j = 0; j < R; ++j) {
+        const auto &ring = rings[j];
+        int p = 0;
+        while (ring[p] != rank) ++p;
+        pos[j] = p;
+        succ[j] = ring[(p + 1) % P];
+        pred[j] = ring[(p + P - 1) % P];
+    }
+    const char *inb = static_cast<const char *>(in);
+    char *outb = static_cast<char *>(out);
+    char *stb = static_cast<char *>(staging);
+    auto mod = [P](int x) { return ((x % P) + P) % P; };
+
+    // reduce-scatter: tick index = s*K + k
+    for (int s = 0; s < P - 1; ++s) {
+        for (int k = 0; k < K; ++k) {
+            Tick t;
+            t.reduce.count = 0;
+            if (s > 0) t.wait_reduce = (s - 1) * K + k;
+            for (int j = 0; j < R; ++j) {
+                const Range sc = chunk_range(n, es, P, R, j, mod(pos[j] - s));
+                const Range rc = chunk_range(n, es, P, R, j, mod(pos[j] - s - 1));
+                const Range ss = slice_range(sc, es, K, k);
+                const Range rs = slice_range(rc, es, K, k);
+                if (ss.size()) {
+                    const char *src = (s == 0 ? inb : outb) + ss.begin * es;
+                    t.ops.push_back(P2POp{true, succ[j], j, const_cast<char *>(src), ss.size() * es});
+                }
+                if (rs.size()) {
+                    char *st = stb + ((size_t)j * prog.staging_stride + (rs.begin - rc.begin)) * es;
+                    t.ops.push_back(P2POp{false, pred[j], j, st, rs.size() * es});
+                    const int c = t.reduce.count++;
+                    t.reduce.a[c] = inb + rs.begin * es;
+                    t.reduce.b[c] = st;
+                    t.reduce.out[c] = outb + rs.begin * es;
+                    t.reduce.n[c] = rs.size();
+                }
+            }
+            t.has_reduce = t.reduce.count > 0;
+            prog.ticks.push_back(std::move(t));
+        }
+    }
+    // allgather: the first step waits for the last reduce-scatter reduce (compute stream is
+    // in order, so that covers every slice)
+    const int last_rs = (P - 1) * K - 1;
+    for (int s = 0; s < P - 1; ++s) {
+        Tick t;
+        t.reduce.count = 0;
+        if (s == 0) t.wait_reduce = last_rs;
+        for (int j = 0; j < R; ++j) {
+            const Range sc = chunk_range(n, es, P, R, j, mod(pos[j] + 1 - s));
+            const Range rc = chunk_range(n, es, P, R, j, mod(pos[j] - s));
+            if (sc.size()) t.ops.push_back(P2POp{true, succ[j], j, outb + sc.begin * es, sc.size() * es});
+            if (rc.size()) t.ops.push_back(P2POp{false, pred[j], j, outb + rc.begin * es, rc.size() * es});
+        }
+        prog.ticks.push_back(std::move(t));
+    }
+}
+
+}  // namespace ddl

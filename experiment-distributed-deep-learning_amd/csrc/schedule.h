@@ -1,0 +1,77 @@
+// schedule.h — the ring reduce-scatter / allgather schedule (host side, no GPU calls).
+//
+// Replaces what MPICH does inside MPI_Allreduce at the reference's data-plane call
+// (src/cpp/communicate/backend/mpi/MPICommunicator.cc:14-28) with an explicit multi-ring
+// schedule for a fully connected xGMI node:
+//   * R rings = edge-disjoint directed Hamiltonian cycles of the P ranks (ring 0 is the
+//     natural ring r -> r+1, the direction of the reference's token ring,
+//     RingTokenCommunicateHandler.cc:52-54); P = 8 gives 7 rings, one per xGMI link;
+//   * the bucket splits into R*P chunks of 256-byte granules (ring j owns chunks j*P..j*P+P-1);
+//   * reduce-scatter: P-1 steps, each chunk split into K slices so the recv of slice k+1
+//     overlaps the reduce of slice k; allgather: P-1 steps, received straight into `out`.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "common.h"
+
+namespace ddl {
+
+struct Range {
+    size_t begin = 0, end = 0;
+    size_t size() const { return end > begin ? end - begin : 0; }
+};
+
+constexpr size_t kGranuleBytes = 256;
+constexpr int kMaxRings = kMaxSegments;  // one reduce segment per ring per launch
+
+// Edge-disjoint directed Hamiltonian cycles of K_P (deterministic DFS; ring 0 = identity).
+// Returns at most max_rings rings; each ring is the list of ranks in ring order.
+const std::vector<std::vector<int>> &rings_for(int P, int max_rings);
+
+// Element range of (ring, chunk) — granules split evenly over R*P parts.
+Range chunk_range(size_t n, size_t esize, int P, int R, int ring, int chunk);
+// Element range of slice k of K inside `chunk` (granule-aligned, relative to the bucket).
+Range slice_range(const Range &chunk, size_t esize, int K, int k);
+
+struct P2POp {
+    bool send;
+    int peer;
+    int tag;  // ring index: matches a send with its recv inside one tick
+    void *ptr;
+    size_t bytes;
+};
+
+struct Tick {
+    std::vector<P2POp> ops;
+    SegTable reduce;       // valid when has_reduce
+    bool has_reduce = false;
+    int wait_reduce = -1;  // the comm stream waits for this tick's reduce before posting ops
+};
+
+struct RingConfig {
+    int rings = kMaxRings;            // upper bound; clipped to what the topology allows
+    size_t slice_bytes = 2u << 20;    // target bytes per reduce-scatter message
+    int max_slices = 8;
+};
+
+// Per-rank tick list of one allreduce. `staging` must hold staging_elems(...) elements per
+// ring (ring j uses staging + j * stride_elems).
+struct RingProgram {
+    int P = 1, R = 1, K = 1, rank = 0;
+    size_t n = 0, esize = 0;
+    size_t staging_stride = 0;  // elements per ring in the staging buffer
+    std::vector<Tick> ticks;
+};
+
+// Number of rings and slices the schedule uses for this problem.
+void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
+                size_t *staging_stride);
+
+// Builds rank `rank`'s program. in/out are that rank's buffers, staging its scratch.
+void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
+                   size_t n, int dtype, const RingConfig &cfg);
+
+}  // namespace ddl

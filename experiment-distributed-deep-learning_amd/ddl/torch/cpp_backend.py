@@ -1,0 +1,122 @@
+"""Loader of the native engine (mirror of reference src/py/ddl/tensorflow/cpp_backend.py:16-80).
+
+The reference loads one library twice — as a TF op library and through ctypes. Here there is
+no op library: every call goes through the C-ABI of lib/libddl_amd.so (include/ddl_amd.h).
+`import torch` happens first so the engine binds to the HIP runtime (and RCCL) PyTorch has
+already loaded. If the library is missing the import fails loudly: there is no fallback path.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: one HIP runtime per process)
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+DEFAULT_LIB = os.path.join(_PKG_ROOT, 'lib', 'libddl_amd.so')
+
+# enum ddl_dtype (tensorflow::DataType numbers, reference src/cpp/def.h:10-53)
+DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_BFLOAT16, DT_HALF, DT_UINT64 = 1, 2, 3, 9, 14, 19, 23
+STATUS_OK = 0
+STATUS_NAMES = {0: 'OK', 1: 'COMM_ERROR', 2: 'ERROR_UNKNOWN', 3: 'INVALID_ARGUMENT',
+                4: 'UNSUPPORTED_DTYPE', 5: 'HIP_ERROR', 6: 'NOT_INITIALIZED', 7: 'DUPLICATE_KEY'}
+OP_SUM = 0
+
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p)
+
+
+class DDLError(RuntimeError):
+    """A non-OK status from the engine (StatusCode, reference src/cpp/def.h:70-74)."""
+
+    def __init__(self, status: int, where: str, detail: str):
+        self.status = status
+        super().__init__(f'{where} failed: {STATUS_NAMES.get(status, status)}: {detail}')
+
+
+class CPPBackend:
+    """Manages the native engine (same role and names as the reference's CPPBackend)."""
+    __path_to_lib = DEFAULT_LIB
+    __initialized = False
+    __c_api = None
+
+    @classmethod
+    def __initialize(cls, path_to_lib: str = None):
+        if path_to_lib is None:
+            path_to_lib = os.environ.get('ddl_lib')  # same override as the reference (:34)
+        if path_to_lib is not None:
+            cls.__path_to_lib = path_to_lib
+        if not os.path.exists(cls.__path_to_lib):
+            raise ImportError(
+                f'ddl engine library not found at {cls.__path_to_lib}; build it with '
+                f'`python -c "import __graft_entry__ as g; g.build()"` (no fallback exists)')
+        lib = ctypes.CDLL(cls.__path_to_lib, mode=ctypes.RTLD_GLOBAL)
+        cid, sz, vp, ci = ctypes.c_longlong, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+
+        def sig(name, restype, *argtypes):
+            f = getattr(lib, name)
+            f.restype = restype
+            f.argtypes = list(argtypes)
+
+        sig('ddl_version', ci)
+        sig('ddl_last_error', ctypes.c_char_p)
+        sig('ddl_dtype_size', sz, ci)
+        sig('ddl_get_unique_id', ci, vp, sz)
+        sig('ddl_init', ci, ci, ci, ci, vp, sz)
+        sig('ddl_init_single', ci, ci)
+        sig('ddl_control_listen', ci, ctypes.c_char_p, sz)
+        sig('ddl_control_connect', ci, ctypes.c_char_p)
+        sig('ddl_control_connect_ranked', ci, ci, ci, ctypes.c_char_p)
+        sig('ddl_control_negotiate', ci, ctypes.c_char_p, ctypes.c_char_p, sz)
+        sig('ddl_allreduce_variant', ci, cid, vp, vp, sz, ci, ci, vp, ci)
+        sig('ddl_ring_program', ci, ci, ci, sz, ci, ctypes.POINTER(ctypes.c_longlong), sz, ctypes.POINTER(sz))
+        sig('ddl_finalize', ci)
+        sig('ddl_is_initialized', ci)
+        sig('ddl_set_config', ci, ctypes.c_char_p, ctypes.c_longlong)
+        sig('ddl_get_config', ctypes.c_longlong, ctypes.c_char_p)
+        # reference c_api.h:15-41 (ctypes signatures as cpp_backend.py:47-78)
+        sig('communicator_rank', ci, cid)
+        sig('communicator_size', ci, cid)
+        sig('world_communicator', cid)
+        sig('split_communicator', cid, cid, ci, ci)
+        sig('detach_communicator', None, cid)
+        sig('py_info', None, ctypes.c_char_p)
+        sig('py_debug', None, ctypes.c_char_p)
+        sig('py_error', None, ctypes.c_char_p)
+        # data plane
+        sig('ddl_allreduce', ci, cid, vp, vp, sz, ci, ci, vp)
+        sig('ddl_allreduce_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
+        sig('ddl_wait_all', ci, cid)
+        sig('ddl_kernel_timing', ci, cid, ci)
+        sig('ddl_kernel_stats', ci, cid, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),
+            ctypes.POINTER(ctypes.c_double))
+        sig('ddl_reduce_local', ci, vp, vp, sz, ci, vp)
+        sig('ddl_reduce_sum2', ci, vp, vp, vp, sz, ci, vp)
+        sig('ddl_reduce_sum2_variant', ci, ci, vp, vp, vp, sz, ci, vp)
+        sig('ddl_pack', ci, vp, ctypes.POINTER(vp), ctypes.POINTER(sz), ci, vp)
+        sig('ddl_unpack', ci, ctypes.POINTER(vp), vp, ctypes.POINTER(sz), ci, vp)
+        sig('ddl_local_ring_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, ci, vp)
+        # schedule introspection
+        sig('ddl_ring_count', ci, ci, ci)
+        sig('ddl_ring_perm', ci, ci, ci, ci, ctypes.POINTER(ci))
+        sig('ddl_chunk_range', ci, sz, ci, ci, ci, ci, ci, ctypes.POINTER(sz), ctypes.POINTER(sz))
+        sig('ddl_ring_shape', ci, sz, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci))
+        sig('ddl_make_plans', ci, ctypes.POINTER(sz), ctypes.POINTER(sz), sz, sz, ctypes.POINTER(sz), sz,
+            ctypes.POINTER(sz))
+        cls.__c_api = lib
+        cls.__initialized = True
+
+    @classmethod
+    def c_api(cls):
+        if not cls.__initialized:
+            cls.__initialize()
+        return cls.__c_api
+
+    @classmethod
+    def path(cls) -> str:
+        cls.c_api()
+        return cls.__path_to_lib
+
+
+def check(status: int, where: str) -> None:
+    """Raise DDLError for a non-OK status, with the engine's last error message."""
+    if status != STATUS_OK:
+        msg = CPPBackend.c_api().ddl_last_error()
+        raise DDLError(status, where, msg.decode(errors='replace') if msg else '')

@@ -1,0 +1,4 @@
+from ddl.torch.parallelism.data.distributed_optimizer import (  # noqa: F401
+    DataParallelismDistributedOptimizer,
+    data_parallelism_distributed_optimizer_wrapper,
+)

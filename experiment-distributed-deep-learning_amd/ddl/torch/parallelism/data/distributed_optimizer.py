@@ -1,0 +1,63 @@
+"""Data-parallel optimizer wrapper for torch.optim (mirror of reference
+src/py/ddl/tensorflow/keras/parallelism/data/distributed_optimizer.py:9-110).
+
+Every rank computes gradients on its shard of the batch; before the wrapped optimizer's
+`step()` each gradient is submitted as a keyed allreduce request (the reference builds one
+`Allreduce` op per gradient, :43-68), the engine negotiates and fuses them, and the sum is
+divided by the communicator size (allreduce_gradient, tensor_communicate.py:21-25). At
+size 1 nothing is communicated (the reference's `tf.cond(size > 1)`, :53-60).
+"""
+import torch
+
+from ddl.torch.communicator import Communicator
+from ddl.torch.tensor_communicate import allreduce_async
+
+
+class DataParallelismDistributedOptimizer:
+    """Mixin placed in front of the wrapped optimizer class (the reference's approach)."""
+    communicator: Communicator = None
+    _ddl_name = 'DataParallelismDistributedOptimizer'
+
+    def allreduce_gradients(self) -> None:
+        comm = self.communicator or Communicator.world()
+        if comm.size <= 1:
+            return
+        handles = []
+        for gi, group in enumerate(self.param_groups):
+            for pi, p in enumerate(group['params']):
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise NotImplementedError('sparse gradients need allgather (not implemented)')
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                key = f'{self._ddl_name}/{type(self).__name__}/Allreduce/group{gi}/param{pi:05d}'
+                handles.append((p, allreduce_async(g, key, comm, output=g)))
+        for p, h in handles:
+            out = h.wait()
+            out.div_(comm.size)
+            if out.data_ptr() != p.grad.data_ptr():
+                p.grad.copy_(out)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        self.allreduce_gradients()
+        return super().step(closure)
+
+    @property
+    def is_distributed_optimizer(self) -> bool:
+        return True
+
+
+def data_parallelism_distributed_optimizer_wrapper(
+        optimizer: torch.optim.Optimizer,
+        communicator: Communicator = None) -> torch.optim.Optimizer:
+    """Return an optimizer of a subclass of `type(optimizer)` whose step() first averages the
+    gradients across `communicator` (default: the world). Parameter groups and state are
+    shared with `optimizer`."""
+    opt_cls = optimizer.__class__
+    assert issubclass(opt_cls, torch.optim.Optimizer)
+    cls = type(opt_cls.__name__, (DataParallelismDistributedOptimizer, opt_cls), {})
+    res = cls.__new__(cls)
+    res.__dict__.update(optimizer.__dict__)
+    res.communicator = communicator
+    return res

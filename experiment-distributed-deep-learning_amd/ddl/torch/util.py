@@ -1,0 +1,35 @@
+"""Helpers between torch tensors and the C-ABI (reference counterpart: src/py/ddl/tensorflow/util.py)."""
+import torch
+
+from ddl.torch import cpp_backend as cb
+
+_DTYPES = {
+    torch.float32: cb.DT_FLOAT,
+    torch.float64: cb.DT_DOUBLE,
+    torch.int32: cb.DT_INT32,
+    torch.int64: cb.DT_INT64,
+    torch.float16: cb.DT_HALF,
+    torch.bfloat16: cb.DT_BFLOAT16,
+}
+if hasattr(torch, 'uint64'):
+    _DTYPES[torch.uint64] = cb.DT_UINT64
+
+
+def ddl_dtype(t: torch.Tensor) -> int:
+    try:
+        return _DTYPES[t.dtype]
+    except KeyError:
+        raise TypeError(f'allreduce: unsupported dtype {t.dtype} '
+                        f'(supported: {sorted(str(d) for d in _DTYPES)})') from None
+
+
+def current_stream_handle(device=None) -> int:
+    """hipStream_t of torch's current stream (0 = legacy default stream)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device_tensor(t: torch.Tensor, what: str = 'tensor') -> None:
+    if not t.is_cuda:
+        raise ValueError(f'{what} must be a device (HBM) tensor')
+    if not t.is_contiguous():
+        raise ValueError(f'{what} must be contiguous')

@@ -1,0 +1,193 @@
+/*
+ * ddl_amd.h — C-ABI of the MI355X gradient-bucket allreduce engine.
+ *
+ * This is the drop-in boundary for the reference's allreduce hot path
+ * (LYL232/Experiment-Distributed-Deep-Learning, paths relative to its src/):
+ *
+ *   reference                                             replaced by
+ *   ---------------------------------------------------   -----------------------------
+ *   cpp/c_api.h:15-17   communicator_rank/size            communicator_rank/size
+ *   cpp/c_api.h:19      world_communicator                world_communicator
+ *   cpp/c_api.h:33-35   split/detach_communicator         split_communicator/detach_communicator
+ *   cpp/c_api.h:37-41   py_info/py_debug/py_error         py_info/py_debug/py_error
+ *   cpp/global/initialize.cc:57-65 + MPIBackend.cc:77-97  ddl_get_unique_id + ddl_init
+ *     (MPI_Init_thread at dlopen)                          (explicit RCCL bootstrap)
+ *   cpp/communicate/backend/Communicator.h:45-48 /        ddl_allreduce (device buffers,
+ *     mpi/MPICommunicator.cc:14-28  (MPI_Allreduce SUM)     ring RS/AG over RCCL + HIP reduce)
+ *   cpp/op/tensorflow/AllreduceOp.cc:32-66 →              ddl_allreduce_submit
+ *     TensorsCollectiveCommunicateController::handleRequest (keyed async request, done callback)
+ *     (.../controller/TensorsCollectiveCommunicateController.h:14-34)
+ *
+ * Conventions (mirroring the reference):
+ *   - communicator ids are 64-bit integers (Communicator::ID = long long, Communicator.h:20);
+ *   - dtypes use tensorflow::DataType numbers, as the reference does (def.h:10 uses
+ *     tensorflow::DataType; ascending enum order is the fusion group order,
+ *     MPIRingTokenCommunication.cc:735-749);
+ *   - every call returns an int status (StatusCode, def.h:70-74, extended); no C++
+ *     exception crosses this boundary; ddl_last_error() describes the last failure
+ *     on the calling thread;
+ *   - buffers are device (HBM) pointers; hip_stream is a hipStream_t (NULL = legacy
+ *     default stream); calls are stream-ordered and never synchronise the host unless
+ *     documented.
+ */
+#ifndef DDL_AMD_H
+#define DDL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tensorflow::DataType numeric values (reference def.h:10-53 comment block). */
+enum ddl_dtype {
+    DDL_FLOAT = 1,
+    DDL_DOUBLE = 2,
+    DDL_INT32 = 3,
+    DDL_INT64 = 9,
+    DDL_BFLOAT16 = 14, /* extension: the reference rejects it (AllreduceOp.cc:18) */
+    DDL_HALF = 19,     /* extension: the reference rejects it (MPIBackend.cc:48-66) */
+    DDL_UINT64 = 23
+};
+
+/* StatusCode (reference def.h:70-74) + extensions. */
+enum ddl_status {
+    DDL_STATUS_OK = 0,
+    DDL_STATUS_COMM_ERROR = 1, /* was STATUS_MPI_ERROR: RCCL / control-channel failure */
+    DDL_STATUS_ERROR_UNKNOWN = 2,
+    DDL_STATUS_INVALID_ARGUMENT = 3,
+    DDL_STATUS_UNSUPPORTED_DTYPE = 4,
+    DDL_STATUS_HIP_ERROR = 5,
+    DDL_STATUS_NOT_INITIALIZED = 6,
+    DDL_STATUS_DUPLICATE_KEY = 7 /* TensorCommunicateRequest.h:21: one pending request per key */
+};
+
+/* Communicator::AllreduceOperation (reference Communicator.h:22-24): SUM only. */
+enum ddl_allreduce_op { DDL_ALLREDUCE_OP_SUM = 0 };
+
+typedef long long ddl_communicator_id;
+
+/* Completion callback of a keyed request: TensorCommunicateRequest::done(StatusCode)
+ * (reference TensorCommunicateRequest.h:41). Runs on the communicator's engine thread. */
+typedef void (*ddl_done_fn)(int status, void *user);
+
+/* ---- library / lifecycle ------------------------------------------------------- */
+int ddl_version(void);
+const char *ddl_last_error(void);
+const char *ddl_dtype_name(int dtype);
+size_t ddl_dtype_size(int dtype); /* 0 for unsupported */
+
+/* RCCL bootstrap id (128 bytes). Rank 0 creates it and the launcher distributes it. */
+int ddl_get_unique_id(void *out, size_t len);
+/* Creates the world communicator for this process (one process per GPU). */
+int ddl_init(int rank, int size, int device, const void *unique_id, size_t len);
+/* Same, for a single-process world (size 1); no RCCL involved. */
+int ddl_init_single(int device);
+/* Optional control channel for keyed requests at size > 1 (ring of TCP links, replaces the
+ * MPI p2p token ring, MPIRingTokenCommunication.cc:29-102). ddl_control_listen opens a
+ * listener and returns "ip:port"; ddl_control_connect takes every rank's endpoint,
+ * separated by ';', in rank order. */
+int ddl_control_listen(char *endpoint_out, size_t len);
+int ddl_control_connect(const char *endpoints);
+/* Control channel without a world communicator (tools / CPU tests of the token protocol). */
+int ddl_control_connect_ranked(int rank, int size, const char *endpoints);
+/* One negotiation round over the control channel with a fixed key set ('\n'-separated):
+ * writes the agreed keys ('\n'-separated, lexicographic) to out. Same protocol as the
+ * keyed-request handler, without the data plane. */
+int ddl_control_negotiate(const char *keys, char *out, size_t len);
+int ddl_finalize(void);
+int ddl_is_initialized(void);
+
+/* Tunables: "slice_bytes", "rings", "fusion_threshold_bytes", "log_level". */
+int ddl_set_config(const char *key, long long value);
+long long ddl_get_config(const char *key);
+
+/* ---- reference c_api.h surface ----------------------------------------------------- */
+int communicator_rank(ddl_communicator_id id);
+int communicator_size(ddl_communicator_id id);
+ddl_communicator_id world_communicator(void);
+ddl_communicator_id split_communicator(ddl_communicator_id id, int color, int key);
+void detach_communicator(ddl_communicator_id id);
+void py_info(const char *log_str);
+void py_debug(const char *log_str);
+void py_error(const char *log_str);
+
+/* ---- data plane ---------------------------------------------------------------------- */
+/* recv = SUM over ranks of send (elementwise). Ring reduce-scatter + allgather over RCCL
+ * send/recv with the HIP reduce kernel; recv may equal send (in place). Stream-ordered. */
+int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements,
+                  int dtype, int op, void *hip_stream);
+
+/* Comparator entry for measurement: variant 0 = the engine's ring (= ddl_allreduce),
+ * variant 1 = RCCL's built-in ncclAllReduce on the same communicator. */
+int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements,
+                          int dtype, int op, void *hip_stream, int variant);
+
+/* Keyed asynchronous request (TF op Allreduce semantics): registered under `key`,
+ * negotiated across ranks, fused by dtype in lexicographic key order, then `done` fires.
+ * `in`/`out` must stay valid until `done`. Work is ordered after `hip_stream`'s current
+ * position; `done` fires once `out` is final. */
+int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
+                         size_t elements, int dtype, int op, void *hip_stream,
+                         ddl_done_fn done, void *user);
+/* Blocks until every request submitted on `id` so far has completed. */
+int ddl_wait_all(ddl_communicator_id id);
+
+/* Measurement: bracket every reduce-kernel launch of ddl_allreduce on `id` with timing
+ * events on the engine's compute stream (the stream the kernel runs on). ddl_kernel_stats
+ * waits for the recorded events and returns launches, algorithmic HBM bytes
+ * (3 * elements * sizeof(T) per launch) and summed kernel milliseconds, then resets. */
+int ddl_kernel_timing(ddl_communicator_id id, int on);
+int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes, double *ms);
+
+/* ---- HIP kernels exposed for measurement and tests ----------------------------------- */
+/* acc[i] = acc[i] + in[i]  (the per-hop reduce of the ring). */
+int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void *hip_stream);
+/* out[i] = a[i] + b[i]; out may alias a or b. */
+int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype,
+                    void *hip_stream);
+/* Kernel variant selection for measurement: 0 = default (register streaming),
+ * 1 = incoming operand staged through LDS by global_load_lds, 2 = non-temporal. */
+int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b,
+                            size_t elements, int dtype, void *hip_stream);
+
+/* Fusion pack/unpack (device): gathers `count` segments into one contiguous buffer and
+ * scatters it back (executeCommunicatePlan_'s memcpy in/out, MPIRingTokenCommunication.cc:548-733). */
+int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream);
+int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int count,
+               void *hip_stream);
+
+/* ---- single-GPU rehearsal of the ring schedule --------------------------------------- */
+/* Runs the exact per-rank ring schedule for `nranks` virtual ranks inside this process on
+ * the current device, with device-to-device copies standing in for RCCL send/recv.
+ * sends[r]/recvs[r] are rank r's buffers. Stream-ordered on hip_stream. */
+int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *recvs,
+                             size_t elements, int dtype, int op, void *hip_stream);
+
+/* ---- schedule introspection (host only, no GPU needed) -------------------------------- */
+int ddl_ring_count(int nranks, int max_rings);
+/* perm_out[p] = rank at ring position p (length nranks). */
+int ddl_ring_perm(int nranks, int max_rings, int ring, int *perm_out);
+/* Element range [begin, end) of (ring, chunk) in a bucket of `elements` of `dtype`. */
+int ddl_chunk_range(size_t elements, int dtype, int nranks, int rings, int ring, int chunk,
+                    size_t *begin, size_t *end);
+/* Rings and reduce-scatter slices the schedule uses for a bucket under the current config. */
+int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slices);
+/* Rank `rank`'s ring program as rows of 8 int64:
+ *   send/recv: {tick, 0=send|1=recv, peer, ring, buffer(0 in, 1 out, 2 staging), offset, count, wait_tick}
+ *   reduce:    {tick, 2, -1, segment, 1 (out), offset, count, staging offset}  (out = in + staging)
+ * Offsets and counts in elements. Host only. */
+int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out,
+                     size_t max_ops, size_t *nops);
+/* Fusion plans (requestBegin, elementBegin, requestEnd, elementEnd) over `count` requests of
+ * one dtype group, capped at `limit` bytes (makeCollectiveCommunicatePlan,
+ * MPIRingTokenCommunication.cc:495-546). plans_out holds 4*max_plans entries. */
+int ddl_make_plans(const size_t *elements, const size_t *esizes, size_t count, size_t limit,
+                   size_t *plans_out, size_t max_plans, size_t *nplans);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DDL_AMD_H */

@@ -1,0 +1,165 @@
+"""Test helpers: ctypes wrapper of the oracle (oracle/ddl_oracle.c) and data generators.
+
+The oracle is the checker only; nothing here is imported by the product.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_LIB = os.path.join(ROOT, 'oracle', 'build', 'libddl_oracle.so')
+
+DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_BFLOAT16, DT_HALF, DT_UINT64 = 1, 2, 3, 9, 14, 19, 23
+# numpy storage type per dtype code (bf16 is stored as raw uint16)
+NP = {DT_FLOAT: np.float32, DT_DOUBLE: np.float64, DT_INT32: np.int32, DT_INT64: np.int64,
+      DT_HALF: np.float16, DT_BFLOAT16: np.uint16, DT_UINT64: np.uint64}
+NAME = {DT_FLOAT: 'float32', DT_DOUBLE: 'float64', DT_INT32: 'int32', DT_INT64: 'int64',
+        DT_HALF: 'float16', DT_BFLOAT16: 'bfloat16', DT_UINT64: 'uint64'}
+ALL_DTYPES = [DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_HALF, DT_BFLOAT16, DT_UINT64]
+FROM_NP = {'float32': DT_FLOAT, 'float64': DT_DOUBLE, 'int32': DT_INT32, 'int64': DT_INT64,
+           'uint64': DT_UINT64, 'float16': DT_HALF}
+
+SZ = ctypes.c_size_t
+
+
+def ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Oracle:
+    def __init__(self, path=ORACLE_LIB):
+        self.lib = L = ctypes.CDLL(path)
+        L.ddlo_sum2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, SZ]
+        L.ddlo_allreduce_seq.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.c_void_p, SZ]
+        L.ddlo_allreduce_ring.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, SZ]
+        L.ddlo_chunk_range.argtypes = [SZ, SZ, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
+        L.ddlo_make_plan.argtypes = [ctypes.POINTER(SZ), ctypes.POINTER(SZ), SZ, SZ, ctypes.POINTER(SZ), SZ]
+        L.ddlo_make_plan.restype = ctypes.c_long
+        L.ddlo_dtype_size.argtypes = [ctypes.c_int]
+        L.ddlo_dtype_size.restype = SZ
+        L.ddlo_reduce_reps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, SZ, ctypes.c_int]
+        L.ddlo_half_to_float.argtypes = [ctypes.c_uint16]
+        L.ddlo_half_to_float.restype = ctypes.c_float
+        L.ddlo_float_to_half.argtypes = [ctypes.c_float]
+        L.ddlo_float_to_half.restype = ctypes.c_uint16
+        L.ddlo_float_to_bf16.argtypes = [ctypes.c_float]
+        L.ddlo_float_to_bf16.restype = ctypes.c_uint16
+
+    def sum2(self, dt, a, b):
+        a = np.ascontiguousarray(a)
+        b = np.ascontiguousarray(b)
+        out = np.empty_like(a)
+        assert self.lib.ddlo_sum2(dt, ptr(out), ptr(a), ptr(b), a.size) == 0
+        return out
+
+    def allreduce_seq(self, dt, xs):
+        xs = [np.ascontiguousarray(x) for x in xs]
+        out = np.empty_like(xs[0])
+        arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
+        assert self.lib.ddlo_allreduce_seq(dt, len(xs), arr, ptr(out), xs[0].size) == 0
+        return out
+
+    def allreduce_ring(self, dt, xs, perms):
+        xs = [np.ascontiguousarray(x) for x in xs]
+        P, R = len(xs), len(perms)
+        flat = (ctypes.c_int * (P * R))(*[v for p in perms for v in p])
+        out = np.empty_like(xs[0])
+        arr = (ctypes.c_void_p * P)(*[x.ctypes.data for x in xs])
+        assert self.lib.ddlo_allreduce_ring(dt, P, R, flat, arr, ptr(out), xs[0].size) == 0
+        return out
+
+    def chunk_range(self, n, esize, P, R, ring, chunk):
+        b, e = SZ(), SZ()
+        assert self.lib.ddlo_chunk_range(n, esize, P, R, ring, chunk, ctypes.byref(b), ctypes.byref(e)) == 0
+        return b.value, e.value
+
+    def make_plan(self, elements, esizes, limit, max_plans=4096):
+        n = len(elements)
+        el = (SZ * n)(*elements)
+        es = (SZ * n)(*esizes)
+        out = (SZ * (4 * max_plans))()
+        k = self.lib.ddlo_make_plan(el, es, n, limit, out, max_plans)
+        assert k >= 0
+        return [tuple(out[4 * i:4 * i + 4]) for i in range(k)]
+
+
+def random_input(dt, n, seed, kind='randn'):
+    """Seeded synthetic gradient bucket of dtype code dt."""
+    rng = np.random.default_rng(seed)
+    if dt in (DT_INT32, DT_INT64, DT_UINT64):
+        info = np.iinfo(NP[dt])
+        return rng.integers(info.min, info.max, size=n, dtype=NP[dt], endpoint=True)
+    if kind == 'exact':  # k * 2^-10, |k| < 2^12: sums of up to 2^11 terms are exact in fp32
+        k = rng.integers(-(2 ** 12) + 1, 2 ** 12, size=n)
+        x = k * 2.0 ** -10
+    else:
+        x = rng.standard_normal(n)
+    if dt == DT_BFLOAT16:
+        f = x.astype(np.float32).view(np.uint32)
+        return ((f + 0x7FFF + ((f >> 16) & 1)) >> 16).astype(np.uint16)
+    if dt == DT_HALF:
+        return (0.25 * x).astype(np.float16)
+    return x.astype(NP[dt])
+
+
+def ring_perms(lib, P, R, max_rings=8):
+    perms = []
+    buf = (ctypes.c_int * P)()
+    for j in range(R):
+        assert lib.ddl_ring_perm(P, max_rings, j, buf) == 0
+        perms.append(list(buf))
+    return perms
+
+
+def ring_shape(lib, n, dt, P):
+    r, k = ctypes.c_int(), ctypes.c_int()
+    assert lib.ddl_ring_shape(n, dt, P, ctypes.byref(r), ctypes.byref(k)) == 0
+    return r.value, k.value
+
+
+def ring_program(lib, rank, P, n, dt):
+    cap = 1 << 16
+    buf = (ctypes.c_longlong * (8 * cap))()
+    nops = SZ()
+    st = lib.ddl_ring_program(rank, P, n, dt, buf, cap, ctypes.byref(nops))
+    assert st == 0, lib.ddl_last_error()
+    return np.frombuffer(buf, dtype=np.int64, count=8 * nops.value).reshape(-1, 8).copy()
+
+
+def simulate_ring(oracle, lib, dt, xs):
+    """Execute every rank's ring program (from the engine's own schedule) on host buffers:
+    sends/recvs matched by (tick, peer, ring), reduces through the oracle's operator."""
+    P, n = len(xs), xs[0].size
+    progs = [ring_program(lib, r, P, n, dt) for r in range(P)]
+    R, _ = ring_shape(lib, n, dt, P)
+    stride = max((e - b for b, e in (oracle.chunk_range(n, xs[0].itemsize, P, R, j, c)
+                                     for j in range(R) for c in range(P))), default=0)
+    stride = (stride + 63) & ~63
+    bufs = [[x.copy(), np.zeros_like(x), np.zeros(max(R * stride, 1), dtype=x.dtype)] for x in xs]
+    T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
+    for t in range(T):
+        sends = {}
+        for r in range(P):
+            for row in progs[r][progs[r][:, 0] == t]:
+                if row[1] == 0:
+                    _, _, peer, ring, b, off, cnt, _ = row
+                    sends[(r, peer, ring)] = bufs[r][b][off:off + cnt].copy()
+        for r in range(P):
+            for row in progs[r][progs[r][:, 0] == t]:
+                if row[1] == 1:
+                    _, _, peer, ring, b, off, cnt, _ = row
+                    data = sends.pop((peer, r, ring))
+                    assert data.size == cnt
+                    bufs[r][b][off:off + cnt] = data
+        assert not sends, f'unmatched sends at tick {t}: {list(sends)}'
+        for r in range(P):
+            for row in progs[r][progs[r][:, 0] == t]:
+                if row[1] == 2:
+                    _, _, _, _, b, off, cnt, soff = row
+                    bufs[r][1][off:off + cnt] = oracle.sum2(dt, bufs[r][0][off:off + cnt],
+                                                            bufs[r][2][soff:soff + cnt])
+    return [b[1] for b in bufs]

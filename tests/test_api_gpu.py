@@ -1,0 +1,161 @@
+"""The reference's operator surface on the GPU at world size 1 (one process per GPU):
+Communicator, allreduce / allreduce_gradient, keyed async requests with fusion, the
+data-parallel optimizer wrapper. At size 1 the sum is the tensor itself (the reference hangs
+there; the build defines out = in)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def world(gpu):
+    from ddl.torch.communicator import Communicator
+    return Communicator.world()
+
+
+def test_world_communicator(world, lib):
+    assert world.rank == 0 and world.size == 1
+    assert world.id == lib.world_communicator() != 0
+
+
+def test_allreduce_returns_new_tensor(world):
+    from ddl.torch.tensor_communicate import allreduce
+    x = torch.randn(1000, 7, device='cuda')
+    y = allreduce(x, world)
+    assert y.data_ptr() != x.data_ptr() and torch.equal(x, y)
+
+
+def test_allreduce_host_tensor(world):
+    from ddl.torch.tensor_communicate import allreduce
+    x = torch.randn(4099)
+    y = allreduce(x, world)
+    assert not y.is_cuda and torch.equal(x, y)
+
+
+def test_allreduce_gradient_mean(world):
+    from ddl.torch.tensor_communicate import allreduce_gradient
+    x = torch.randn(333, device='cuda', dtype=torch.float16)
+    assert torch.equal(allreduce_gradient(x, world), x)
+
+
+def test_unsupported_dtype_raises(world):
+    from ddl.torch.tensor_communicate import allreduce
+    with pytest.raises(TypeError):
+        allreduce(torch.ones(4, dtype=torch.int8, device='cuda'), world)
+
+
+@pytest.mark.parametrize('threshold', [(1 << 31) - 1, 4096 + 1, 777])
+def test_keyed_requests_fused(world, lib, threshold):
+    """Many keyed requests of mixed dtypes: negotiated (size 1: all pending), grouped by dtype,
+    fused into plans capped at the threshold, packed/unpacked — outputs equal inputs."""
+    from ddl.torch.tensor_communicate import allreduce_async, wait_all
+    old = lib.ddl_get_config(b'fusion_threshold_bytes')
+    assert lib.ddl_set_config(b'fusion_threshold_bytes', threshold) == 0
+    try:
+        rng = np.random.default_rng(0)
+        tensors, handles = [], []
+        for i in rng.permutation(200):
+            n = int(rng.integers(0, 5000))
+            dt = [torch.float32, torch.float16, torch.int32, torch.bfloat16, torch.float64][i % 5]
+            t = (torch.randn(n, device='cuda') * 100).to(dt)
+            tensors.append(t)
+            handles.append(allreduce_async(t, f'grad_{i:05d}', world))
+        for t, h in zip(tensors, handles):
+            assert torch.equal(h.wait(timeout=60), t)
+        wait_all(world)
+    finally:
+        lib.ddl_set_config(b'fusion_threshold_bytes', old)
+
+
+def test_keyed_duplicate_key_rejected(world):
+    from ddl.torch.cpp_backend import DDLError
+    from ddl.torch.tensor_communicate import allreduce_async
+    # hold the handler busy is not needed: a duplicate pending key is rejected at submit when
+    # the first one is still registered; submit twice quickly and accept either outcome of the
+    # race, but a reject must carry DUPLICATE_KEY.
+    t = torch.randn(10, device='cuda')
+    h = allreduce_async(t, 'dup_key', world)
+    try:
+        h2 = allreduce_async(t, 'dup_key', world)
+        h2.wait(60)
+    except DDLError as e:
+        assert e.status == 7
+    h.wait(60)
+
+
+def test_done_callbacks_fire_in_reference_order(world, lib):
+    """done() order: dtype groups ascending (float32=1 < float64=2 < int32=3 < half=19),
+    keys lexicographic inside a group (MPIRingTokenCommunication.cc:105-157, 735-749)."""
+    from ddl.torch import cpp_backend as cb
+    order = []
+
+    @cb.DONE_FN
+    def done(status, user):
+        order.append(user)
+
+    api = cb.CPPBackend.c_api()
+    keep = []
+    block = torch.cuda.Stream()
+    # park the handler behind a long kernel so all requests are pending together
+    with torch.cuda.stream(block):
+        big = torch.randn(1 << 24, device='cuda')
+        for _ in range(20):
+            big = big * 1.0001
+        specs = [('b', torch.float16), ('a', torch.float64), ('c', torch.float32), ('a', torch.float32),
+                 ('z', torch.int32), ('m', torch.float16)]
+        for i, (k, dt) in enumerate(specs):
+            t = torch.ones(100, device='cuda', dtype=dt)
+            keep.append(t)
+            from ddl.torch.util import ddl_dtype
+            st = api.ddl_allreduce_submit(world.id, f'{k}{i}'.encode(), t.data_ptr(), t.data_ptr(), t.numel(),
+                                          ddl_dtype(t), 0, block.cuda_stream, done, i)
+            assert st == 0
+    assert api.ddl_wait_all(world.id) == 0
+    names = [f'{specs[i][0]}{i}' for i in order]
+    dts = [specs[i][1] for i in order]
+    rank = {torch.float32: 1, torch.float64: 2, torch.int32: 3, torch.float16: 19}
+    assert [rank[d] for d in dts] == sorted(rank[d] for d in dts)
+    for d in set(dts):
+        grp = [n for n, x in zip(names, dts) if x == d]
+        assert grp == sorted(grp)
+    assert len(order) == len(specs)
+
+
+def test_dp_optimizer_wrapper_size1(world):
+    from ddl.torch.parallelism.data import data_parallelism_distributed_optimizer_wrapper
+    torch.manual_seed(0)
+    m = torch.nn.Linear(16, 4).cuda()
+    ref = torch.nn.Linear(16, 4).cuda()
+    ref.load_state_dict(m.state_dict())
+    opt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(m.parameters(), lr=0.1), world)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    assert opt.is_distributed_optimizer and isinstance(opt, torch.optim.SGD)
+    x = torch.randn(8, 16, device='cuda')
+    for mod, o in ((m, opt), (ref, ref_opt)):
+        o.zero_grad()
+        mod(x).square().sum().backward()
+        o.step()
+    for a, b in zip(m.parameters(), ref.parameters()):
+        assert torch.equal(a, b)
+
+
+def test_split_size1(world):
+    sub = world.split_communicator(0)
+    assert sub.size == 1 and sub.rank == 0
+    from ddl.torch.tensor_communicate import allreduce
+    x = torch.arange(10.0, device='cuda')
+    assert torch.equal(allreduce(x, sub), x)
+    sub.detach()
+
+
+def test_rccl_comparator_entry_size1(world, lib):
+    x = torch.randn(1000, device='cuda')
+    y = torch.empty_like(x)
+    assert lib.ddl_allreduce_variant(world.id, x.data_ptr(), y.data_ptr(), 1000, 1, 0,
+                                     torch.cuda.current_stream().cuda_stream, 1) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)

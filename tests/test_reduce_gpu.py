@@ -1,0 +1,123 @@
+"""Per-hop reduce kernel (reduce_kernels.hip) vs the oracle's MPI_SUM operator: bit-exact for
+every dtype (fp16/bf16: one rounding per add, identical to round(float(a)+float(b)))."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import ALL_DTYPES, DT_BFLOAT16, DT_FLOAT, DT_HALF, NAME, NP, random_input
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 3, 4, 5, 63, 64, 65, 255, 256, 1000, 4097, 65_536 + 3, 1 << 20, (1 << 22) + 13]
+
+
+def to_dev(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def from_dev(t, like):
+    return t.cpu().numpy().view(like.dtype)
+
+
+@pytest.mark.parametrize('dt', ALL_DTYPES, ids=lambda d: NAME[d])
+@pytest.mark.parametrize('n', SIZES)
+def test_sum2_bit_exact(lib, oracle, gpu, dt, n):
+    a, b = random_input(dt, n, 11), random_input(dt, n, 12)
+    ta, tb, to = to_dev(a, gpu), to_dev(b, gpu), torch.empty(max(n, 1), dtype=to_dev(a[:0], gpu).dtype, device=gpu)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.ddl_reduce_sum2(to.data_ptr(), ta.data_ptr(), tb.data_ptr(), n, dt, s) == 0
+    torch.cuda.synchronize()
+    want = oracle.sum2(dt, a, b)
+    assert from_dev(to[:n], a).tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize('dt', ALL_DTYPES, ids=lambda d: NAME[d])
+def test_reduce_local_in_place(lib, oracle, gpu, dt):
+    n = 300_001
+    a, b = random_input(dt, n, 21), random_input(dt, n, 22)
+    ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+    assert lib.ddl_reduce_local(ta.data_ptr(), tb.data_ptr(), n, dt, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert from_dev(ta, a).tobytes() == oracle.sum2(dt, a, b).tobytes()
+
+
+@pytest.mark.parametrize('variant', [0, 1, 2])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_HALF, DT_BFLOAT16, 3, 2], ids=lambda d: str(d))
+def test_variants_agree(lib, oracle, gpu, variant, dt):
+    n = (1 << 20) + 77
+    a, b = random_input(dt, n, 31), random_input(dt, n, 32)
+    ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+    to = torch.empty_like(ta)
+    assert lib.ddl_reduce_sum2_variant(variant, to.data_ptr(), ta.data_ptr(), tb.data_ptr(), n, dt,
+                                       torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert from_dev(to, a).tobytes() == oracle.sum2(dt, a, b).tobytes()
+
+
+@pytest.mark.parametrize('offset', [1, 2, 3])
+def test_misaligned_buffers(lib, oracle, gpu, offset):
+    """Sub-tensor views that are not 16-byte aligned take the scalar path, same result."""
+    n = 100_000
+    a, b = random_input(DT_FLOAT, n + 8, 41), random_input(DT_FLOAT, n + 8, 42)
+    ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+    to = torch.zeros_like(ta)
+    av, bv, ov = ta[offset:offset + n], tb[offset:offset + n], to[offset:offset + n]
+    assert lib.ddl_reduce_sum2(ov.data_ptr(), av.data_ptr(), bv.data_ptr(), n, DT_FLOAT,
+                               torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    want = oracle.sum2(DT_FLOAT, a[offset:offset + n], b[offset:offset + n])
+    assert to.cpu().numpy()[offset:offset + n].tobytes() == want.tobytes()
+    assert np.all(to.cpu().numpy()[:offset] == 0)
+
+
+def test_special_values(lib, oracle, gpu):
+    """inf, nan, signed zeros, denormals and fp16 overflow follow IEEE exactly as the oracle."""
+    f = np.array([np.inf, -np.inf, np.nan, 0.0, -0.0, 1e-45, -1e-45, 3.4e38, 3.4e38, 1.0], np.float32)
+    g = np.array([1.0, np.inf, 1.0, -0.0, -0.0, 1e-45, 1e-45, 3.4e38, -3.4e38, -1.0], np.float32)
+    for dt, cast in ((DT_FLOAT, np.float32), (DT_HALF, np.float16)):
+        a, b = f.astype(cast), g.astype(cast)
+        if dt == DT_HALF:
+            a = np.concatenate([a, np.array([65504, 6e-8, -6e-8], np.float16)])
+            b = np.concatenate([b, np.array([16, 6e-8, 0], np.float16)])
+        ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+        to = torch.empty_like(ta)
+        assert lib.ddl_reduce_sum2(to.data_ptr(), ta.data_ptr(), tb.data_ptr(), a.size, dt,
+                                   torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        got, want = from_dev(to, a), oracle.sum2(dt, a, b)
+        bits = np.uint16 if dt == DT_HALF else np.uint32
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(got), nan)
+        assert np.array_equal(got.view(bits)[~nan], want.view(bits)[~nan])
+
+
+def test_int32_wraparound(lib, oracle, gpu):
+    a = np.array([2 ** 31 - 1, -2 ** 31, -1, 123], np.int32)
+    b = np.array([1, -1, 1, -123], np.int32)
+    ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+    assert lib.ddl_reduce_local(ta.data_ptr(), tb.data_ptr(), 4, 3, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert ta.cpu().numpy().tolist() == [-2 ** 31, 2 ** 31 - 1, 0, 0]
+
+
+def test_pack_unpack_roundtrip(lib, gpu):
+    rng = np.random.default_rng(5)
+    sizes = [int(s) for s in rng.integers(1, 70_000, size=150)] + [4, 16, 256, 4096]
+    srcs = [torch.from_numpy(rng.integers(0, 255, size=s, dtype=np.uint8)).to(gpu) for s in sizes]
+    total = sum((s + 255) // 256 * 256 for s in sizes)
+    fused = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    P = ctypes.c_void_p * len(sizes)
+    S = ctypes.c_size_t * len(sizes)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert lib.ddl_pack(fused.data_ptr(), P(*[t.data_ptr() for t in srcs]), S(*sizes), len(sizes), stream) == 0
+    outs = [torch.zeros_like(t) for t in srcs]
+    assert lib.ddl_unpack(P(*[t.data_ptr() for t in outs]), fused.data_ptr(), S(*sizes), len(sizes), stream) == 0
+    torch.cuda.synchronize()
+    off = 0
+    f = fused.cpu().numpy()
+    for s, src, out in zip(sizes, srcs, outs):
+        assert np.array_equal(f[off:off + s], src.cpu().numpy())
+        assert torch.equal(out, src)
+        off += (s + 255) // 256 * 256

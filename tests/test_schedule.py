@@ -1,0 +1,126 @@
+"""The ring schedule (host side of the engine, no GPU): ring construction, bucket partition,
+per-rank programs and fusion plans — each checked against the oracle's restatement."""
+import itertools
+
+import numpy as np
+import pytest
+
+from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, DT_INT32, NP, random_input, ring_perms, ring_program,
+                      ring_shape, simulate_ring)
+
+SZ_OF = {1: 4, 2: 8, 3: 4, 9: 8, 14: 2, 19: 2, 23: 8}
+
+
+@pytest.mark.parametrize('P', range(1, 9))
+def test_rings_are_edge_disjoint_hamiltonian_cycles(lib, P):
+    R = lib.ddl_ring_count(P, 8)
+    expected = {1: 1, 2: 1, 3: 2, 4: 2, 5: 4, 6: 4, 7: 6, 8: 7}[P]
+    assert R == expected  # P-1 except K4*/K6* (Tillson), natural ring only at P<=2
+    perms = ring_perms(lib, P, R)
+    assert perms[0] == list(range(P))  # ring 0 = the reference's token direction r -> r+1
+    edges = set()
+    for p in perms:
+        assert sorted(p) == list(range(P))
+        for i in range(P if P > 1 else 0):
+            e = (p[i], p[(i + 1) % P])
+            if P > 2:
+                assert e not in edges
+            edges.add(e)
+
+
+@pytest.mark.parametrize('n', [0, 1, 63, 64, 65, 1000, 4099, 1 << 16, 3 * (1 << 20) + 7])
+@pytest.mark.parametrize('P', [2, 3, 4, 8])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_HALF, 2])
+def test_chunk_partition_matches_oracle_and_tiles_bucket(lib, oracle, n, P, dt):
+    import ctypes
+    R, _ = ring_shape(lib, n, dt, P)
+    es = SZ_OF[dt]
+    covered = []
+    for j in range(R):
+        for c in range(P):
+            b, e = ctypes.c_size_t(), ctypes.c_size_t()
+            assert lib.ddl_chunk_range(n, dt, P, R, j, c, ctypes.byref(b), ctypes.byref(e)) == 0
+            assert (b.value, e.value) == oracle.chunk_range(n, es, P, R, j, c)
+            assert (b.value * es) % 256 == 0  # granule-aligned starts
+            covered.append((b.value, e.value))
+    pos = 0
+    for b, e in covered:  # contiguous, in order, covering [0, n)
+        assert b == pos or e <= b
+        pos = max(pos, e)
+    assert pos == n
+
+
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 8])
+@pytest.mark.parametrize('n', [1, 100, 4099, 50_000])
+@pytest.mark.parametrize('dt', ALL_DTYPES)
+def test_ring_programs_compute_the_ring_order_sum(lib, oracle, P, n, dt):
+    """All P per-rank programs, executed with matched sends/recvs, give the oracle's
+    ring-order result bit for bit on every rank."""
+    xs = [random_input(dt, n, 1234 + 7919 * r) for r in range(P)]
+    outs = simulate_ring(oracle, lib, dt, xs)
+    R, _ = ring_shape(lib, n, dt, P)
+    want = oracle.allreduce_ring(dt, xs, ring_perms(lib, P, R))
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_ring_program_slices_and_dependencies(lib):
+    """Reduce-scatter ticks: every send of step s>0 waits on the reduce of step s-1 that produced
+    it; staging offsets stay inside the staging buffer; each rank sends and receives the same
+    byte volume 2(P-1)/P * S (the ring's wire cost)."""
+    P, n, dt = 8, 256 << 20 >> 2, DT_FLOAT  # 256 MiB fp32 (C3)
+    R, K = ring_shape(lib, n, dt, P)
+    assert R == 7 and K >= 2
+    for rank in range(P):
+        prog = ring_program(lib, rank, P, n, dt)
+        sent = prog[prog[:, 1] == 0][:, 6].sum()
+        recv = prog[prog[:, 1] == 1][:, 6].sum()
+        expect = 2 * (P - 1) * n / P
+        assert abs(sent - expect) <= 2 * R * P * 64 and abs(recv - expect) <= 2 * R * P * 64
+        rs_ticks = (P - 1) * K
+        for row in prog[(prog[:, 1] == 0) & (prog[:, 0] < rs_ticks)]:
+            t = row[0]
+            if t >= K:
+                assert row[7] == t - K and row[4] == 1  # forwards the previous step's output
+            else:
+                assert row[7] == -1 and row[4] == 0  # step 0 sends the rank's own input
+
+
+def test_plans_match_reference_plan_walk(lib, oracle):
+    """makeCollectiveCommunicatePlan (MPIRingTokenCommunication.cc:495-546) restated in the
+    oracle vs the engine's make_plans, on cases where the reference's walk is well defined
+    (odd byte caps with even element sizes, as its 2^31-1 cap)."""
+    import ctypes
+    rng = np.random.default_rng(3)
+    for trial in range(300):
+        k = int(rng.integers(1, 12))
+        esz = [int(rng.choice([2, 4, 8]))] * k  # one dtype group
+        el = [int(rng.integers(0, 5000)) for _ in range(k)]
+        el[0] = max(el[0], 1)
+        limit = int(rng.integers(1, 40000)) | 1
+        ref = oracle.make_plan(el, esz, limit)
+        n = len(el)
+        out = (ctypes.c_size_t * (4 * 8192))()
+        np_ = ctypes.c_size_t()
+        assert lib.ddl_make_plans((ctypes.c_size_t * n)(*el), (ctypes.c_size_t * n)(*esz), n, limit, out, 8192,
+                                  ctypes.byref(np_)) == 0
+        got = [tuple(out[4 * i:4 * i + 4]) for i in range(np_.value)]
+        assert got == ref, (el, esz, limit)
+
+
+def test_plan_cap_2gib_single_plan_for_large_bucket(oracle):
+    """With the reference's cap (2^31-1 bytes) a 256 MiB fp32 bucket is one plan (C3), and a
+    C5-like mixed set splits where the reference would."""
+    cap = (1 << 31) - 1
+    assert oracle.make_plan([64 << 20], [4], cap) == [(0, 0, 0, 64 << 20)]
+    el = [600 << 20 >> 2] * 4  # 4 x 600 MiB fp32 -> 2.34 GiB -> two plans
+    plans = oracle.make_plan(el, [4] * 4, cap)
+    assert len(plans) == 2 and plans[0][2] == 3 and plans[1][0] == 3
+
+
+def test_token_key_order_is_bytewise_lexicographic():
+    """std::set<pair<string,string>> order (RingTokenCommunicateHandler.cc:365-400) is bytewise:
+    the engine keeps pending requests in a std::map<std::string,...> — same order as Python
+    sorting of bytes keys."""
+    keys = [b'grad_00010', b'grad_9', b'Grad_1', b'grad_\xc3\xa9', b'grad_0001']
+    assert sorted(keys) == [b'Grad_1', b'grad_0001', b'grad_00010', b'grad_9', b'grad_\xc3\xa9']
