@@ -40,9 +40,11 @@ def parse():
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--bucket-mib', type=int, default=256)
     ap.add_argument('--no-sweep', action='store_true')
+    ap.add_argument('--no-variants', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
-    ap.add_argument('--variant', type=int, default=0, help='reduce kernel variant (0 reg, 1 lds, 2 nt)')
+    ap.add_argument('--variant', type=int, default=-1,
+                    help='reduce kernel variant bits (-1 default; 1 nt-load a, 2 nt-load b, 4 nt-store, 8 lds b)')
     return ap.parse_args()
 
 
@@ -79,6 +81,12 @@ def cpu_baseline(n_bytes_sample, seconds):
                       f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM on the reference data plane'}
 
 
+NSETS = 3  # rotating buffer sets: >= 2 x 768 MiB of traffic between reuses of one set, so the
+           # 256 MiB Infinity Cache cannot serve a re-read (MI355X_MICROARCH.md §Infinity Cache)
+VARIANTS = {'default': -1, 'plain': 0, 'nt_load_a': 1, 'nt_load_ab': 3, 'nt_all': 7, 'lds_stage_b': 8,
+            'lds_stage_b_nt_a': 9}
+
+
 def single_gpu(args):
     import torch
     from ddl.torch.cpp_backend import CPPBackend, check
@@ -88,14 +96,26 @@ def single_gpu(args):
     S = args.bucket_mib << 20
     n = S // 4
     g = torch.Generator(device=dev).manual_seed(1234)
-    acc = torch.rand(n, device=dev, generator=g) * 2 - 1
-    inp = torch.rand(n, device=dev, generator=g) * 2 - 1
+    sets = [((torch.rand(n, device=dev, generator=g) * 2 - 1), (torch.rand(n, device=dev, generator=g) * 2 - 1))
+            for _ in range(NSETS)]
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    counter = [0]
 
-    def step(a=acc, b=inp, m=n, variant=args.variant):
-        check(lib.ddl_reduce_sum2_variant(variant, a.data_ptr(), a.data_ptr(), b.data_ptr(), m, DT_FLOAT, sh),
+    def step(m=n, variant=args.variant, bufs=sets):
+        acc, inp = bufs[counter[0] % len(bufs)]
+        counter[0] += 1
+        check(lib.ddl_reduce_sum2_variant(variant, acc.data_ptr(), acc.data_ptr(), inp.data_ptr(), m, DT_FLOAT, sh),
               'ddl_reduce_sum2_variant')
+
+    def timed_kernel_ms(reps, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            step(**kw)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
 
     for _ in range(args.warmup):
         step()
@@ -114,41 +134,26 @@ def single_gpu(args):
     achieved = 3.0 * S / (kernel_ms / 1e3) / 1e9
 
     extra = {}
-    # kernel variants at the same size (interleaved in one process, guide §5.4 rule 24)
-    variants = {}
-    for v in (0, 1, 2):
-        times = []
+    if not args.no_variants:  # interleaved rounds in one process (guide §5.4 rule 24)
+        best = {k: float('inf') for k in VARIANTS}
         for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(10):
-                step(variant=v)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1) / 10)
-        variants[['reg_stream', 'lds_stage', 'nontemporal'][v]] = round(3.0 * S / (min(times) / 1e3) / 1e9, 1)
-    extra['variants_achieved_GBs'] = variants
+            for k, v in VARIANTS.items():
+                best[k] = min(best[k], timed_kernel_ms(12, variant=v))
+        extra['variants_achieved_GBs'] = {k: round(3.0 * S / (t / 1e3) / 1e9, 1) for k, t in best.items()}
 
     if not args.no_sweep:
         sweep = []
         size = 4 << 10
         while size <= (1 << 30):
             m = size // 4
-            a = torch.zeros(m, device=dev)
-            b = torch.ones(m, device=dev)
-            reps = int(min(2000, max(5, (64 << 20) // size * 4)))
+            bufs = [(torch.zeros(m, device=dev), torch.ones(m, device=dev)) for _ in range(NSETS)]
+            reps = int(min(3000, max(6, (256 << 20) // size)))
             for _ in range(3):
-                step(a, b, m)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                step(a, b, m)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            t = e0.elapsed_time(e1) / reps / 1e3
+                step(m=m, bufs=bufs)
+            t = timed_kernel_ms(reps, m=m, bufs=bufs) / 1e3
             sweep.append({'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
                           'hbm_GBs': round(3 * size / t / 1e9, 1)})
-            del a, b
+            del bufs
             size *= 4
         extra['sweep_fp32'] = sweep
 
@@ -165,13 +170,13 @@ def single_gpu(args):
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'synthetic U(-1,1) fp32 bucket, resident in HBM',
+        'data': f'synthetic U(-1,1) fp32 buckets resident in HBM, {NSETS} rotating buffer sets',
         'config': {'workload': 'C2: local reduce kernel acc += in (per-hop ring reduce), fp32, '
                                f'{args.bucket_mib} MiB bucket, 1xMI355X',
                    'bucket_bytes': S, 'parallelism': 'none (1 GPU)'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'k_sum2_vec<float>', 'kernel_ms': round(kernel_ms, 4),
+                     'kernel': 'k_sum2_tile<DDL_FLOAT, default variant>', 'kernel_ms': round(kernel_ms, 4),
                      'algorithmic_bytes_per_launch': 3 * S,
                      'frac_of_measured_copy_peak': round(achieved / HBM_MEASURED_GBS, 4)},
     }

@@ -178,6 +178,7 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value > 0, DDL_STATUS_INVALID_ARGUMENT, "fusion threshold must be > 0");
             c.fusion_threshold_bytes = value;
         } else if (k == "log_level") c.log_level = value;
+        else if (k == "cycle_time_us") c.cycle_time_us = value;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
     });
 }
@@ -191,6 +192,7 @@ long long ddl_get_config(const char *key) {
     if (k == "max_slices") return c.max_slices;
     if (k == "fusion_threshold_bytes") return c.fusion_threshold_bytes;
     if (k == "log_level") return c.log_level;
+    if (k == "cycle_time_us") return c.cycle_time_us;
     return -1;
 }
 
@@ -327,7 +329,7 @@ int ddl_wait_all(ddl_communicator_id id) {
 int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b, size_t elements,
                             int dtype, void *hip_stream) {
     return guarded([&] {
-        DDL_REQUIRE(variant >= 0 && variant <= 2, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
+        DDL_REQUIRE(variant >= -1 && variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
         SegTable t;
         t.count = 1;
         t.a[0] = a;
@@ -339,11 +341,11 @@ int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b
 }
 
 int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype, void *hip_stream) {
-    return ddl_reduce_sum2_variant(0, out, a, b, elements, dtype, hip_stream);
+    return ddl_reduce_sum2_variant(-1, out, a, b, elements, dtype, hip_stream);
 }
 
 int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void *hip_stream) {
-    return ddl_reduce_sum2_variant(0, acc, acc, in, elements, dtype, hip_stream);
+    return ddl_reduce_sum2_variant(-1, acc, acc, in, elements, dtype, hip_stream);
 }
 
 int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream) {

@@ -96,10 +96,21 @@ struct SegTable {
     int count;
 };
 
-enum ReduceVariant { kRegStream = 0, kLdsStage = 1, kNonTemporal = 2 };
+// Reduce-kernel cache-policy / staging flags (bit set). kVariantDefault is what the engine uses;
+// the others exist for measurement (ddl_reduce_sum2_variant, bench.py, tools/reduce_tune.hip).
+enum ReduceVariant : int {
+    kNtLoadA = 1,   // non-temporal loads of operand a (the rank's own gradient: read once)
+    kNtLoadB = 2,   // non-temporal loads of operand b (the received chunk)
+    kNtStore = 4,   // non-temporal stores of out
+    kLdsStageB = 8, // operand b staged through LDS by global_load_lds_dwordx4
+    kVariantMask = 15,
+};
+int default_variant();  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2)
+int ring_variant();     // reduce-scatter step of the ring
 
 // out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.
-void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant = kRegStream);
+// variant < 0 selects default_variant().
+void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant = -1);
 // Gather/scatter segments into/out of a contiguous fusion buffer.
 void launch_pack(void *dst, const void *const *srcs, const size_t *bytes, int count,
                  hipStream_t stream);

@@ -26,6 +26,7 @@ Config &config() {
         if (const char *e = std::getenv("DDL_MAX_SLICES")) cfg->max_slices = std::atoll(e);
         if (const char *e = std::getenv("DDL_FUSION_THRESHOLD")) cfg->fusion_threshold_bytes = std::atoll(e);
         if (const char *e = std::getenv("DDL_LOG_LEVEL")) cfg->log_level = std::atoll(e);
+        if (const char *e = std::getenv("DDL_CYCLE_TIME_US")) cfg->cycle_time_us = std::atoll(e);
         return cfg;
     }();
     return *c;

@@ -26,6 +26,9 @@ struct Config {
     // fusion plan cap; the reference uses MAX_MPI_BUFFER_SIZE = 2^31 - 1 (MPIBackend.h:12)
     std::atomic<long long> fusion_threshold_bytes{(1ll << 31) - 1};
     std::atomic<long long> log_level{0};
+    // keyed requests: rank 0 waits this long after the first registration before proposing
+    // a round (0 = propose at once, as the reference's READY token does)
+    std::atomic<long long> cycle_time_us{0};
     RingConfig ring() const {
         RingConfig c;
         c.rings = (int)rings.load();

@@ -137,7 +137,7 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
                 }
                 DDL_HIP(hipEventRecord(tp.first, res_.compute));
             }
-            launch_sum2(tk.reduce, dtype, res_.compute);
+            launch_sum2(tk.reduce, dtype, res_.compute, ring_variant());
             if (timing_) {
                 DDL_HIP(hipEventRecord(tp.second, res_.compute));
                 double elems = 0;
@@ -221,7 +221,7 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
             if (!tk.has_reduce) continue;
             DDL_HIP(hipEventRecord(rr.comm_ev[t], rr.comm));
             DDL_HIP(hipStreamWaitEvent(rr.compute, rr.comm_ev[t], 0));
-            launch_sum2(tk.reduce, dtype, rr.compute);
+            launch_sum2(tk.reduce, dtype, rr.compute, ring_variant());
             DDL_HIP(hipEventRecord(rr.red_ev[t], rr.compute));
         }
     }

@@ -126,6 +126,11 @@ void RequestHandler::main_() {
                     std::unique_lock<std::mutex> lk(mu_);
                     cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
                     if (stop_) break;
+                    // optional fusion window: let more registrations join this round
+                    const long long cycle_us = config().cycle_time_us.load();
+                    if (cycle_us > 0)
+                        cv_.wait_for(lk, std::chrono::microseconds(cycle_us), [this] { return stop_; });
+                    if (stop_) break;
                     for (auto &kv : pending_) keys.push_back(kv.first);
                 }
                 if (P == 1) execute_(keys);

@@ -5,19 +5,26 @@
 // Memory-bound vector add: no MFMA. Algorithmic HBM bytes per element = 3 * sizeof(T)
 // (two reads, one write).
 //
-// Layout / mapping:
-//   * one launch covers up to kMaxSegments independent (out, a, b, n) problems — the ring
-//     issues one segment per concurrent ring — with blockIdx.y = segment;
-//   * 256-thread workgroups (4 waves of 64), every lane moves 16 B per access
-//     (global_load_dwordx4), UNROLL independent accesses per operand in flight per lane;
-//   * grid-stride over 16-byte vectors, the grid capped at 8 workgroups per CU so the launch
-//     fills all 256 CUs / 8 XCDs without a tail of tiny workgroups;
-//   * the n mod V tail is done by the first lanes of the grid (one element each), so there is
-//     no separate epilogue launch; misaligned buffers take a scalar grid-stride kernel.
+// Layout / mapping (measured in profiles/r01/reduce_tune_*.txt):
+//   * one workgroup = 256 lanes = one 4 KiB tile of each operand: lane l moves bytes
+//     [16l, 16l+16) of the tile with one global_load_dwordx4 per operand and one
+//     global_store_dwordx4. The grid has one workgroup per tile (no grid-stride loop): the
+//     dispatcher hands out workgroups in order, so the tiles in flight form one compact
+//     address window and every HBM page opened is drained by neighbouring workgroups.
+//     This measured 5.9-6.1 TB/s vs 4.6 for an 8-workgroups-per-CU grid-stride loop.
+//   * up to kMaxSegments independent (out, a, b, n) problems per launch (one per ring):
+//     blockIdx.y = segment, workgroups past a segment's last tile exit at once.
+//   * cache policy per operand: non-temporal loads of the once-read operands keep the
+//     256 MiB Infinity Cache for data that is re-read (kNtLoad*, measured +4% at 1 GiB).
+//   * the n mod V tail (V = elements per 16 B) is done by the lanes of the last tile, one
+//     element each: no epilogue launch. Misaligned buffers take a scalar grid-stride kernel.
 //   * fp16 adds with v_pk_add_f16 (IEEE, round-to-nearest-even, denormals kept) — identical to
 //     round_f16(float(a) + float(b)) because fp32 has >= 2*11+2 significand bits; bf16 adds in
 //     fp32 and rounds once (v_cvt_pk_bf16_f32).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <vector>
 
 #include "common.h"
 
@@ -29,9 +36,9 @@ using f32x4 = float __attribute__((ext_vector_type(4)));
 using f64x2 = double __attribute__((ext_vector_type(2)));
 using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 using h16x8 = _Float16 __attribute__((ext_vector_type(8)));
-using f32x2 = float __attribute__((ext_vector_type(2)));
 
 constexpr int kThreads = 256;
+constexpr uint64_t kTileVec = kThreads;  // 16-byte vectors per tile (4 KiB)
 
 template <int DT>
 struct Add;
@@ -101,70 +108,55 @@ struct Add<DDL_BFLOAT16> {
 typedef __attribute__((address_space(1))) void *gptr_t;
 typedef __attribute__((address_space(3))) void *lptr_t;
 
-template <int VARIANT>
+template <bool NT>
 __device__ __forceinline__ u32x4 load_v(const u32x4 *p) {
-    if constexpr (VARIANT == kNonTemporal) return __builtin_nontemporal_load(p);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <int VARIANT>
-__device__ __forceinline__ void store_v(u32x4 *p, u32x4 v) {
-    if constexpr (VARIANT == kNonTemporal) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 
-// out = a + b on 16-byte vectors. out may alias a or b (no __restrict__): every access of
-// a lane touches only its own vectors, loads of an unrolled group precede its stores.
-template <int DT, int VARIANT, int UNROLL>
-__global__ void __launch_bounds__(kThreads) k_sum2_vec(SegTable t) {
+// out = a + b, one 4 KiB tile per workgroup. out may alias a or b (no __restrict__): each lane
+// reads its own 16 bytes of a and b before it writes the same 16 bytes of out.
+template <int DT, int VARIANT>
+__global__ void __launch_bounds__(kThreads) k_sum2_tile(SegTable t) {
     using A = Add<DT>;
     using S = typename A::S;
-    constexpr int V = 16 / sizeof(S);
+    constexpr uint64_t V = 16 / sizeof(S);
     const int seg = blockIdx.y;
+    const uint64_t n = t.n[seg];
+    const uint64_t nv = n / V;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t i = tile * kTileVec + threadIdx.x;
     const u32x4 *a = static_cast<const u32x4 *>(t.a[seg]);
     const u32x4 *b = static_cast<const u32x4 *>(t.b[seg]);
     u32x4 *o = static_cast<u32x4 *>(t.out[seg]);
-    const uint64_t n = t.n[seg];
-    const uint64_t nv = n / V;
-    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-    const uint64_t gid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    uint64_t i = gid;
 
-    if constexpr (VARIANT == kLdsStage) {
-        // Incoming operand b staged through LDS by LDS-DMA (global_load_lds_dwordx4): each wave
-        // owns a private 1 KiB slot per unrolled access, lane l lands at slot + 16*l.
-        __shared__ __attribute__((aligned(16))) u32x4 stage[UNROLL * kThreads];
+    if constexpr ((VARIANT & kLdsStageB) != 0) {
+        // operand b through LDS by LDS-DMA: each wave owns a 1 KiB slot, lane l lands at 16*l
+        __shared__ __attribute__((aligned(16))) u32x4 stage[kThreads];
+        if (tile * kTileVec > nv) return;  // (uniform) past this segment's tiles
         const int wave = threadIdx.x >> 6;
-        for (; i + (uint64_t)(UNROLL - 1) * stride < nv; i += (uint64_t)UNROLL * stride) {
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                __builtin_amdgcn_global_load_lds((gptr_t)(b + i + (uint64_t)u * stride),
-                                                 (lptr_t)(stage + u * kThreads + wave * 64), 16, 0, 0);
-            u32x4 x[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) x[u] = a[i + (uint64_t)u * stride];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                o[i + (uint64_t)u * stride] = A::vec(x[u], stage[u * kThreads + threadIdx.x]);
+        if (i < nv)
+            __builtin_amdgcn_global_load_lds((gptr_t)(b + i), (lptr_t)(stage + wave * 64), 16, 0, 0);
+        u32x4 x = i < nv ? load_v<(VARIANT & kNtLoadA) != 0>(a + i) : u32x4{0, 0, 0, 0};
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (i < nv) {
+            u32x4 r = A::vec(x, stage[threadIdx.x]);
+            if constexpr ((VARIANT & kNtStore) != 0) __builtin_nontemporal_store(r, o + i);
+            else o[i] = r;
         }
     } else {
-        for (; i + (uint64_t)(UNROLL - 1) * stride < nv; i += (uint64_t)UNROLL * stride) {
-            u32x4 x[UNROLL], y[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                x[u] = load_v<VARIANT>(a + i + (uint64_t)u * stride);
-                y[u] = load_v<VARIANT>(b + i + (uint64_t)u * stride);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) store_v<VARIANT>(o + i + (uint64_t)u * stride, A::vec(x[u], y[u]));
+        if (i < nv) {
+            const u32x4 x = load_v<(VARIANT & kNtLoadA) != 0>(a + i);
+            const u32x4 y = load_v<(VARIANT & kNtLoadB) != 0>(b + i);
+            const u32x4 r = A::vec(x, y);
+            if constexpr ((VARIANT & kNtStore) != 0) __builtin_nontemporal_store(r, o + i);
+            else o[i] = r;
         }
     }
-    for (; i < nv; i += stride) o[i] = A::vec(a[i], b[i]);
-
-    // tail: n mod V elements, one per lane of the first wave(s) of the grid
+    // tail: the n mod V elements past the last full vector, one per lane of the tile holding nv
     const uint64_t rem = n - nv * V;
-    if (gid < rem) {
-        const uint64_t e = nv * V + gid;
+    if (rem && tile == nv / kTileVec && threadIdx.x < rem) {
+        const uint64_t e = nv * V + threadIdx.x;
         const S *as = reinterpret_cast<const S *>(t.a[seg]);
         const S *bs = reinterpret_cast<const S *>(t.b[seg]);
         S *os = reinterpret_cast<S *>(t.out[seg]);
@@ -187,26 +179,29 @@ __global__ void __launch_bounds__(kThreads) k_sum2_scalar(SegTable t) {
         o[i] = A::one(a[i], b[i]);
 }
 
-constexpr int kUnroll = 4;
+template <int DT, int V>
+void launch_variant(const SegTable &t, hipStream_t stream, int variant, dim3 grid) {
+    if constexpr (V > kVariantMask) {
+        fail(DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant");
+    } else {
+        if (variant == V) hipLaunchKernelGGL((k_sum2_tile<DT, V>), grid, dim3(kThreads), 0, stream, t);
+        else launch_variant<DT, V + 1>(t, stream, variant, grid);
+    }
+}
 
 template <int DT>
-void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned, int blocks_x) {
-    dim3 grid(blocks_x, t.count), block(kThreads);
+void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned, uint64_t max_n) {
     if (!aligned) {
-        hipLaunchKernelGGL(k_sum2_scalar<DT>, grid, block, 0, stream, t);
+        uint64_t blocks = (max_n + kThreads * 4 - 1) / (kThreads * 4);
+        const uint64_t cap = (uint64_t)device_cu_count() * 8;
+        blocks = blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
+        hipLaunchKernelGGL(k_sum2_scalar<DT>, dim3((unsigned)blocks, t.count), dim3(kThreads), 0, stream, t);
         return;
     }
-    switch (variant) {
-        case kLdsStage:
-            hipLaunchKernelGGL((k_sum2_vec<DT, kLdsStage, kUnroll>), grid, block, 0, stream, t);
-            break;
-        case kNonTemporal:
-            hipLaunchKernelGGL((k_sum2_vec<DT, kNonTemporal, kUnroll>), grid, block, 0, stream, t);
-            break;
-        default:
-            hipLaunchKernelGGL((k_sum2_vec<DT, kRegStream, kUnroll>), grid, block, 0, stream, t);
-            break;
-    }
+    constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
+    const uint64_t tiles = (max_n / V + kTileVec) / kTileVec;  // +1 vector of room for the tail
+    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << max_n << " elements");
+    launch_variant<DT, 0>(t, stream, variant, dim3((unsigned)tiles, t.count));
 }
 
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -251,57 +246,8 @@ __global__ void __launch_bounds__(kThreads) k_copy_segments(PackTable t) {
 
 int g_cu_count = 0;
 
-}  // namespace
-
-int device_cu_count() {
-    if (g_cu_count == 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            g_cu_count = cus;
-        else
-            g_cu_count = 256;
-    }
-    return g_cu_count;
-}
-
-void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) {
-    DDL_REQUIRE(t.count >= 1 && t.count <= kMaxSegments, DDL_STATUS_INVALID_ARGUMENT,
-                "segment count " << t.count << " outside [1, " << kMaxSegments << "]");
-    const size_t es = dtype_size(dtype);
-    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
-    uint64_t max_n = 0;
-    bool aligned = true;
-    for (int s = 0; s < t.count; ++s) {
-        if (t.n[s] == 0) continue;
-        DDL_REQUIRE(t.a[s] && t.b[s] && t.out[s], DDL_STATUS_INVALID_ARGUMENT, "null buffer in segment " << s);
-        max_n = t.n[s] > max_n ? t.n[s] : max_n;
-        aligned = aligned && aligned16(t.a[s]) && aligned16(t.b[s]) && aligned16(t.out[s]);
-    }
-    if (max_n == 0) return;
-    const uint64_t per_block = aligned ? (uint64_t)kThreads * kUnroll * (16 / es) : (uint64_t)kThreads * 4;
-    const uint64_t cap = (uint64_t)device_cu_count() * 8 / (uint64_t)t.count;
-    uint64_t blocks = (max_n + per_block - 1) / per_block;
-    if (blocks > cap) blocks = cap;
-    if (blocks < 1) blocks = 1;
-    switch (dtype) {
-        case DDL_FLOAT: launch_dt<DDL_FLOAT>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_DOUBLE: launch_dt<DDL_DOUBLE>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_INT32: launch_dt<DDL_INT32>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_INT64: launch_dt<DDL_INT64>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_UINT64: launch_dt<DDL_UINT64>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_HALF: launch_dt<DDL_HALF>(t, stream, variant, aligned, (int)blocks); break;
-        case DDL_BFLOAT16: launch_dt<DDL_BFLOAT16>(t, stream, variant, aligned, (int)blocks); break;
-        default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
-    }
-    DDL_HIP(hipGetLastError());
-}
-
-namespace {
 void launch_copy(const char *const *srcs, char *const *dsts, const size_t *bytes, int count,
-                 hipStream_t stream, bool to_flat_dst, char *flat) {
-    (void)to_flat_dst;
-    (void)flat;
+                 hipStream_t stream) {
     for (int base = 0; base < count; base += kPackBatch) {
         PackTable t;
         t.count = count - base < kPackBatch ? count - base : kPackBatch;
@@ -326,50 +272,101 @@ void launch_copy(const char *const *srcs, char *const *dsts, const size_t *bytes
         DDL_HIP(hipGetLastError());
     }
 }
+
 }  // namespace
 
-// Fused layout: segment i occupies [off_i, off_i + bytes_i) of dst with off_i the running sum
-// of the 256-byte-rounded sizes of the segments before it (FusionLayout in engine.cpp).
+int device_cu_count() {
+    if (g_cu_count == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            g_cu_count = cus;
+        else
+            g_cu_count = 256;
+    }
+    return g_cu_count;
+}
+
+// Standalone reduce (acc += in over whole buckets): every operand streams through once, so all
+// accesses are non-temporal (measured 6.47 TB/s vs 5.75 plain, 256 MiB fp32, rotating buffers).
+int default_variant() {
+    static int v = [] {
+        const char *e = std::getenv("DDL_REDUCE_VARIANT");
+        const int dflt = kNtLoadA | kNtLoadB | kNtStore;
+        int x = e ? std::atoi(e) : dflt;
+        return (x >= 0 && x <= kVariantMask) ? x : dflt;
+    }();
+    return v;
+}
+
+// Ring reduce-scatter step: a = the rank's own gradient (read once: non-temporal), b = the slice
+// RCCL just received (likely still in the Infinity Cache: plain), out = forwarded by the next
+// step's send (keep it cache-resident: plain store).
+int ring_variant() {
+    static int v = [] {
+        const char *e = std::getenv("DDL_RING_REDUCE_VARIANT");
+        const int dflt = kNtLoadA;
+        int x = e ? std::atoi(e) : dflt;
+        return (x >= 0 && x <= kVariantMask) ? x : dflt;
+    }();
+    return v;
+}
+
+void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) {
+    DDL_REQUIRE(t.count >= 1 && t.count <= kMaxSegments, DDL_STATUS_INVALID_ARGUMENT,
+                "segment count " << t.count << " outside [1, " << kMaxSegments << "]");
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (variant < 0) variant = default_variant();
+    DDL_REQUIRE(variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant " << variant);
+    uint64_t max_n = 0;
+    bool aligned = true;
+    for (int s = 0; s < t.count; ++s) {
+        if (t.n[s] == 0) continue;
+        DDL_REQUIRE(t.a[s] && t.b[s] && t.out[s], DDL_STATUS_INVALID_ARGUMENT, "null buffer in segment " << s);
+        max_n = t.n[s] > max_n ? t.n[s] : max_n;
+        aligned = aligned && aligned16(t.a[s]) && aligned16(t.b[s]) && aligned16(t.out[s]);
+    }
+    if (max_n == 0) return;
+    switch (dtype) {
+        case DDL_FLOAT: launch_dt<DDL_FLOAT>(t, stream, variant, aligned, max_n); break;
+        case DDL_DOUBLE: launch_dt<DDL_DOUBLE>(t, stream, variant, aligned, max_n); break;
+        case DDL_INT32: launch_dt<DDL_INT32>(t, stream, variant, aligned, max_n); break;
+        case DDL_INT64: launch_dt<DDL_INT64>(t, stream, variant, aligned, max_n); break;
+        case DDL_UINT64: launch_dt<DDL_UINT64>(t, stream, variant, aligned, max_n); break;
+        case DDL_HALF: launch_dt<DDL_HALF>(t, stream, variant, aligned, max_n); break;
+        case DDL_BFLOAT16: launch_dt<DDL_BFLOAT16>(t, stream, variant, aligned, max_n); break;
+        default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
+    }
+    DDL_HIP(hipGetLastError());
+}
+
+// Fused layout: segment i occupies [off_i, off_i + bytes_i) of the fusion buffer with off_i the
+// running sum of the 256-byte-rounded sizes of the segments before it.
 void launch_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, hipStream_t stream) {
     if (count <= 0) return;
-    const char **s = new const char *[count];
-    char **d = new char *[count];
+    std::vector<const char *> s(count);
+    std::vector<char *> d(count);
     uint64_t off = 0;
     for (int i = 0; i < count; ++i) {
         s[i] = static_cast<const char *>(srcs[i]);
         d[i] = static_cast<char *>(dst) + off;
         off += (bytes[i] + 255) & ~uint64_t(255);
     }
-    try {
-        launch_copy(s, d, bytes, count, stream, true, static_cast<char *>(dst));
-    } catch (...) {
-        delete[] s;
-        delete[] d;
-        throw;
-    }
-    delete[] s;
-    delete[] d;
+    launch_copy(s.data(), d.data(), bytes, count, stream);
 }
 
 void launch_unpack(void *const *dsts, const void *src, const size_t *bytes, int count, hipStream_t stream) {
     if (count <= 0) return;
-    const char **s = new const char *[count];
-    char **d = new char *[count];
+    std::vector<const char *> s(count);
+    std::vector<char *> d(count);
     uint64_t off = 0;
     for (int i = 0; i < count; ++i) {
         s[i] = static_cast<const char *>(src) + off;
         d[i] = static_cast<char *>(dsts[i]);
         off += (bytes[i] + 255) & ~uint64_t(255);
     }
-    try {
-        launch_copy(s, d, bytes, count, stream, false, nullptr);
-    } catch (...) {
-        delete[] s;
-        delete[] d;
-        throw;
-    }
-    delete[] s;
-    delete[] d;
+    launch_copy(s.data(), d.data(), bytes, count, stream);
 }
 
 }  // namespace ddl

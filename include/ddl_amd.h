@@ -147,8 +147,9 @@ int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void
 /* out[i] = a[i] + b[i]; out may alias a or b. */
 int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype,
                     void *hip_stream);
-/* Kernel variant selection for measurement: 0 = default (register streaming),
- * 1 = incoming operand staged through LDS by global_load_lds, 2 = non-temporal. */
+/* Kernel variant selection for measurement (bit set; -1 = the engine's default):
+ * 1 = non-temporal loads of a, 2 = non-temporal loads of b, 4 = non-temporal stores,
+ * 8 = operand b staged through LDS by global_load_lds_dwordx4. */
 int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b,
                             size_t elements, int dtype, void *hip_stream);
 

@@ -100,11 +100,9 @@ def test_done_callbacks_fire_in_reference_order(world, lib):
     api = cb.CPPBackend.c_api()
     keep = []
     block = torch.cuda.Stream()
-    # park the handler behind a long kernel so all requests are pending together
+    # a fusion window so every request registers before the handler proposes the round
+    assert api.ddl_set_config(b'cycle_time_us', 300_000) == 0
     with torch.cuda.stream(block):
-        big = torch.randn(1 << 24, device='cuda')
-        for _ in range(20):
-            big = big * 1.0001
         specs = [('b', torch.float16), ('a', torch.float64), ('c', torch.float32), ('a', torch.float32),
                  ('z', torch.int32), ('m', torch.float16)]
         for i, (k, dt) in enumerate(specs):
@@ -112,10 +110,12 @@ def test_done_callbacks_fire_in_reference_order(world, lib):
             keep.append(t)
             from ddl.torch.util import ddl_dtype
             st = api.ddl_allreduce_submit(world.id, f'{k}{i}'.encode(), t.data_ptr(), t.data_ptr(), t.numel(),
-                                          ddl_dtype(t), 0, block.cuda_stream, done, i)
+                                          ddl_dtype(t), 0, block.cuda_stream, done, i + 1)
             assert st == 0
     assert api.ddl_wait_all(world.id) == 0
-    names = [f'{specs[i][0]}{i}' for i in order]
+    api.ddl_set_config(b'cycle_time_us', 0)
+    order = [u - 1 for u in order]
+    names = [f"{specs[i][0]}{i}" for i in order]
     dts = [specs[i][1] for i in order]
     rank = {torch.float32: 1, torch.float64: 2, torch.int32: 3, torch.float16: 19}
     assert [rank[d] for d in dts] == sorted(rank[d] for d in dts)
