@@ -109,7 +109,7 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
     int R, K;
     size_t stride;
     ring_shape(n, es, size_, cfg, &R, &K, &stride);
-    void *staging = res_.ensure_staging((size_t)R * stride * es);
+    void *staging = res_.ensure_staging(staging_elems(R, stride) * es);
     build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
     res_.ensure_events(prog_.ticks.size());
 
@@ -171,7 +171,7 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
     size_t stride;
     ring_shape(n, es, P_, cfg, &R, &K, &stride);
     for (int r = 0; r < P_; ++r) {
-        void *st = res_[r]->ensure_staging((size_t)R * stride * es);
+        void *st = res_[r]->ensure_staging(staging_elems(R, stride) * es);
         build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
         res_[r]->ensure_events(progs_[r].ticks.size());
     }

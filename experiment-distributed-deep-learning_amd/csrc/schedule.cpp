@@ -194,7 +194,10 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
                     t.ops.push_back(P2POp{true, succ[j], j, const_cast<char *>(src), ss.size() * es});
                 }
                 if (rs.size()) {
-                    char *st = stb + ((size_t)j * prog.staging_stride + (rs.begin - rc.begin)) * es;
+                    // staging is double-buffered by step parity: the recv of step s never lands
+                    // in the region the reduce of step s-1 may still be reading (chunks differ
+                    // by up to one granule, so their slice boundaries differ)
+                    char *st = stb + ((size_t)(2 * j + (s & 1)) * prog.staging_stride + (rs.begin - rc.begin)) * es;
                     t.ops.push_back(P2POp{false, pred[j], j, st, rs.size() * es});
                     const int c = t.reduce.count++;
                     t.reduce.a[c] = inb + rs.begin * es;

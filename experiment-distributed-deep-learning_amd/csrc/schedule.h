@@ -57,8 +57,9 @@ struct RingConfig {
     int max_slices = 8;
 };
 
-// Per-rank tick list of one allreduce. `staging` must hold staging_elems(...) elements per
-// ring (ring j uses staging + j * stride_elems).
+// Per-rank tick list of one allreduce. `staging` must hold staging_elems(R, stride) elements:
+// two slots per ring (reduce-scatter step parity), ring j / parity q at (2j + q) * stride.
+inline size_t staging_elems(int R, size_t stride) { return 2 * (size_t)R * stride; }
 struct RingProgram {
     int P = 1, R = 1, K = 1, rank = 0;
     size_t n = 0, esize = 0;

@@ -139,7 +139,7 @@ def simulate_ring(oracle, lib, dt, xs):
     stride = max((e - b for b, e in (oracle.chunk_range(n, xs[0].itemsize, P, R, j, c)
                                      for j in range(R) for c in range(P))), default=0)
     stride = (stride + 63) & ~63
-    bufs = [[x.copy(), np.zeros_like(x), np.zeros(max(R * stride, 1), dtype=x.dtype)] for x in xs]
+    bufs = [[x.copy(), np.zeros_like(x), np.zeros(max(2 * R * stride, 1), dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
     for t in range(T):
         sends = {}

@@ -86,6 +86,49 @@ def test_ring_program_slices_and_dependencies(lib):
                 assert row[7] == -1 and row[4] == 0  # step 0 sends the rank's own input
 
 
+def _overlap(a0, a1, b0, b1):
+    return a0 < b1 and b0 < a1
+
+
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
+@pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
+def test_schedule_has_no_stream_races(lib, P, n, slice_bytes):
+    """Comm tick T runs after the reduce it waits on (W) and every earlier reduce (the compute
+    stream is in order), but concurrently with the reduces of ticks W+1..T-1. None of T's
+    sends/recvs may touch a buffer range those reduces read or write."""
+    old = lib.ddl_get_config(b'slice_bytes')
+    lib.ddl_set_config(b'slice_bytes', slice_bytes)
+    try:
+        for rank in range(P):
+            prog = ring_program(lib, rank, P, n, DT_FLOAT)
+            red = {}
+            for row in prog[prog[:, 1] == 2]:
+                red.setdefault(int(row[0]), []).append(row)
+            w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
+            for t in sorted(set(prog[:, 0].tolist())):
+                ops = prog[(prog[:, 0] == t) & (prog[:, 1] != 2)]
+                if not len(ops):
+                    continue
+                w = int(ops[0][7])
+                w = max([x for x in red if x <= w], default=-1) if w >= 0 else -1
+                w_eff = max(w_eff, w)
+                running = [r for tt, rows in red.items() if w_eff < tt < t for r in rows]
+                for op in ops:
+                    _, kind, _, _, buf, off, cnt, _ = op
+                    for r in running:
+                        _, _, _, _, _, roff, rcnt, soff = r
+                        # reduce reads in[roff:+rcnt] and staging[soff:+rcnt], writes out[roff:+rcnt]
+                        if buf == 2:
+                            assert not _overlap(off, off + cnt, soff, soff + rcnt), (rank, t, 'staging')
+                        if buf == 1:
+                            assert not _overlap(off, off + cnt, roff, roff + rcnt), (rank, t, 'out')
+                        if buf == 0 and kind == 1:
+                            raise AssertionError('recv into the input buffer')
+    finally:
+        lib.ddl_set_config(b'slice_bytes', old)
+
+
 def test_plans_match_reference_plan_walk(lib, oracle):
     """makeCollectiveCommunicatePlan (MPIRingTokenCommunication.cc:495-546) restated in the
     oracle vs the engine's make_plans, on cases where the reference's walk is well defined
