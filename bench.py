@@ -42,6 +42,10 @@ def parse():
     ap.add_argument('--no-sweep', action='store_true')
     ap.add_argument('--no-variants', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe) measurement')
+    ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
+    ap.add_argument('--watchdog-s', type=float, default=900.0, help='N>1: abort a hung run after this')
+    ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--variant', type=int, default=-1,
                     help='reduce kernel variant bits (-1 default; 1 nt-load a, 2 nt-load b, 4 nt-store, 8 lds b)')
@@ -181,12 +185,35 @@ def single_gpu(args):
                      'frac_of_measured_copy_peak': round(achieved / HBM_MEASURED_GBS, 4)},
     }
     out.update(extra)
+    if not args.no_host:
+        from ddl.torch.communicator import Communicator
+        out['host_resident'] = host_resident_rate(lib, Communicator.world(), S, reps=8)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
     print(json.dumps(out), flush=True)
 
 
+def host_resident_rate(lib, comm, S, reps):
+    """Deployment case: the bucket starts and ends in (pinned) host memory; ddl_allreduce_host
+    pipelines H2D -> device ring -> D2H in 32 MiB chunks. PCIe-inclusive rate, never `value`."""
+    import torch
+    from ddl.torch.cpp_backend import check
+    n = S // 4
+    src = torch.rand(n, pin_memory=True)
+    dst = torch.empty(n, pin_memory=True)
+    check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
+    dt = (time.perf_counter() - t0) / reps
+    return {'bucket_GiBs': round(S / GiB / dt, 2), 'ms': round(dt * 1e3, 3), 'bucket_bytes': S,
+            'path': 'pinned host -> H2D -> ring allreduce -> D2H -> pinned host, 32 MiB chunks on 3 streams',
+            'pcie_bytes_per_bucket': 2 * S}
+
+
 def multi_gpu(args):
+    import threading
+
     import torch
     import torch.distributed as dist
     from ddl.torch.communicator import Communicator
@@ -194,8 +221,18 @@ def multi_gpu(args):
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', rank))
+
+    def hung():  # a hung collective must not eat the driver's whole scaling run
+        sys.stderr.write(f'[bench rank {rank}] watchdog: no completion after {args.watchdog_s:.0f} s, aborting\n')
+        sys.stderr.flush()
+        os._exit(3)
+
+    dog = threading.Timer(args.watchdog_s, hung)
+    dog.daemon = True
+    dog.start()
     torch.cuda.set_device(local)
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('gloo', rank=rank, world_size=world)
     comm = Communicator.world()
     lib = CPPBackend.c_api()
@@ -225,9 +262,9 @@ def multi_gpu(args):
         dist.barrier()
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return t.item()
+        return t.item() / steps
 
-    el = timed(0, args.steps, args.warmup)
+    sec = timed(0, args.steps, args.warmup)
     # reduce-kernel roofline: time every reduce launch on the engine's compute stream
     check(lib.ddl_kernel_timing(comm.id, 1), 'ddl_kernel_timing')
     for _ in range(min(args.steps, 10)):
@@ -237,8 +274,21 @@ def multi_gpu(args):
     launches, kbytes, kms = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
     check(lib.ddl_kernel_stats(comm.id, ctypes.byref(launches), ctypes.byref(kbytes), ctypes.byref(kms)),
           'ddl_kernel_stats')
-    el_rccl = timed(1, max(5, args.steps // 2), 3)
-    # correctness spot check: every rank's sum must match across ranks (checksum of checksums)
+    sec_rccl = timed(1, max(5, args.steps // 2), 3)
+    # ring configurations (every rank sets the same values in the same order: the schedule
+    # must be identical on all ranks)
+    sweep = []
+    if not args.no_config_sweep:
+        defaults = {k: lib.ddl_get_config(k.encode()) for k in ('rings', 'slice_bytes')}
+        for rings, slice_mib in ((1, 2), (7, 1), (7, 4), (7, 8), (3, 2)):
+            lib.ddl_set_config(b'rings', rings)
+            lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
+            t = timed(0, max(5, args.steps // 4), 2)
+            sweep.append({'rings': rings, 'slice_MiB': slice_mib, 'ms': round(t * 1e3, 4),
+                          'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
+        for k, v in defaults.items():
+            lib.ddl_set_config(k.encode(), v)
+    # correctness spot check: every rank's sum must match (checksum of checksums)
     step(0)
     torch.cuda.synchronize()
     cs = torch.tensor([recv.double().sum().item()], dtype=torch.float64)
@@ -247,18 +297,18 @@ def multi_gpu(args):
     cs_max, cs_min = cs.clone(), cs.clone()
     dist.all_reduce(cs_max, op=dist.ReduceOp.MAX)
     dist.all_reduce(cs_min, op=dist.ReduceOp.MIN)
+    host = None if args.no_host else host_resident_rate(lib, comm, S, reps=4)
 
-    ms = el * 1e3 / args.steps
-    algbw = S / GiB / (ms / 1e3)
-    busbw = 2 * (world - 1) / world * algbw
-    ms_rccl = el_rccl * 1e3 / max(5, args.steps // 2)
+    ms = sec * 1e3
+    algbw = S / GiB / sec
+    busbw_gbs = 2 * (world - 1) / world * S / sec / 1e9
     link_ceiling = min(HBM_PEAK_GBS * 2 / 7, 7 * XGMI_LINK_GBS)  # SURVEY §8d, L = 7 links
     avg_kernel_ms = kms.value / max(1, launches.value)
     achieved = kbytes.value / max(1e-9, kms.value / 1e3) / 1e9
     if rank == 0:
         out = {
             'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
-            'value': round(world * S / GiB / (ms / 1e3), 2),
+            'value': round(world * S / GiB / sec, 2),
             'unit': 'GiB/s',
             'n_gpus': world,
             'steps': args.steps,
@@ -273,15 +323,16 @@ def multi_gpu(args):
                                    f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
                        'bucket_bytes': S, 'parallelism': f'dp{world}'},
             'algbw_GiBs': round(algbw, 2),
-            'busbw_GBs': round(busbw * GiB / 1e9, 2),
-            'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling,
-                              'frac': round(busbw * GiB / 1e9 / link_ceiling, 4)},
-            'rccl_allreduce_comparator': {'ms': round(ms_rccl, 4),
-                                          'busbw_GBs': round(2 * (world - 1) / world * S / (ms_rccl / 1e3) / 1e9, 2)},
+            'busbw_GBs': round(busbw_gbs, 2),
+            'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
+            'rccl_allreduce_comparator': {'ms': round(sec_rccl * 1e3, 4),
+                                          'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)},
+            'ring_config_sweep': sweep,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                         'kernel': 'k_sum2_vec<float> (reduce-scatter step)',
+                         'kernel': 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)',
                          'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
+            'host_resident': host,
             'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
                       'sum_of_inputs': ref.item()},
         }
@@ -290,12 +341,13 @@ def multi_gpu(args):
     from ddl.torch.communicator import finalize
     finalize()
     dist.destroy_process_group()
+    dog.cancel()
 
 
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', args.gpus))
-    if world <= 1:
+    if world <= 1 and not args.force_multi:
         single_gpu(args)
     else:
         multi_gpu(args)

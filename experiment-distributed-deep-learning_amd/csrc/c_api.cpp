@@ -179,7 +179,10 @@ int ddl_set_config(const char *key, long long value) {
             c.fusion_threshold_bytes = value;
         } else if (k == "log_level") c.log_level = value;
         else if (k == "cycle_time_us") c.cycle_time_us = value;
-        else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
+        else if (k == "host_chunk_bytes") {
+            DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
+            c.host_chunk_bytes = value;
+        } else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
     });
 }
 
@@ -193,6 +196,7 @@ long long ddl_get_config(const char *key) {
     if (k == "fusion_threshold_bytes") return c.fusion_threshold_bytes;
     if (k == "log_level") return c.log_level;
     if (k == "cycle_time_us") return c.cycle_time_us;
+    if (k == "host_chunk_bytes") return c.host_chunk_bytes;
     return -1;
 }
 
@@ -237,6 +241,10 @@ void py_error(const char *s) { DDL_LOG(0, "[py]: " << (s ? s : "")); }
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,
                   int op, void *hip_stream) {
     return guarded([&] { Registry::get().find(id)->allreduce(send, recv, elements, dtype, op, as_stream(hip_stream)); });
+}
+
+int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype, int op) {
+    return guarded([&] { Registry::get().find(id)->allreduce_host(send, recv, elements, dtype, op); });
 }
 
 int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,

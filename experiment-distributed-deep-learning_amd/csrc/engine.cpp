@@ -64,6 +64,10 @@ Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl)
 Communicator::~Communicator() {
     handler_.reset();
     exec_.reset();
+    for (void *s : slots_)
+        if (s) (void)hipFree(s);
+    for (hipStream_t s : {h2d_, ring_, d2h_})
+        if (s) (void)hipStreamDestroy(s);
     if (nccl_) (void)rccl().CommDestroy(nccl_);
 }
 
@@ -74,6 +78,92 @@ void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, 
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
     exec_->allreduce(send, recv, n, dtype, stream, config().ring());
+}
+
+namespace {
+
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Registers a pageable host range for async DMA for the lifetime of the guard.
+class HostRegistration {
+public:
+    HostRegistration(const void *p, size_t bytes) {
+        if (!p || !bytes || host_pinned(p)) return;
+        DDL_HIP(hipHostRegister(const_cast<void *>(p), bytes, hipHostRegisterDefault));
+        p_ = const_cast<void *>(p);
+    }
+    ~HostRegistration() {
+        if (p_) (void)hipHostUnregister(p_);
+    }
+
+private:
+    void *p_ = nullptr;
+};
+
+}  // namespace
+
+void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dtype, int op) {
+    DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported (op " << op << ")");
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    const size_t total = n * es;
+    if (total == 0) return;
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    size_t chunk = (size_t)config().host_chunk_bytes.load();
+    chunk = chunk < 4096 ? 4096 : chunk & ~size_t(255);
+    if (chunk > total) chunk = (total + 255) & ~size_t(255);
+    if (!h2d_) {
+        DDL_HIP(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
+        DDL_HIP(hipStreamCreateWithFlags(&ring_, hipStreamNonBlocking));
+        DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+    }
+    if (slot_bytes_ < chunk) {
+        for (void *&s : slots_)
+            if (s) {
+                DDL_HIP(hipFree(s));
+                s = nullptr;
+            }
+        for (void *&s : slots_) DDL_HIP(hipMalloc(&s, chunk));
+        slot_bytes_ = chunk;
+    }
+    HostRegistration rs(send, total);
+    HostRegistration rr(recv == send ? nullptr : recv, total);
+    hipEvent_t ev[6];  // h2d done, ring done, d2h done — per slot
+    for (hipEvent_t &e : ev) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    try {
+        const RingConfig cfg = config().ring();
+        const size_t nchunks = (total + chunk - 1) / chunk;
+        for (size_t i = 0; i < nchunks; ++i) {
+            const int s = (int)(i & 1);
+            const size_t off = i * chunk, bytes = total - off < chunk ? total - off : chunk;
+            if (i >= 2) DDL_HIP(hipStreamWaitEvent(h2d_, ev[4 + s], 0));  // slot's previous D2H done
+            DDL_HIP(hipMemcpyAsync(slots_[s], static_cast<const char *>(send) + off, bytes, hipMemcpyHostToDevice, h2d_));
+            DDL_HIP(hipEventRecord(ev[s], h2d_));
+            DDL_HIP(hipStreamWaitEvent(ring_, ev[s], 0));
+            exec_->allreduce(slots_[s], slots_[s], bytes / es, dtype, ring_, cfg);
+            DDL_HIP(hipEventRecord(ev[2 + s], ring_));
+            DDL_HIP(hipStreamWaitEvent(d2h_, ev[2 + s], 0));
+            DDL_HIP(hipMemcpyAsync(static_cast<char *>(recv) + off, slots_[s], bytes, hipMemcpyDeviceToHost, d2h_));
+            DDL_HIP(hipEventRecord(ev[4 + s], d2h_));
+        }
+        DDL_HIP(hipStreamSynchronize(d2h_));
+    } catch (...) {
+        (void)hipStreamSynchronize(h2d_);
+        (void)hipStreamSynchronize(ring_);
+        (void)hipStreamSynchronize(d2h_);
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 }
 
 std::shared_ptr<Communicator> Communicator::split(int color, int key) {

@@ -29,6 +29,8 @@ struct Config {
     // keyed requests: rank 0 waits this long after the first registration before proposing
     // a round (0 = propose at once, as the reference's READY token does)
     std::atomic<long long> cycle_time_us{0};
+    // host-resident pipeline chunk (ddl_allreduce_host)
+    std::atomic<long long> host_chunk_bytes{32ll << 20};
     RingConfig ring() const {
         RingConfig c;
         c.rings = (int)rings.load();
@@ -52,6 +54,10 @@ public:
 
     // Communicator::allreduce (reference Communicator.h:45-48), device buffers, stream-ordered.
     void allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream);
+    // Host-resident buckets (the reference's deployment case: framework CPU tensors behind the
+    // MPI buffers): chunked pinned H2D -> device ring -> D2H pipeline; returns when recv holds
+    // the result.
+    void allreduce_host(const void *send, void *recv, size_t n, int dtype, int op);
     std::shared_ptr<Communicator> split(int color, int key);
 
     RequestHandler &handler();
@@ -65,6 +71,10 @@ private:
     std::unique_ptr<RingExecutor> exec_;
     std::unique_ptr<RequestHandler> handler_;
     std::mutex handler_mu_;
+    // host pipeline resources (lazily created)
+    hipStream_t h2d_ = nullptr, ring_ = nullptr, d2h_ = nullptr;
+    void *slots_[2] = {nullptr, nullptr};
+    size_t slot_bytes_ = 0;
 };
 
 class Registry {

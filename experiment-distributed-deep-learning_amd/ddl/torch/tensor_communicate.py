@@ -11,7 +11,6 @@ Device tensors stay in HBM; the call is ordered on torch's current stream and do
 synchronise the host. A host (CPU) tensor — the reference's deployment case — is staged
 through pinned memory to the GPU, reduced there and copied back.
 """
-import ctypes
 import itertools
 import threading
 
@@ -43,13 +42,12 @@ def allreduce(tensor: torch.Tensor, communicator: Communicator = None) -> torch.
         out = torch.empty_like(src)
         _allreduce_device(src, out, communicator)
         return out.view_as(tensor)
-    # host-resident bucket: pinned H2D, device ring, D2H (PCIe-inclusive path)
-    dev = torch.device('cuda', torch.cuda.current_device())
-    staged = tensor.contiguous().pin_memory().to(dev, non_blocking=True)
-    _allreduce_device(staged, staged, communicator)
+    # host-resident bucket: the engine's chunked H2D -> device ring -> D2H pipeline
+    src = tensor.contiguous()
     out = torch.empty(tensor.shape, dtype=tensor.dtype, pin_memory=True)
-    out.copy_(staged, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
+    check(CPPBackend.c_api().ddl_allreduce_host(
+        communicator.id, src.data_ptr(), out.data_ptr(), src.numel(), ddl_dtype(src), cb.OP_SUM),
+        'ddl_allreduce_host')
     return out
 
 

@@ -119,6 +119,14 @@ void py_error(const char *log_str);
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements,
                   int dtype, int op, void *hip_stream);
 
+/* Host-resident buckets (the reference's deployment case: CPU tensors behind the MPI buffers,
+ * MPIRingTokenCommunication.cc:548-733): chunked H2D -> ddl_allreduce -> D2H pipeline on three
+ * streams ("host_chunk_bytes", default 32 MiB, double-buffered in HBM). Pageable memory is
+ * registered for the call; pinned memory avoids that cost. Synchronous: returns when `recv`
+ * holds the result. Collective: every rank calls it with the same element count. */
+int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, size_t elements,
+                       int dtype, int op);
+
 /* Comparator entry for measurement: variant 0 = the engine's ring (= ddl_allreduce),
  * variant 1 = RCCL's built-in ncclAllReduce on the same communicator. */
 int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements,

@@ -36,6 +36,27 @@ def test_allreduce_host_tensor(world):
     assert not y.is_cuda and torch.equal(x, y)
 
 
+@pytest.mark.parametrize('chunk', [4096, 1 << 20, 32 << 20])
+@pytest.mark.parametrize('n,dtype', [(1, torch.float32), (1000, torch.float16), (3_000_001, torch.float32),
+                                     (777_777, torch.int64)])
+def test_allreduce_host_pipeline(world, lib, chunk, n, dtype):
+    """Chunked H2D -> ring -> D2H pipeline (pageable input registered for the call)."""
+    from ddl.torch.cpp_backend import check
+    from ddl.torch.util import ddl_dtype
+    old = lib.ddl_get_config(b'host_chunk_bytes')
+    assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
+    try:
+        x = (torch.randn(n) * 1000).to(dtype)
+        y = torch.zeros_like(x)
+        check(lib.ddl_allreduce_host(world.id, x.data_ptr(), y.data_ptr(), n, ddl_dtype(x), 0), 'host')
+        assert torch.equal(x, y)
+        z = x.clone()  # in place
+        check(lib.ddl_allreduce_host(world.id, z.data_ptr(), z.data_ptr(), n, ddl_dtype(z), 0), 'host')
+        assert torch.equal(x, z)
+    finally:
+        lib.ddl_set_config(b'host_chunk_bytes', old)
+
+
 def test_allreduce_gradient_mean(world):
     from ddl.torch.tensor_communicate import allreduce_gradient
     x = torch.randn(333, device='cuda', dtype=torch.float16)
