@@ -43,6 +43,7 @@ def parse():
     ap.add_argument('--no-variants', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe) measurement')
+    ap.add_argument('--no-fusion', action='store_true', help='skip the C5 many-bucket fusion measurement')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
     ap.add_argument('--watchdog-s', type=float, default=900.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
@@ -185,12 +186,54 @@ def single_gpu(args):
                      'frac_of_measured_copy_peak': round(achieved / HBM_MEASURED_GBS, 4)},
     }
     out.update(extra)
+    from ddl.torch.communicator import Communicator
     if not args.no_host:
-        from ddl.torch.communicator import Communicator
         out['host_resident'] = host_resident_rate(lib, Communicator.world(), S, reps=8)
+    if not args.no_fusion:
+        del sets
+        out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
     print(json.dumps(out), flush=True)
+
+
+def fusion_c5(lib, comm, dev, steps, k=4096):
+    """C5: k buckets, byte sizes log-uniform in [4 KiB, 4 MiB] rounded to 256 B,
+    dtype fp32/fp16 with p = 0.5, keys grad_%05d submitted in random order, one batch per step
+    through the keyed path (negotiation, dtype grouping, plans, pack -> ring -> unpack)."""
+    import numpy as np
+    import torch
+    from ddl.torch.cpp_backend import DONE_FN, check
+    rng = np.random.default_rng(5)
+    sizes = (np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=k)).astype(np.int64) // 256) * 256
+    order = rng.permutation(k)
+    tensors, dts, keys = [], [], []
+    for i in order:
+        half = rng.random() < 0.5
+        n = int(sizes[i]) // (2 if half else 4)
+        tensors.append(torch.randn(n, device=dev).to(torch.float16 if half else torch.float32))
+        dts.append(19 if half else 1)
+        keys.append(f'grad_{i:05d}'.encode())
+    total = sum(t.numel() * t.element_size() for t in tensors)
+    K = ctypes.c_char_p * k
+    V = ctypes.c_void_p * k
+    args = (k, K(*keys), V(*[t.data_ptr() for t in tensors]), V(*[t.data_ptr() for t in tensors]),
+            (ctypes.c_size_t * k)(*[t.numel() for t in tensors]), (ctypes.c_int * k)(*dts), 0,
+            torch.cuda.current_stream(dev).cuda_stream, DONE_FN(), None)  # DONE_FN() = NULL callback
+
+    def step():
+        check(lib.ddl_allreduce_submit_batch(comm.id, *args), 'ddl_allreduce_submit_batch')
+        check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3),
+            'bucket_GiBs': round(total / GiB / dt, 2),
+            'path': 'keyed batch -> token negotiation -> dtype groups -> plans -> pack -> ring -> unpack (in place)'}
 
 
 def host_resident_rate(lib, comm, S, reps):
@@ -298,6 +341,7 @@ def multi_gpu(args):
     dist.all_reduce(cs_max, op=dist.ReduceOp.MAX)
     dist.all_reduce(cs_min, op=dist.ReduceOp.MIN)
     host = None if args.no_host else host_resident_rate(lib, comm, S, reps=4)
+    fusion = None if args.no_fusion else fusion_c5(lib, comm, dev, steps=3)
 
     ms = sec * 1e3
     algbw = S / GiB / sec
@@ -333,6 +377,7 @@ def multi_gpu(args):
                          'kernel': 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)',
                          'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
             'host_resident': host,
+            'fusion_c5': fusion,
             'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
                       'sum_of_inputs': ref.item()},
         }

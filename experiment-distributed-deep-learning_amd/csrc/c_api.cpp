@@ -32,6 +32,16 @@ int guarded(F &&f) {
 
 hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }
 
+// ddl_pack / ddl_unpack share one copier (its table slots are not thread-safe).
+std::mutex &abi_copier_mu() {
+    static std::mutex mu;
+    return mu;
+}
+SegmentCopier &abi_copier() {
+    static SegmentCopier *c = new SegmentCopier();  // leaked: no destruction-order issues at exit
+    return *c;
+}
+
 int current_device() {
     int d = 0;
     DDL_HIP(hipGetDevice(&d));
@@ -293,18 +303,35 @@ int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in
         r.op = op;
         r.done = done;
         r.user = user;
-        DDL_HIP(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming));
-        hipError_t e = hipEventRecord(r.ready, as_stream(hip_stream));
-        if (e != hipSuccess) {
-            (void)hipEventDestroy(r.ready);
-            DDL_HIP(e);
+        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        c->handler().submit(r);
+    });
+}
+
+int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys, const void *const *ins,
+                               void *const *outs, const size_t *elements, const int *dtypes, int op,
+                               void *hip_stream, ddl_done_fn done, void *const *users) {
+    return guarded([&] {
+        DDL_REQUIRE(count >= 0 && (count == 0 || (keys && ins && outs && elements && dtypes)),
+                    DDL_STATUS_INVALID_ARGUMENT, "bad batch arguments");
+        if (count == 0) return;
+        auto c = Registry::get().find(id);
+        DeviceGuard g(c->device());
+        auto ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        std::vector<Request> rs(count);
+        for (int i = 0; i < count; ++i) {
+            DDL_REQUIRE(keys[i], DDL_STATUS_INVALID_ARGUMENT, "null key " << i);
+            rs[i].key = keys[i];
+            rs[i].in = ins[i];
+            rs[i].out = outs[i];
+            rs[i].n = elements[i];
+            rs[i].dtype = dtypes[i];
+            rs[i].op = op;
+            rs[i].done = done;
+            rs[i].user = users ? users[i] : nullptr;
+            rs[i].ready = ready;
         }
-        try {
-            c->handler().submit(r);
-        } catch (...) {
-            (void)hipEventDestroy(r.ready);
-            throw;
-        }
+        c->handler().submit_batch(rs);
     });
 }
 
@@ -359,14 +386,16 @@ int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void
 int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream) {
     return guarded([&] {
         DDL_REQUIRE(count >= 0 && (count == 0 || (dst && srcs && bytes)), DDL_STATUS_INVALID_ARGUMENT, "bad pack args");
-        launch_pack(dst, srcs, bytes, count, as_stream(hip_stream));
+        std::lock_guard<std::mutex> g(abi_copier_mu());
+        abi_copier().run(0, dst, const_cast<void *const *>(srcs), bytes, count, as_stream(hip_stream));
     });
 }
 
 int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int count, void *hip_stream) {
     return guarded([&] {
         DDL_REQUIRE(count >= 0 && (count == 0 || (src && dsts && bytes)), DDL_STATUS_INVALID_ARGUMENT, "bad unpack args");
-        launch_unpack(dsts, src, bytes, count, as_stream(hip_stream));
+        std::lock_guard<std::mutex> g(abi_copier_mu());
+        abi_copier().run(1, const_cast<void *>(src), dsts, bytes, count, as_stream(hip_stream));
     });
 }
 

@@ -111,11 +111,29 @@ int ring_variant();     // reduce-scatter step of the ring
 // out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.
 // variant < 0 selects default_variant().
 void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant = -1);
-// Gather/scatter segments into/out of a contiguous fusion buffer.
-void launch_pack(void *dst, const void *const *srcs, const size_t *bytes, int count,
-                 hipStream_t stream);
-void launch_unpack(void *const *dsts, const void *src, const size_t *bytes, int count,
-                   hipStream_t stream);
 int device_cu_count();
+
+// Gather (dir 0: segments -> flat) / scatter (dir 1: flat -> segments) between tensors and a
+// fusion buffer in one launch (pack.hip). Segment i sits at the running sum of the 256-byte-
+// rounded lengths before it. Not thread-safe: one copier per engine thread.
+class SegmentCopier {
+public:
+    SegmentCopier() = default;
+    ~SegmentCopier();
+    SegmentCopier(const SegmentCopier &) = delete;
+    SegmentCopier &operator=(const SegmentCopier &) = delete;
+    void run(int dir, void *flat, void *const *segs, const size_t *bytes, int count, hipStream_t stream);
+    static size_t flat_bytes(const size_t *bytes, int count);
+
+private:
+    struct Slot {
+        void *host = nullptr, *dev = nullptr;
+        size_t cap = 0;
+        hipEvent_t ready = nullptr;
+    };
+    static constexpr int kSlots = 4;
+    Slot slots_[kSlots];
+    int next_ = 0;
+};
 
 }  // namespace ddl

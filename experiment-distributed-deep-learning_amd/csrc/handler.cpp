@@ -47,6 +47,20 @@ std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vec
     return plans;
 }
 
+ReadyEvent::ReadyEvent(hipStream_t s) {
+    DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipError_t r = hipEventRecord(e, s);
+    if (r != hipSuccess) {
+        (void)hipEventDestroy(e);
+        e = nullptr;
+        DDL_HIP(r);
+    }
+}
+
+ReadyEvent::~ReadyEvent() {
+    if (e) (void)hipEventDestroy(e);
+}
+
 ControlChannel &world_control() {
     static ControlChannel *ch = new ControlChannel();
     return *ch;
@@ -96,6 +110,24 @@ void RequestHandler::submit(Request r) {
     cv_.notify_all();
 }
 
+void RequestHandler::submit_batch(std::vector<Request> &rs) {
+    for (const Request &r : rs) {
+        DDL_REQUIRE(dtype_size(r.dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << r.dtype);
+        DDL_REQUIRE(r.op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported");
+        DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    }
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
+        std::set<std::string> seen;
+        for (const Request &r : rs)
+            DDL_REQUIRE(pending_.find(r.key) == pending_.end() && seen.insert(r.key).second,
+                        DDL_STATUS_DUPLICATE_KEY, "a request with key '" << r.key << "' is already pending");
+        for (Request &r : rs) pending_.emplace(r.key, r);
+    }
+    cv_.notify_all();
+}
+
 void RequestHandler::wait_all() {
     std::unique_lock<std::mutex> lk(mu_);
     idle_cv_.wait(lk, [this] { return (pending_.empty() && inflight_ == 0) || stop_; });
@@ -108,7 +140,6 @@ void RequestHandler::fail_all_(int status) {
         left.swap(pending_);
     }
     for (auto &kv : left) {
-        if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
         if (kv.second.done) kv.second.done(status, kv.second.user);
     }
     idle_cv_.notify_all();
@@ -272,7 +303,7 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
     };
     std::vector<Done> dones;
     size_t nplans = 0;
-    std::set<size_t> waited;
+    std::set<hipEvent_t> waited;
     int status = DDL_STATUS_OK;
     try {
         for (auto &g : groups) {
@@ -287,8 +318,8 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
             for (const Plan &p : plans) {
                 for (size_t q = p.req_begin; q <= p.req_end; ++q) {
                     const Request &r = reqs[g.second[q]];
-                    if (r.ready && waited.insert(g.second[q]).second)
-                        DDL_HIP(hipStreamWaitEvent(stream_, r.ready, 0));
+                    if (r.ready && waited.insert(r.ready->e).second)
+                        DDL_HIP(hipStreamWaitEvent(stream_, r.ready->e, 0));
                 }
                 if (p.req_begin == p.req_end) {
                     const Request &r = reqs[g.second[p.req_begin]];
@@ -318,9 +349,10 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
                         fusion_bytes_ = total + total / 2;  // x1.5 growth (MPIRTC.cc:13, 480)
                         DDL_HIP(hipMalloc(&fusion_, fusion_bytes_));
                     }
-                    launch_pack(fusion_, srcs.data(), bytes.data(), (int)srcs.size(), stream_);
+                    copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(),
+                                stream_);
                     data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
-                    launch_unpack(dsts.data(), fusion_, bytes.data(), (int)dsts.size(), stream_);
+                    copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
                 }
                 if (plan_events_.size() <= nplans) {
                     hipEvent_t e;
@@ -354,8 +386,6 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
     }
     for (size_t i = 0; i < reqs.size(); ++i)
         if (!fired[i] && reqs[i].done) reqs[i].done(status == DDL_STATUS_OK ? DDL_STATUS_ERROR_UNKNOWN : status, reqs[i].user);
-    for (const Request &r : reqs)
-        if (r.ready) (void)hipEventDestroy(r.ready);
     {
         std::lock_guard<std::mutex> g(mu_);
         inflight_ -= reqs.size();

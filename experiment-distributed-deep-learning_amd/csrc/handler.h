@@ -30,6 +30,15 @@
 
 namespace ddl {
 
+// Input-ready event recorded on the submitter's stream; shared by the requests of one batch.
+struct ReadyEvent {
+    hipEvent_t e = nullptr;
+    explicit ReadyEvent(hipStream_t s);
+    ~ReadyEvent();
+    ReadyEvent(const ReadyEvent &) = delete;
+    ReadyEvent &operator=(const ReadyEvent &) = delete;
+};
+
 struct Request {
     std::string key;
     const void *in = nullptr;
@@ -37,7 +46,7 @@ struct Request {
     size_t n = 0;
     int dtype = 0;
     int op = 0;
-    hipEvent_t ready = nullptr;  // input ready on the submitter's stream
+    std::shared_ptr<ReadyEvent> ready;
     ddl_done_fn done = nullptr;
     void *user = nullptr;
 };
@@ -74,6 +83,8 @@ public:
     ~RequestHandler();
 
     void submit(Request r);
+    // All-or-nothing registration of several requests under one lock (one wake-up).
+    void submit_batch(std::vector<Request> &rs);
     void wait_all();
 
 private:
@@ -88,6 +99,7 @@ private:
     hipStream_t stream_ = nullptr;
     void *fusion_ = nullptr;
     size_t fusion_bytes_ = 0;
+    SegmentCopier copier_;
     std::vector<hipEvent_t> plan_events_;
 
     std::mutex mu_;

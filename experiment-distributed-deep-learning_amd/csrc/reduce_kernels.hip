@@ -206,72 +206,7 @@ void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned,
 
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// ---- fusion pack / unpack --------------------------------------------------------------
-constexpr int kPackBatch = 64;
-
-struct PackTable {
-    const char *src[kPackBatch];
-    char *dst[kPackBatch];
-    uint64_t start[kPackBatch + 1];  // byte offset of each segment's slot in the flat space
-    uint64_t len[kPackBatch];        // bytes to move
-    int count;
-    int vec_ok;                      // every pointer/offset/length is 16-byte aligned
-};
-
-// Flat byte space [0, start[count]) covers all segments back to back; each thread moves
-// 16-byte units (or single bytes when some segment is not 16-byte aligned) and finds its
-// segment by binary search over start[].
-__global__ void __launch_bounds__(kThreads) k_copy_segments(PackTable t) {
-    const uint64_t total = t.start[t.count];
-    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-    const uint64_t gid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    const uint64_t unit = t.vec_ok ? 16 : 1;
-    for (uint64_t u = gid; u * unit < total; u += stride) {
-        const uint64_t off = u * unit;
-        int lo = 0, hi = t.count - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (t.start[mid] <= off) lo = mid; else hi = mid - 1;
-        }
-        const uint64_t local = off - t.start[lo];
-        if (local >= t.len[lo]) continue;
-        if (t.vec_ok) {
-            *reinterpret_cast<u32x4 *>(t.dst[lo] + local) =
-                *reinterpret_cast<const u32x4 *>(t.src[lo] + local);
-        } else {
-            t.dst[lo][local] = t.src[lo][local];
-        }
-    }
-}
-
 int g_cu_count = 0;
-
-void launch_copy(const char *const *srcs, char *const *dsts, const size_t *bytes, int count,
-                 hipStream_t stream) {
-    for (int base = 0; base < count; base += kPackBatch) {
-        PackTable t;
-        t.count = count - base < kPackBatch ? count - base : kPackBatch;
-        uint64_t off = 0;
-        bool vec_ok = true;
-        for (int i = 0; i < t.count; ++i) {
-            t.src[i] = srcs[base + i];
-            t.dst[i] = dsts[base + i];
-            t.len[i] = bytes[base + i];
-            t.start[i] = off;
-            off += (bytes[base + i] + 15) & ~uint64_t(15);
-            vec_ok = vec_ok && aligned16(t.src[i]) && aligned16(t.dst[i]) && (t.len[i] % 16 == 0);
-        }
-        t.start[t.count] = off;
-        t.vec_ok = vec_ok ? 1 : 0;
-        if (off == 0) continue;
-        const uint64_t units = vec_ok ? off / 16 : off;
-        uint64_t blocks = (units + kThreads - 1) / kThreads;
-        const uint64_t cap = (uint64_t)device_cu_count() * 8;
-        if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(k_copy_segments, dim3((unsigned)blocks), dim3(kThreads), 0, stream, t);
-        DDL_HIP(hipGetLastError());
-    }
-}
 
 }  // namespace
 
@@ -339,34 +274,6 @@ void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) 
         default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
     }
     DDL_HIP(hipGetLastError());
-}
-
-// Fused layout: segment i occupies [off_i, off_i + bytes_i) of the fusion buffer with off_i the
-// running sum of the 256-byte-rounded sizes of the segments before it.
-void launch_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, hipStream_t stream) {
-    if (count <= 0) return;
-    std::vector<const char *> s(count);
-    std::vector<char *> d(count);
-    uint64_t off = 0;
-    for (int i = 0; i < count; ++i) {
-        s[i] = static_cast<const char *>(srcs[i]);
-        d[i] = static_cast<char *>(dst) + off;
-        off += (bytes[i] + 255) & ~uint64_t(255);
-    }
-    launch_copy(s.data(), d.data(), bytes, count, stream);
-}
-
-void launch_unpack(void *const *dsts, const void *src, const size_t *bytes, int count, hipStream_t stream) {
-    if (count <= 0) return;
-    std::vector<const char *> s(count);
-    std::vector<char *> d(count);
-    uint64_t off = 0;
-    for (int i = 0; i < count; ++i) {
-        s[i] = static_cast<const char *>(src) + off;
-        d[i] = static_cast<char *>(dsts[i]);
-        off += (bytes[i] + 255) & ~uint64_t(255);
-    }
-    launch_copy(s.data(), d.data(), bytes, count, stream);
 }
 
 }  // namespace ddl

@@ -84,6 +84,8 @@ class CPPBackend:
         # data plane
         sig('ddl_allreduce', ci, cid, vp, vp, sz, ci, ci, vp)
         sig('ddl_allreduce_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
+        sig('ddl_allreduce_submit_batch', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
+            ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, vp, DONE_FN, ctypes.POINTER(vp))
         sig('ddl_wait_all', ci, cid)
         sig('ddl_kernel_timing', ci, cid, ci)
         sig('ddl_kernel_stats', ci, cid, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),

@@ -10,7 +10,7 @@ size 1 nothing is communicated (the reference's `tf.cond(size > 1)`, :53-60).
 import torch
 
 from ddl.torch.communicator import Communicator
-from ddl.torch.tensor_communicate import allreduce_async
+from ddl.torch.tensor_communicate import allreduce_async_batch
 
 
 class DataParallelismDistributedOptimizer:
@@ -22,16 +22,19 @@ class DataParallelismDistributedOptimizer:
         comm = self.communicator or Communicator.world()
         if comm.size <= 1:
             return
-        handles = []
+        params, grads, keys = [], [], []
         for gi, group in enumerate(self.param_groups):
             for pi, p in enumerate(group['params']):
                 if p.grad is None:
                     continue
                 if p.grad.is_sparse:
                     raise NotImplementedError('sparse gradients need allgather (not implemented)')
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                key = f'{self._ddl_name}/{type(self).__name__}/Allreduce/group{gi}/param{pi:05d}'
-                handles.append((p, allreduce_async(g, key, comm, output=g)))
+                params.append(p)
+                grads.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
+                keys.append(f'{self._ddl_name}/{type(self).__name__}/Allreduce/group{gi}/param{pi:05d}')
+        # one keyed request per gradient (the reference builds one Allreduce op per grad,
+        # distributed_optimizer.py:50-63), registered as one batch, reduced in place
+        handles = zip(params, allreduce_async_batch(grads, keys, comm, outputs=grads))
         for p, h in handles:
             out = h.wait()
             out.div_(comm.size)

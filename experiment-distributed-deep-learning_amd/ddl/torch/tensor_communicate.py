@@ -136,6 +136,43 @@ def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     return h
 
 
+def allreduce_async_batch(tensors, names, communicator: Communicator = None, outputs=None):
+    """Register several keyed allreduces at once (one engine wake-up, one input-ready event);
+    returns one Handle per tensor. Same key rules as `allreduce_async`."""
+    import ctypes
+    communicator = _comm(communicator)
+    tensors = list(tensors)
+    names = list(names)
+    if len(tensors) != len(names):
+        raise ValueError('one name per tensor')
+    outputs = [torch.empty_like(t) for t in tensors] if outputs is None else list(outputs)
+    k = len(tensors)
+    if k == 0:
+        return []
+    for t, o in zip(tensors, outputs):
+        require_device_tensor(t, 'allreduce_async_batch input')
+        require_device_tensor(o, 'allreduce_async_batch output')
+    uids = [next(_ids) for _ in range(k)]
+    handles = [Handle(n, o, (t, o)) for n, t, o in zip(names, tensors, outputs)]
+    with _pending_lock:
+        _pending.update(zip(uids, handles))
+    keys = (ctypes.c_char_p * k)(*[n.encode() for n in names])
+    ins = (ctypes.c_void_p * k)(*[t.data_ptr() for t in tensors])
+    outs = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outputs])
+    ns = (ctypes.c_size_t * k)(*[t.numel() for t in tensors])
+    dts = (ctypes.c_int * k)(*[ddl_dtype(t) for t in tensors])
+    users = (ctypes.c_void_p * k)(*uids)
+    st = CPPBackend.c_api().ddl_allreduce_submit_batch(
+        communicator.id, k, keys, ins, outs, ns, dts, cb.OP_SUM, current_stream_handle(tensors[0].device),
+        _on_done, users)
+    if st != cb.STATUS_OK:
+        with _pending_lock:
+            for u in uids:
+                _pending.pop(u, None)
+        check(st, 'ddl_allreduce_submit_batch')
+    return handles
+
+
 def synchronize(handle: Handle) -> torch.Tensor:
     return handle.wait()
 

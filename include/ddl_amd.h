@@ -139,6 +139,13 @@ int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, 
 int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
                          size_t elements, int dtype, int op, void *hip_stream,
                          ddl_done_fn done, void *user);
+/* Batch form: registers `count` keyed requests at once (one input-ready event on hip_stream,
+ * one wake-up of the engine thread); users[i] (or NULL) is passed to done for request i.
+ * All-or-nothing: a duplicate key rejects the whole batch. */
+int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys,
+                               const void *const *ins, void *const *outs, const size_t *elements,
+                               const int *dtypes, int op, void *hip_stream, ddl_done_fn done,
+                               void *const *users);
 /* Blocks until every request submitted on `id` so far has completed. */
 int ddl_wait_all(ddl_communicator_id id);
 

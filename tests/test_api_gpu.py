@@ -92,6 +92,36 @@ def test_keyed_requests_fused(world, lib, threshold):
         lib.ddl_set_config(b'fusion_threshold_bytes', old)
 
 
+def test_keyed_batch_c5_shape(world, lib):
+    """C5 shape: many buckets, byte sizes log-uniform in [4 KiB, 4 MiB] rounded to
+    256 B, fp32/fp16 mixed, keys grad_%05d in random order — one batch, fused, exact."""
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    rng = np.random.default_rng(42)
+    k = 512
+    sizes = np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=k)).astype(np.int64) // 256 * 256
+    tensors, names = [], []
+    for i in rng.permutation(k):
+        dt = torch.float32 if rng.random() < 0.5 else torch.float16
+        n = int(sizes[i]) // (4 if dt == torch.float32 else 2)
+        tensors.append(torch.randn(n, device='cuda').to(dt))
+        names.append(f'grad_{i:05d}')
+    hs = allreduce_async_batch(tensors, names, world)
+    for t, h in zip(tensors, hs):
+        assert torch.equal(h.wait(60), t)
+
+
+def test_keyed_batch_duplicate_rejected_atomically(world):
+    from ddl.torch.cpp_backend import DDLError
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    ts = [torch.randn(8, device='cuda') for _ in range(3)]
+    with pytest.raises(DDLError) as e:
+        allreduce_async_batch(ts, ['x1', 'x2', 'x1'], world)
+    assert e.value.status == 7
+    hs = allreduce_async_batch(ts, ['x1', 'x2', 'x3'], world)  # nothing of the failed batch stuck
+    for t, h in zip(ts, hs):
+        assert torch.equal(h.wait(60), t)
+
+
 def test_keyed_duplicate_key_rejected(world):
     from ddl.torch.cpp_backend import DDLError
     from ddl.torch.tensor_communicate import allreduce_async
