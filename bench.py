@@ -86,6 +86,31 @@ def cpu_baseline(n_bytes_sample, seconds):
                       f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM on the reference data plane'}
 
 
+def cpu_reference_path(P=2):
+    """The reference's whole CPU+MPI loopback path (3-lap token ring over MPI p2p, fusion memcpy,
+    MPI_Allreduce) as a labelled C restatement (oracle/ref_path_port.c; the reference itself is
+    unbuildable here), under MPICH with P ranks on the host cores: C1 (fp32[1024]) and the C3
+    bucket shape (256 MiB fp32). Bounded to a few seconds."""
+    import shutil
+    import subprocess
+    exe = os.path.join(ROOT, 'oracle', 'build', 'ref_path_port')
+    mpiexec = '/opt/conda/bin/mpiexec'
+    if not (os.path.exists(exe) and shutil.which(mpiexec)):
+        return {'value': None, 'reason': 'MPICH or oracle/build/ref_path_port missing on this host'}
+    env = dict(os.environ)
+    env['LD_LIBRARY_PATH'] = '/opt/conda/lib:' + env.get('LD_LIBRARY_PATH', '')
+    res = {'kind': 'port', 'ranks': P, 'cores': P,
+           'what': 'oracle/ref_path_port.c: reference token ring + fusion + MPI_Allreduce (MPICH 3.3.2 loopback)'}
+    for tag, n, reps in (('C1_fp32_1024', 1024, 200), ('C3shape_fp32_256MiB', 64 << 20, 3)):
+        try:
+            p = subprocess.run([mpiexec, '-n', str(P), exe, str(n), '1', str(reps)], capture_output=True,
+                               text=True, timeout=120, env=env)
+            res[tag] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {'error': p.stderr[-300:]}
+        except Exception as e:  # never let the baseline leg break the bench line
+            res[tag] = {'error': repr(e)}
+    return res
+
+
 NSETS = 3  # rotating buffer sets: >= 2 x 768 MiB of traffic between reuses of one set, so the
            # 256 MiB Infinity Cache cannot serve a re-read (MI355X_MICROARCH.md §Infinity Cache)
 VARIANTS = {'default': -1, 'plain': 0, 'nt_load_a': 1, 'nt_load_ab': 3, 'nt_all': 7, 'lds_stage_b': 8,
@@ -194,7 +219,8 @@ def single_gpu(args):
         out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
-    print(json.dumps(out), flush=True)
+        out['cpu_reference_path'] = cpu_reference_path(P=2)
+    emit(out)
 
 
 def fusion_c5(lib, comm, dev, steps, k=4096):
@@ -231,9 +257,29 @@ def fusion_c5(lib, comm, dev, steps, k=4096):
     for _ in range(steps):
         step()
     dt = (time.perf_counter() - t0) / steps
-    return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3),
-            'bucket_GiBs': round(total / GiB / dt, 2),
-            'path': 'keyed batch -> token negotiation -> dtype groups -> plans -> pack -> ring -> unpack (in place)'}
+    res = {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3),
+           'bucket_GiBs': round(total / GiB / dt, 2),
+           'path': 'keyed batch -> token negotiation -> dtype groups -> plans -> pack -> ring -> unpack (in place)'}
+    if comm.size == 1:
+        res['note'] = 'one-rank world: the engine skips pack/ring/unpack (out = in), so this is host overhead'
+    # the fusion gather/scatter kernels on the same buckets (one launch each, device segment table)
+    fused = torch.empty(sum((t.numel() * t.element_size() + 255) // 256 * 256 for t in tensors), dtype=torch.uint8,
+                        device=dev)
+    ptrs = V(*[t.data_ptr() for t in tensors])
+    nbytes = (ctypes.c_size_t * k)(*[t.numel() * t.element_size() for t in tensors])
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    check(lib.ddl_pack(fused.data_ptr(), ptrs, nbytes, k, sh), 'ddl_pack')
+    e0.record()
+    for _ in range(steps):
+        check(lib.ddl_pack(fused.data_ptr(), ptrs, nbytes, k, sh), 'ddl_pack')
+        check(lib.ddl_unpack(ptrs, fused.data_ptr(), nbytes, k, sh), 'ddl_unpack')
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / (2 * steps)
+    res['pack_unpack'] = {'us_per_launch': round(t * 1e6, 1), 'hbm_GBs': round(2 * total / t / 1e9, 1),
+                          'algorithmic_bytes_per_launch': 2 * int(total)}
+    return res
 
 
 def host_resident_rate(lib, comm, S, reps):
@@ -381,7 +427,7 @@ def multi_gpu(args):
             'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
                       'sum_of_inputs': ref.item()},
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     dist.barrier()
     from ddl.torch.communicator import finalize
     finalize()
@@ -389,7 +435,22 @@ def multi_gpu(args):
     dog.cancel()
 
 
+_REAL_STDOUT = None
+
+
+def emit(obj):
+    """Write the ONE result line to the real stdout (libraries such as gloo print banners on
+    fd 1; everything but this line goes to stderr)."""
+    line = (json.dumps(obj) + '\n').encode()
+    fd = _REAL_STDOUT if _REAL_STDOUT is not None else 1
+    os.write(fd, line)
+
+
 def main():
+    global _REAL_STDOUT
+    sys.stdout.flush()
+    _REAL_STDOUT = os.dup(1)
+    os.dup2(2, 1)  # native and Python chatter -> stderr
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', args.gpus))
     if world <= 1 and not args.force_multi:

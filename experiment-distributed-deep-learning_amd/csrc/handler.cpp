@@ -321,7 +321,18 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
                     if (r.ready && waited.insert(r.ready->e).second)
                         DDL_HIP(hipStreamWaitEvent(stream_, r.ready->e, 0));
                 }
-                if (p.req_begin == p.req_end) {
+                if (data_->size() == 1) {
+                    // a one-rank world: the sum is the input; move bytes only where out != in
+                    for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                        const Request &r = reqs[g.second[q]];
+                        const size_t b = q == p.req_begin ? p.elem_begin : 0;
+                        const size_t e = q == p.req_end ? p.elem_end : r.n;
+                        if (r.in != r.out && e > b)
+                            DDL_HIP(hipMemcpyAsync(static_cast<char *>(r.out) + b * es,
+                                                   static_cast<const char *>(r.in) + b * es, (e - b) * es,
+                                                   hipMemcpyDeviceToDevice, stream_));
+                    }
+                } else if (p.req_begin == p.req_end) {
                     const Request &r = reqs[g.second[p.req_begin]];
                     const size_t cnt = p.elem_end - p.elem_begin;
                     data_->allreduce(static_cast<const char *>(r.in) + p.elem_begin * es,
@@ -375,10 +386,12 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
     }
     // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725)
     std::vector<char> fired(reqs.size(), 0);
+    size_t synced = kNoPlan;  // dones are in plan order: wait for each plan's event once
     for (const Done &d : dones) {
-        if (status == DDL_STATUS_OK && d.plan != kNoPlan) {
+        if (status == DDL_STATUS_OK && d.plan != kNoPlan && d.plan != synced) {
             hipError_t he = hipEventSynchronize(plan_events_[d.plan]);
             if (he != hipSuccess) status = DDL_STATUS_HIP_ERROR;
+            synced = d.plan;
         }
         const Request &r = reqs[d.req];
         fired[d.req] = 1;

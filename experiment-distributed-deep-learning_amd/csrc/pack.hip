@@ -57,8 +57,12 @@ __global__ void __launch_bounds__(kThreads) k_segments(char *flat, const SegDesc
     char *seg = reinterpret_cast<char *>(d[s].ptr) + local;
     char *fl = flat + off;
     if (d[s].vec && local + 16 <= len) {
-        if (DIR == 0) *reinterpret_cast<u32x4 *>(fl) = *reinterpret_cast<const u32x4 *>(seg);
-        else *reinterpret_cast<u32x4 *>(seg) = *reinterpret_cast<const u32x4 *>(fl);
+        // the source is read once (non-temporal load); the destination is read next (the ring
+        // sends the fused bucket; the optimizer reads the gradient): plain, cacheable store
+        if (DIR == 0)
+            *reinterpret_cast<u32x4 *>(fl) = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(seg));
+        else
+            *reinterpret_cast<u32x4 *>(seg) = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(fl));
     } else {
         const uint64_t m = len - local < 16 ? len - local : 16;
         for (uint64_t k = 0; k < m; ++k) {

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Single-GPU rehearsal timing of the ring schedule (not the product metric).
+
+Runs ddl_local_ring_allreduce — P virtual ranks on one GPU, the exact per-rank programs with
+their streams, events and reduce kernels, device-to-device copies standing in for RCCL — and
+prints per-P timings. It shows executor overheads (ticks, event chains, launch gaps) under
+rocprofv3; the D2D copies share one GPU's HBM, so the numbers are no link measurement.
+
+    python tools/local_ring_bench.py [--mib 256] [--ranks 2 4 8] [--reps 5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--mib', type=int, default=256)
+    ap.add_argument('--ranks', type=int, nargs='+', default=[2, 4, 8])
+    ap.add_argument('--reps', type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from ddl.torch.cpp_backend import CPPBackend, check
+    lib = CPPBackend.c_api()
+    dev = torch.device('cuda', 0)
+    n = (args.mib << 20) // 4
+    res = []
+    for P in args.ranks:
+        ins = [torch.randn(n, device=dev) for _ in range(P)]
+        outs = [torch.empty_like(t) for t in ins]
+        send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+        recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+        s = torch.cuda.current_stream().cuda_stream
+        check(lib.ddl_local_ring_allreduce(P, send, recv, n, 1, 0, s), 'local ring')
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            check(lib.ddl_local_ring_allreduce(P, send, recv, n, 1, 0, s), 'local ring')
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.reps
+        r, k = ctypes.c_int(), ctypes.c_int()
+        lib.ddl_ring_shape(n, 1, P, ctypes.byref(r), ctypes.byref(k))
+        res.append({'P': P, 'rings': r.value, 'slices': k.value, 'ms': round(dt * 1e3, 3),
+                    'all_ranks_bucket_GiBs': round(P * n * 4 / dt / 2 ** 30, 1)})
+        del ins, outs
+        torch.cuda.empty_cache()
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()
