@@ -366,15 +366,35 @@ def multi_gpu(args):
     sec_rccl = timed(1, max(5, args.steps // 2), 3)
     # ring configurations (every rank sets the same values in the same order: the schedule
     # must be identical on all ranks)
+    # the autotuner's record for this bucket (tuned during the first warmup call)
+    tune = None
+    chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
+    cfgs = (ctypes.c_longlong * 64)()
+    tms = (ctypes.c_float * 16)()
+    check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
+          'ddl_tune_result')
+    if chosen.value >= 0:
+        cands = [{'algo': ['ring', 'direct'][cfgs[4 * i]], 'rings': cfgs[4 * i + 1],
+                  'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
+                  'ms': round(tms[i], 4)} for i in range(min(count.value, 16))]
+        tune = {'chosen': cands[chosen.value], 'candidates': cands}
+    # fixed schedules, tuner off (every rank sets the same values in the same order: the
+    # schedule must be identical on all ranks)
     sweep = []
     if not args.no_config_sweep:
-        defaults = {k: lib.ddl_get_config(k.encode()) for k in ('rings', 'slice_bytes')}
-        for rings, slice_mib in ((1, 2), (7, 1), (7, 4), (7, 8), (3, 2)):
+        keys = ('algo', 'rings', 'slice_bytes', 'tune')
+        defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
+        lib.ddl_set_config(b'tune', 0)
+        for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
+                                       (1, 1, 2), (1, 1, 8)):
+            if algo == 1 and world < 3:
+                continue
+            lib.ddl_set_config(b'algo', algo)
             lib.ddl_set_config(b'rings', rings)
             lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
             t = timed(0, max(5, args.steps // 4), 2)
-            sweep.append({'rings': rings, 'slice_MiB': slice_mib, 'ms': round(t * 1e3, 4),
-                          'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
+            sweep.append({'algo': ['ring', 'direct'][algo], 'rings': rings, 'slice_MiB': slice_mib,
+                          'ms': round(t * 1e3, 4), 'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
         for k, v in defaults.items():
             lib.ddl_set_config(k.encode(), v)
     # correctness spot check: every rank's sum must match (checksum of checksums)
@@ -409,7 +429,8 @@ def multi_gpu(args):
             'vs_baseline': None,
             'dtype': 'f32',
             'data': 'synthetic N(0,1) fp32 bucket per rank, resident in HBM',
-            'config': {'workload': f'C3: ring allreduce (RS+AG over RCCL send/recv, HIP reduce), fp32 '
+            'config': {'workload': f'C3: allreduce (autotuned multi-ring or direct RS+AG over RCCL send/recv, '
+                                   f'HIP reduce), fp32 '
                                    f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
                        'bucket_bytes': S, 'parallelism': f'dp{world}'},
             'algbw_GiBs': round(algbw, 2),
@@ -417,10 +438,13 @@ def multi_gpu(args):
             'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
             'rccl_allreduce_comparator': {'ms': round(sec_rccl * 1e3, 4),
                                           'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)},
-            'ring_config_sweep': sweep,
+            'autotune': tune,
+            'schedule_sweep': sweep,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                         'kernel': 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)',
+                         'kernel': (f'k_sumN_tile<float,{world - 1}> (direct reduce-scatter fold)'
+                                    if tune and tune['chosen']['algo'] == 'direct' else
+                                    'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
                          'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
             'host_resident': host,
             'fusion_c5': fusion,

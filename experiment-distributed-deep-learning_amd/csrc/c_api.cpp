@@ -182,7 +182,11 @@ int ddl_set_config(const char *key, long long value) {
         std::string k(key);
         Config &c = config();
         if (k == "slice_bytes") c.slice_bytes = value;
-        else if (k == "rings") c.rings = value;
+        else if (k == "algo") {
+            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect, DDL_STATUS_INVALID_ARGUMENT,
+                        "algo must be 0 (ring) or 1 (direct)");
+            c.algo = value;
+        } else if (k == "rings") c.rings = value;
         else if (k == "max_slices") c.max_slices = value;
         else if (k == "fusion_threshold_bytes") {
             DDL_REQUIRE(value > 0, DDL_STATUS_INVALID_ARGUMENT, "fusion threshold must be > 0");
@@ -192,7 +196,9 @@ int ddl_set_config(const char *key, long long value) {
         else if (k == "host_chunk_bytes") {
             DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
             c.host_chunk_bytes = value;
-        } else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
+        } else if (k == "tune") c.tune = value ? 1 : 0;
+        else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
+        c.epoch.fetch_add(1);
     });
 }
 
@@ -201,12 +207,14 @@ long long ddl_get_config(const char *key) {
     std::string k(key);
     Config &c = config();
     if (k == "slice_bytes") return c.slice_bytes;
+    if (k == "algo") return c.algo;
     if (k == "rings") return c.rings;
     if (k == "max_slices") return c.max_slices;
     if (k == "fusion_threshold_bytes") return c.fusion_threshold_bytes;
     if (k == "log_level") return c.log_level;
     if (k == "cycle_time_us") return c.cycle_time_us;
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
+    if (k == "tune") return c.tune;
     return -1;
 }
 
@@ -284,6 +292,66 @@ int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, 
             default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
         }
         rccl_check(rccl().AllReduce(send, recv, elements, t, ncclSum, c->nccl(), as_stream(hip_stream)), "ncclAllReduce");
+    });
+}
+
+namespace {
+void export_tune(const TuneResult &r, int *chosen, int *count, long long *configs, float *ms, int max_candidates) {
+    DDL_REQUIRE(chosen && count, DDL_STATUS_INVALID_ARGUMENT, "null output");
+    *chosen = r.chosen;
+    *count = (int)r.candidates.size();
+    for (int i = 0; i < *count && i < max_candidates; ++i) {
+        const RingConfig &c = r.candidates[i];
+        if (configs) {
+            configs[4 * i + 0] = c.algo;
+            configs[4 * i + 1] = c.rings;
+            configs[4 * i + 2] = (long long)c.slice_bytes;
+            configs[4 * i + 3] = c.max_slices;
+        }
+        if (ms) ms[i] = r.ms[i];
+    }
+}
+}  // namespace
+
+int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, int *count, long long *configs,
+                    float *ms, int max_candidates) {
+    return guarded([&] {
+        export_tune(Registry::get().find(id)->tune_result(bucket_bytes), chosen, count, configs, ms, max_candidates);
+    });
+}
+
+int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
+                   long long *configs, float *ms, int max_candidates) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 2 && nranks <= 16, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        const size_t es = dtype_size(dtype), bytes = elements * es;
+        DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+        DDL_REQUIRE(elements > 0, DDL_STATUS_INVALID_ARGUMENT, "empty bucket");
+        (void)current_device();
+        hipStream_t stream = as_stream(hip_stream);
+        std::vector<void *> bufs(2 * nranks, nullptr);
+        auto release = [&] {
+            (void)hipStreamSynchronize(stream);
+            for (void *p : bufs)
+                if (p) (void)hipFree(p);
+        };
+        TuneResult r;
+        try {
+            for (void *&p : bufs) {
+                DDL_HIP(hipMalloc(&p, bytes));
+                DDL_HIP(hipMemsetAsync(p, 0, bytes, stream));
+            }
+            LocalWorld &w = local_world(nranks);
+            r = run_tuning(
+                nranks, bytes, stream, config().ring(),
+                [&](const RingConfig &c) { w.allreduce(bufs.data(), bufs.data() + nranks, elements, dtype, stream, c); },
+                [](float *, int) {});
+        } catch (...) {
+            release();
+            throw;
+        }
+        release();
+        export_tune(r, chosen, count, configs, ms, max_candidates);
     });
 }
 
@@ -479,6 +547,19 @@ int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long
                             "unexpected reduce operands");
                 long long row[8] = {(long long)t, 2, -1, sgi, obuf, ooff, (long long)tk.reduce.n[sgi], boff};
                 rows.insert(rows.end(), row, row + 8);
+            }
+            if (tk.has_reduce && tk.multi) {  // N-input fold: one row per received input, in fold order
+                long long obuf, ooff, abuf, aoff;
+                decode(tk.reduceN.out, &obuf, &ooff);
+                decode(tk.reduceN.a, &abuf, &aoff);
+                DDL_REQUIRE(abuf == 0 && aoff == ooff && obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "unexpected fold operands");
+                for (int i = 0; i < tk.reduceN.nb; ++i) {
+                    long long bbuf, boff;
+                    decode(tk.reduceN.b[i], &bbuf, &boff);
+                    DDL_REQUIRE(bbuf == 2, DDL_STATUS_ERROR_UNKNOWN, "fold input outside staging");
+                    long long row[8] = {(long long)t, 3, tk.reduceN.nb, i, obuf, ooff, (long long)tk.reduceN.n, boff};
+                    rows.insert(rows.end(), row, row + 8);
+                }
             }
         }
         *nops = rows.size() / 8;

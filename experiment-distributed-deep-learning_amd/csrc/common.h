@@ -96,6 +96,20 @@ struct SegTable {
     int count;
 };
 
+// One N-input problem: out = a + b[0] + b[1] + ... + b[nb-1] (left fold in that order); the
+// direct schedule's reduce of a rank's own chunk with the P-1 received copies.
+constexpr int kMaxInputs = 15;
+struct SegTableN {
+    const void *a;
+    const void *b[kMaxInputs];
+    void *out;
+    uint64_t n;
+    int nb;
+};
+// fp32/fp64/int: one rounding per add (= the ring order's arithmetic); fp16/bf16: accumulate in
+// fp32 and round once at the end.
+void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream);
+
 // Reduce-kernel cache-policy / staging flags (bit set). kVariantDefault is what the engine uses;
 // the others exist for measurement (ddl_reduce_sum2_variant, bench.py, tools/reduce_tune.hip).
 enum ReduceVariant : int {

@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 
 #include "handler.h"
@@ -21,12 +22,14 @@ const char *last_error() { return t_last_error.c_str(); }
 Config &config() {
     static Config *c = [] {
         Config *cfg = new Config();
+        if (const char *e = std::getenv("DDL_ALGO")) cfg->algo = std::atoll(e);
         if (const char *e = std::getenv("DDL_SLICE_BYTES")) cfg->slice_bytes = std::atoll(e);
         if (const char *e = std::getenv("DDL_RINGS")) cfg->rings = std::atoll(e);
         if (const char *e = std::getenv("DDL_MAX_SLICES")) cfg->max_slices = std::atoll(e);
         if (const char *e = std::getenv("DDL_FUSION_THRESHOLD")) cfg->fusion_threshold_bytes = std::atoll(e);
         if (const char *e = std::getenv("DDL_LOG_LEVEL")) cfg->log_level = std::atoll(e);
         if (const char *e = std::getenv("DDL_CYCLE_TIME_US")) cfg->cycle_time_us = std::atoll(e);
+        if (const char *e = std::getenv("DDL_TUNE")) cfg->tune = std::atoll(e);
         return cfg;
     }();
     return *c;
@@ -77,7 +80,145 @@ void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, 
     DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
-    exec_->allreduce(send, recv, n, dtype, stream, config().ring());
+    exec_->allreduce(send, recv, n, dtype, stream, ring_config(n, dtype, stream));
+}
+
+namespace {
+
+}  // namespace
+
+int size_class(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned long long)bytes) : -1; }
+
+namespace {
+
+// Candidate schedules for a P-rank communicator (the configured one first). Every rank builds
+// the same list: it depends on P and the shared config only.
+std::vector<RingConfig> tune_candidates(int P, const RingConfig &base) {
+    std::vector<RingConfig> c{base};
+    auto add = [&](int algo, int rings, size_t slice, int max_slices) {
+        RingConfig r;
+        r.algo = algo;
+        r.rings = rings;
+        r.slice_bytes = slice;
+        r.max_slices = max_slices;
+        for (const RingConfig &x : c)
+            if (x.algo == r.algo && x.rings == r.rings && x.slice_bytes == r.slice_bytes &&
+                x.max_slices == r.max_slices)
+                return;
+        c.push_back(r);
+    };
+    const int R = (int)rings_for(P, kMaxRings).size();
+    add(kAlgoRing, kMaxRings, 2u << 20, 8);
+    add(kAlgoRing, kMaxRings, 512u << 10, 16);
+    add(kAlgoRing, kMaxRings, 8u << 20, 8);
+    if (R > 1) add(kAlgoRing, 1, 2u << 20, 8);
+    if (P > 2 && P - 1 <= kMaxInputs) {
+        add(kAlgoDirect, 1, 2u << 20, 8);
+        add(kAlgoDirect, 1, 512u << 10, 16);
+        add(kAlgoDirect, 1, 8u << 20, 8);
+    }
+    return c;
+}
+
+}  // namespace
+
+TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig &base,
+                      const std::function<void(const RingConfig &)> &run,
+                      const std::function<void(float *, int)> &agree_max) {
+    TuneResult res;
+    res.candidates = tune_candidates(P, base);
+    const int nc = (int)res.candidates.size();
+    const int warm = 2, reps = bytes >= (64u << 20) ? 5 : (bytes >= (4u << 20) ? 10 : 20);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    try {
+        DDL_HIP(hipEventCreate(&e0));
+        DDL_HIP(hipEventCreate(&e1));
+        res.ms.assign(nc, 0.f);
+        for (int i = 0; i < nc; ++i) {
+            for (int w = 0; w < warm; ++w) run(res.candidates[i]);
+            DDL_HIP(hipEventRecord(e0, stream));
+            for (int r = 0; r < reps; ++r) run(res.candidates[i]);
+            DDL_HIP(hipEventRecord(e1, stream));
+            DDL_HIP(hipEventSynchronize(e1));
+            float ms = 0;
+            DDL_HIP(hipEventElapsedTime(&ms, e0, e1));
+            res.ms[i] = ms / reps;
+        }
+        agree_max(res.ms.data(), nc);
+    } catch (...) {
+        (void)hipStreamSynchronize(stream);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    res.chosen = 0;
+    for (int i = 1; i < nc; ++i)
+        if (res.ms[i] < res.ms[res.chosen]) res.chosen = i;
+    const RingConfig &c = res.candidates[res.chosen];
+    DDL_LOG(1, "tuned " << bytes << " B (class " << size_class(bytes) << "): algo " << c.algo << " rings " << c.rings
+                        << " slice " << c.slice_bytes << " -> " << res.ms[res.chosen] << " ms (configured: "
+                        << res.ms[0] << " ms)");
+    return res;
+}
+
+// Collective: every rank reaches this for the same bucket size in the same order (buckets are
+// issued in the same order on all ranks, as any collective requires), runs the same candidate
+// list with the same repetition counts on scratch buffers, and takes the max-over-ranks time of
+// each candidate (one ncclAllReduce of nc floats), so all ranks pick the same schedule.
+TuneResult Communicator::tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base) {
+    const size_t bytes = n * dtype_size(dtype);
+    void *a = nullptr, *b = nullptr;
+    float *dms = nullptr;
+    auto cleanup = [&] {
+        (void)hipStreamSynchronize(stream);
+        if (a) (void)hipFree(a);
+        if (b) (void)hipFree(b);
+        if (dms) (void)hipFree(dms);
+    };
+    TuneResult res;
+    try {
+        DDL_HIP(hipMalloc(&a, bytes));
+        DDL_HIP(hipMalloc(&b, bytes));
+        DDL_HIP(hipMalloc(&dms, sizeof(float) * 64));
+        DDL_HIP(hipMemsetAsync(a, 0, bytes, stream));
+        res = run_tuning(
+            size_, bytes, stream, base, [&](const RingConfig &c) { exec_->allreduce(a, b, n, dtype, stream, c); },
+            [&](float *ms, int nc) {
+                DDL_REQUIRE(nc <= 64, DDL_STATUS_ERROR_UNKNOWN, "too many tuning candidates");
+                DDL_HIP(hipMemcpyAsync(dms, ms, sizeof(float) * nc, hipMemcpyHostToDevice, stream));
+                rccl_check(rccl().AllReduce(dms, dms, nc, ncclFloat32, ncclMax, nccl_, stream), "ncclAllReduce(tune)");
+                DDL_HIP(hipMemcpyAsync(ms, dms, sizeof(float) * nc, hipMemcpyDeviceToHost, stream));
+                DDL_HIP(hipStreamSynchronize(stream));
+            });
+    } catch (...) {
+        cleanup();
+        throw;
+    }
+    cleanup();
+    return res;
+}
+
+RingConfig Communicator::ring_config(size_t n, int dtype, hipStream_t stream) {
+    const RingConfig base = config().ring();
+    if (size_ <= 1 || n == 0 || !config().tune.load()) return base;
+    const long long ep = config().epoch.load();
+    if (ep != tuned_epoch_) {
+        tuned_.clear();
+        tuned_epoch_ = ep;
+    }
+    const int cls = size_class(n * dtype_size(dtype));
+    auto it = tuned_.find(cls);
+    if (it == tuned_.end()) it = tuned_.emplace(cls, tune_(n, dtype, stream, base)).first;
+    return it->second.candidates[it->second.chosen];
+}
+
+TuneResult Communicator::tune_result(size_t bytes) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = tuned_.find(size_class(bytes));
+    if (it == tuned_.end() || tuned_epoch_ != config().epoch.load()) return TuneResult{};
+    return it->second;
 }
 
 namespace {
@@ -140,7 +281,7 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
     hipEvent_t ev[6];  // h2d done, ring done, d2h done — per slot
     for (hipEvent_t &e : ev) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     try {
-        const RingConfig cfg = config().ring();
+        const RingConfig cfg = ring_config(chunk / es, dtype, ring_);
         const size_t nchunks = (total + chunk - 1) / chunk;
         for (size_t i = 0; i < nchunks; ++i) {
             const int s = (int)(i & 1);

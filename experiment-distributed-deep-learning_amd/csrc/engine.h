@@ -8,10 +8,12 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "executor.h"
 
@@ -20,6 +22,7 @@ namespace ddl {
 class RequestHandler;  // keyed requests (handler.h)
 
 struct Config {
+    std::atomic<long long> algo{kAlgoRing};  // kAlgoRing / kAlgoDirect (schedule.h)
     std::atomic<long long> slice_bytes{2ll << 20};
     std::atomic<long long> rings{kMaxRings};
     std::atomic<long long> max_slices{8};
@@ -31,8 +34,14 @@ struct Config {
     std::atomic<long long> cycle_time_us{0};
     // host-resident pipeline chunk (ddl_allreduce_host)
     std::atomic<long long> host_chunk_bytes{32ll << 20};
+    // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
+    // fields above as set
+    std::atomic<long long> tune{1};
+    // bumped by every ddl_set_config: tuned choices are dropped when the tunables change
+    std::atomic<long long> epoch{0};
     RingConfig ring() const {
         RingConfig c;
+        c.algo = (int)algo.load();
         c.rings = (int)rings.load();
         c.slice_bytes = (size_t)slice_bytes.load();
         c.max_slices = (int)max_slices.load();
@@ -40,6 +49,22 @@ struct Config {
     }
 };
 Config &config();
+
+struct TuneResult {
+    std::vector<RingConfig> candidates;  // [0] = the configured schedule
+    std::vector<float> ms;               // per candidate, max over ranks
+    int chosen = -1;
+};
+
+// floor(log2(bytes)): the autotuner's bucket-size class.
+int size_class(size_t bytes);
+
+// Times every candidate schedule for a P-rank bucket of `bytes` (`run` launches one allreduce
+// on `stream`), combines the per-candidate times across ranks with `agree_max` and picks the
+// fastest. Deterministic given the agreed times, so all ranks choose the same schedule.
+TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig &base,
+                      const std::function<void(const RingConfig &)> &run,
+                      const std::function<void(float *, int)> &agree_max);
 
 class Communicator : public std::enable_shared_from_this<Communicator> {
 public:
@@ -60,6 +85,12 @@ public:
     void allreduce_host(const void *send, void *recv, size_t n, int dtype, int op);
     std::shared_ptr<Communicator> split(int color, int key);
 
+    // The schedule for an n-element bucket: the tuned choice for its size class (tuning it now,
+    // collectively, if this is the class's first bucket), or the configured one.
+    RingConfig ring_config(size_t n, int dtype, hipStream_t stream);
+    // Tuning result for the size class of `bytes` (chosen = -1 if not tuned yet).
+    TuneResult tune_result(size_t bytes);
+
     RequestHandler &handler();
     RingExecutor &executor() { return *exec_; }
     std::mutex &mutex() { return mu_; }
@@ -71,6 +102,9 @@ private:
     std::unique_ptr<RingExecutor> exec_;
     std::unique_ptr<RequestHandler> handler_;
     std::mutex handler_mu_;
+    std::map<int, TuneResult> tuned_;  // by floor(log2(bucket bytes)); guarded by mu_
+    long long tuned_epoch_ = -1;
+    TuneResult tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base);
     // host pipeline resources (lazily created)
     hipStream_t h2d_ = nullptr, ring_ = nullptr, d2h_ = nullptr;
     void *slots_[2] = {nullptr, nullptr};

@@ -62,6 +62,18 @@ void *RankResources::ensure_staging(size_t bytes) {
     return staging_;
 }
 
+double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream) {
+    const double es = (double)dtype_size(dtype);
+    if (tk.multi) {
+        launch_sumN(tk.reduceN, dtype, stream);
+        return (tk.reduceN.nb + 2.0) * (double)tk.reduceN.n * es;
+    }
+    launch_sum2(tk.reduce, dtype, stream, ring_variant());
+    double elems = 0;
+    for (int s = 0; s < tk.reduce.count; ++s) elems += (double)tk.reduce.n[s];
+    return 3.0 * elems * es;
+}
+
 int last_reduce_at_or_before(const RingProgram &p, int w) {
     for (int t = w; t >= 0; --t)
         if (p.ticks[t].has_reduce) return t;
@@ -106,10 +118,7 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
         if (in != out) DDL_HIP(hipMemcpyAsync(out, in, n * es, hipMemcpyDeviceToDevice, user));
         return;
     }
-    int R, K;
-    size_t stride;
-    ring_shape(n, es, size_, cfg, &R, &K, &stride);
-    void *staging = res_.ensure_staging(staging_elems(R, stride) * es);
+    void *staging = res_.ensure_staging(program_staging_elems(n, es, size_, cfg) * es);
     build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
     res_.ensure_events(prog_.ticks.size());
 
@@ -137,13 +146,11 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
                 }
                 DDL_HIP(hipEventRecord(tp.first, res_.compute));
             }
-            launch_sum2(tk.reduce, dtype, res_.compute, ring_variant());
+            const double bytes = launch_tick_reduce(tk, dtype, res_.compute);
             if (timing_) {
                 DDL_HIP(hipEventRecord(tp.second, res_.compute));
-                double elems = 0;
-                for (int sgi = 0; sgi < tk.reduce.count; ++sgi) elems += (double)tk.reduce.n[sgi];
                 timed_.push_back(tp);
-                timed_bytes_.push_back(3.0 * elems * (double)es);
+                timed_bytes_.push_back(bytes);
             }
             DDL_HIP(hipEventRecord(res_.red_ev[t], res_.compute));
         }
@@ -167,11 +174,8 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
         if (in[0] != out[0]) DDL_HIP(hipMemcpyAsync(out[0], in[0], n * es, hipMemcpyDeviceToDevice, user));
         return;
     }
-    int R, K;
-    size_t stride;
-    ring_shape(n, es, P_, cfg, &R, &K, &stride);
     for (int r = 0; r < P_; ++r) {
-        void *st = res_[r]->ensure_staging(staging_elems(R, stride) * es);
+        void *st = res_[r]->ensure_staging(program_staging_elems(n, es, P_, cfg) * es);
         build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
         res_[r]->ensure_events(progs_[r].ticks.size());
     }
@@ -221,7 +225,7 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
             if (!tk.has_reduce) continue;
             DDL_HIP(hipEventRecord(rr.comm_ev[t], rr.comm));
             DDL_HIP(hipStreamWaitEvent(rr.compute, rr.comm_ev[t], 0));
-            launch_sum2(tk.reduce, dtype, rr.compute, ring_variant());
+            launch_tick_reduce(tk, dtype, rr.compute);
             DDL_HIP(hipEventRecord(rr.red_ev[t], rr.compute));
         }
     }

@@ -102,4 +102,8 @@ private:
 // Most recent tick <= w that launched a reduce (-1 if none).
 int last_reduce_at_or_before(const RingProgram &p, int w);
 
+// Launches a tick's reduce (2-input ring step or N-input direct fold) on `stream`; returns its
+// algorithmic HBM bytes.
+double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream);
+
 }  // namespace ddl

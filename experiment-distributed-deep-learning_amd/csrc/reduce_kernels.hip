@@ -164,6 +164,99 @@ __global__ void __launch_bounds__(kThreads) k_sum2_tile(SegTable t) {
     }
 }
 
+// ---- N-input fold (direct schedule) --------------------------------------------------------
+// Accumulator type: fp32 for fp16/bf16 (one rounding at the end), the element type otherwise.
+template <int DT>
+struct Acc {
+    using S = typename Add<DT>::S;
+    using T = S;
+    __device__ static T widen(S x) { return x; }
+    __device__ static S narrow(T x) { return x; }
+    __device__ static T add(T a, T b) { return Add<DT>::one(a, b); }
+};
+template <>
+struct Acc<DDL_HALF> {
+    using T = float;
+    __device__ static T widen(_Float16 x) { return (float)x; }
+    __device__ static _Float16 narrow(T x) { return (_Float16)x; }
+    __device__ static T add(T a, T b) { return a + b; }
+};
+template <>
+struct Acc<DDL_BFLOAT16> {
+    using T = float;
+    __device__ static T widen(__bf16 x) { return (float)x; }
+    __device__ static __bf16 narrow(T x) { return (__bf16)x; }
+    __device__ static T add(T a, T b) { return a + b; }
+};
+
+// One 4 KiB tile of the output per workgroup: each lane folds its 16 bytes across a and the nb
+// received inputs (loads of all inputs issued before the adds), one store. HBM bytes per
+// element: (nb + 2) * sizeof(T).
+// NB (received inputs) is a template parameter: every load is unconditional and all of them
+// are in flight before the first add (a runtime "load or skip" per input makes hipcc wait
+// vmcnt(0) per input).
+template <int DT, int NB>
+__global__ void __launch_bounds__(kThreads) k_sumN_tile(SegTableN t) {
+    using A = Acc<DT>;
+    using S = typename Add<DT>::S;
+    using T = typename A::T;
+    constexpr int V = 16 / sizeof(S);
+    const uint64_t nv = t.n / V;
+    const uint64_t i = (uint64_t)blockIdx.x * kTileVec + threadIdx.x;
+    if (i < nv) {
+        u32x4 raw[NB + 1];
+        raw[0] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.a) + i);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) raw[k + 1] = static_cast<const u32x4 *>(t.b[k])[i];
+        const S *s0 = reinterpret_cast<const S *>(&raw[0]);
+        T acc[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = A::widen(s0[e]);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const S *sk = reinterpret_cast<const S *>(&raw[k + 1]);
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc[e] = A::add(acc[e], A::widen(sk[e]));
+        }
+        u32x4 res;
+        S *rs = reinterpret_cast<S *>(&res);
+#pragma unroll
+        for (int e = 0; e < V; ++e) rs[e] = A::narrow(acc[e]);
+        static_cast<u32x4 *>(t.out)[i] = res;
+    }
+    const uint64_t rem = t.n - nv * V;
+    if (rem && blockIdx.x == nv / kTileVec && threadIdx.x < rem) {
+        const uint64_t e = nv * V + threadIdx.x;
+        T acc = A::widen(static_cast<const S *>(t.a)[e]);
+        for (int k = 0; k < NB; ++k) acc = A::add(acc, A::widen(static_cast<const S *>(t.b[k])[e]));
+        static_cast<S *>(t.out)[e] = A::narrow(acc);
+    }
+}
+
+template <int DT, int NB>
+void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
+    if constexpr (NB > kMaxInputs) {
+        fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
+    } else {
+        if (t.nb == NB) hipLaunchKernelGGL((k_sumN_tile<DT, NB>), dim3(tiles), dim3(kThreads), 0, stream, t);
+        else launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
+    }
+}
+
+// Misaligned buffers for the N-input fold: element-granular grid-stride.
+template <int DT>
+__global__ void __launch_bounds__(kThreads) k_sumN_scalar(SegTableN t) {
+    using A = Acc<DT>;
+    using S = typename Add<DT>::S;
+    using T = typename A::T;
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t e = (uint64_t)blockIdx.x * kThreads + threadIdx.x; e < t.n; e += stride) {
+        T acc = A::widen(static_cast<const S *>(t.a)[e]);
+        for (int k = 0; k < t.nb; ++k) acc = A::add(acc, A::widen(static_cast<const S *>(t.b[k])[e]));
+        static_cast<S *>(t.out)[e] = A::narrow(acc);
+    }
+}
+
 // Misaligned buffers: element-granular grid-stride (correct for any alignment of T).
 template <int DT>
 __global__ void __launch_bounds__(kThreads) k_sum2_scalar(SegTable t) {
@@ -220,6 +313,43 @@ int device_cu_count() {
             g_cu_count = 256;
     }
     return g_cu_count;
+}
+
+namespace {
+template <int DT>
+void launch_sumN_dt(const SegTableN &t, hipStream_t stream) {
+    constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
+    bool aligned = aligned16(t.a) && aligned16(t.out);
+    for (int k = 0; k < t.nb; ++k) aligned = aligned && aligned16(t.b[k]);
+    if (!aligned) {
+        uint64_t blocks = (t.n + kThreads * 4 - 1) / (kThreads * 4);
+        const uint64_t cap = (uint64_t)device_cu_count() * 8;
+        blocks = blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
+        hipLaunchKernelGGL(k_sumN_scalar<DT>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, t);
+        return;
+    }
+    const uint64_t tiles = (t.n / V + kTileVec) / kTileVec;
+    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << t.n << " elements");
+    launch_sumN_nb<DT, 1>(t, stream, (unsigned)tiles);
+}
+}  // namespace
+
+void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) {
+    DDL_REQUIRE(t.nb >= 1 && t.nb <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "reduce inputs " << t.nb);
+    if (t.n == 0) return;
+    DDL_REQUIRE(t.a && t.out, DDL_STATUS_INVALID_ARGUMENT, "null reduce buffer");
+    for (int k = 0; k < t.nb; ++k) DDL_REQUIRE(t.b[k], DDL_STATUS_INVALID_ARGUMENT, "null reduce input " << k);
+    switch (dtype) {
+        case DDL_FLOAT: launch_sumN_dt<DDL_FLOAT>(t, stream); break;
+        case DDL_DOUBLE: launch_sumN_dt<DDL_DOUBLE>(t, stream); break;
+        case DDL_INT32: launch_sumN_dt<DDL_INT32>(t, stream); break;
+        case DDL_INT64: launch_sumN_dt<DDL_INT64>(t, stream); break;
+        case DDL_UINT64: launch_sumN_dt<DDL_UINT64>(t, stream); break;
+        case DDL_HALF: launch_sumN_dt<DDL_HALF>(t, stream); break;
+        case DDL_BFLOAT16: launch_sumN_dt<DDL_BFLOAT16>(t, stream); break;
+        default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
+    }
+    DDL_HIP(hipGetLastError());
 }
 
 // Standalone reduce (acc += in over whole buckets): every operand streams through once, so all

@@ -1,6 +1,7 @@
 // schedule.cpp — ring construction, bucket partition and per-rank tick lists.
 #include "schedule.h"
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -77,6 +78,19 @@ std::vector<std::vector<int>> search_rings(int P, int max_rings) {
     for (int i = 0; i < P; ++i) nat[i] = i;
     res.push_back(nat);
     if (P <= 2 || max_rings <= 1) return res;
+    if (P > 8) {
+        // beyond one node the exhaustive search is out of reach (it enumerates (P-1)! cycles):
+        // stride rings r -> r + s for s coprime to P are Hamiltonian and pairwise edge-disjoint
+        for (int st = 2; st < P && (int)res.size() < std::min(P - 1, max_rings); ++st) {
+            int a = P, b = st;
+            while (b) { int t = a % b; a = b; b = t; }
+            if (a != 1) continue;
+            std::vector<int> ring(P);
+            for (int i = 0; i < P; ++i) ring[i] = (int)((long long)i * st % P);
+            res.push_back(ring);
+        }
+        return res;
+    }
     RingSearch s;
     s.P = P;
     s.used.assign(P, std::vector<char>(P, 0));
@@ -129,8 +143,7 @@ Range slice_range(const Range &chunk, size_t esize, int K, int k) {
 
 void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
                 size_t *staging_stride) {
-    const auto &rings = rings_for(P, cfg.rings);
-    int r = (int)rings.size();
+    int r = cfg.algo == kAlgoDirect ? 1 : (int)rings_for(P, cfg.rings).size();
     // Small buckets: fewer rings so every message stays >= 64 KiB (latency-bound regime).
     const size_t bytes = n * esize;
     while (r > 1 && bytes / ((size_t)r * (size_t)P) < (64u << 10)) --r;
@@ -152,6 +165,74 @@ void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, in
     *staging_stride = (max_chunk + 63) & ~size_t(63);
 }
 
+size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cfg) {
+    int R, K;
+    size_t stride;
+    ring_shape(n, esize, P, cfg, &R, &K, &stride);
+    const size_t slots = cfg.algo == kAlgoDirect ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)R;
+    return slots * stride;
+}
+
+namespace {
+
+// Direct reduce-scatter / allgather on a fully connected mesh. Chunk c (of P) is reduced by rank
+// c. RS tick k: send slice k of chunk q to every peer q, receive slice k of my chunk from every
+// peer into its staging slot; then one N-input fold out = in + x_{me+1} + x_{me+2} + ... (the
+// ring's left-fold order for ring 0). AG tick k (waits the fold of slice k): send my reduced
+// slice to every peer, receive theirs straight into out.
+void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
+                  size_t es) {
+    const int K = prog.K;
+    DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "direct schedule supports up to "
+                                                                       << kMaxInputs + 1 << " ranks");
+    const Range mine = chunk_range(n, es, P, 1, 0, rank);
+    for (int k = 0; k < K; ++k) {
+        Tick t;
+        t.reduce.count = 0;
+        const Range ms = slice_range(mine, es, K, k);
+        for (int d = 1; d < P; ++d) {
+            const int q = (rank + d) % P;  // peer
+            const Range qs = slice_range(chunk_range(n, es, P, 1, 0, q), es, K, k);
+            if (qs.size()) t.ops.push_back(P2POp{true, q, d, const_cast<char *>(inb + qs.begin * es), qs.size() * es});
+            if (ms.size()) {
+                // receive from the rank d positions before me: fold order me, me+1, ..., so the
+                // peer at offset d' = P - d ... keep slot = offset of the sender after me
+                const int from = (rank + P - d) % P;
+                const int slot = (from - rank + P) % P - 1;  // sender me+1 -> slot 0
+                char *st = stb + ((size_t)slot * prog.staging_stride + (ms.begin - mine.begin)) * es;
+                t.ops.push_back(P2POp{false, from, d, st, ms.size() * es});
+            }
+        }
+        if (ms.size()) {
+            t.has_reduce = true;
+            t.multi = true;
+            t.reduceN.a = inb + ms.begin * es;
+            t.reduceN.out = outb + ms.begin * es;
+            t.reduceN.n = ms.size();
+            t.reduceN.nb = P - 1;
+            for (int s = 0; s < P - 1; ++s)
+                t.reduceN.b[s] = stb + ((size_t)s * prog.staging_stride + (ms.begin - mine.begin)) * es;
+        }
+        prog.ticks.push_back(std::move(t));
+    }
+    for (int k = 0; k < K; ++k) {
+        Tick t;
+        t.reduce.count = 0;
+        t.wait_reduce = k;
+        const Range ms = slice_range(mine, es, K, k);
+        for (int d = 1; d < P; ++d) {
+            const int q = (rank + d) % P;
+            const int from = (rank + P - d) % P;
+            const Range fs = slice_range(chunk_range(n, es, P, 1, 0, from), es, K, k);
+            if (ms.size()) t.ops.push_back(P2POp{true, q, d, outb + ms.begin * es, ms.size() * es});
+            if (fs.size()) t.ops.push_back(P2POp{false, from, d, outb + fs.begin * es, fs.size() * es});
+        }
+        prog.ticks.push_back(std::move(t));
+    }
+}
+
+}  // namespace
+
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
                    size_t n, int dtype, const RingConfig &cfg) {
     const size_t es = dtype_size(dtype);
@@ -159,9 +240,16 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     prog.rank = rank;
     prog.n = n;
     prog.esize = es;
+    prog.algo = cfg.algo;
     prog.ticks.clear();
     ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
+    prog.staging_slots = cfg.algo == kAlgoDirect ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)prog.R;
     if (P <= 1 || n == 0) return;
+    if (cfg.algo == kAlgoDirect) {
+        build_direct(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
+                     static_cast<char *>(staging), n, es);
+        return;
+    }
     const int R = prog.R, K = prog.K;
     const auto &rings = rings_for(P, cfg.rings);
     std::vector<int> pos(R), succ(R), pred(R);

@@ -46,12 +46,20 @@ struct P2POp {
 
 struct Tick {
     std::vector<P2POp> ops;
-    SegTable reduce;       // valid when has_reduce
+    SegTable reduce;       // valid when has_reduce && !multi
+    SegTableN reduceN;     // valid when has_reduce && multi (direct schedule)
     bool has_reduce = false;
+    bool multi = false;
     int wait_reduce = -1;  // the comm stream waits for this tick's reduce before posting ops
 };
 
+enum Algo : int {
+    kAlgoRing = 0,    // multi-ring reduce-scatter + allgather (edge-disjoint Hamiltonian cycles)
+    kAlgoDirect = 1,  // every rank exchanges with every peer at once (fully connected mesh)
+};
+
 struct RingConfig {
+    int algo = kAlgoRing;
     int rings = kMaxRings;            // upper bound; clipped to what the topology allows
     size_t slice_bytes = 2u << 20;    // target bytes per reduce-scatter message
     int max_slices = 8;
@@ -61,15 +69,18 @@ struct RingConfig {
 // two slots per ring (reduce-scatter step parity), ring j / parity q at (2j + q) * stride.
 inline size_t staging_elems(int R, size_t stride) { return 2 * (size_t)R * stride; }
 struct RingProgram {
-    int P = 1, R = 1, K = 1, rank = 0;
+    int P = 1, R = 1, K = 1, rank = 0, algo = kAlgoRing;
     size_t n = 0, esize = 0;
-    size_t staging_stride = 0;  // elements per ring in the staging buffer
+    size_t staging_stride = 0;  // elements per staging slot
+    size_t staging_slots = 0;   // ring: 2 per ring (step parity); direct: P-1 (one per peer)
     std::vector<Tick> ticks;
 };
 
-// Number of rings and slices the schedule uses for this problem.
+// Number of rings and slices the schedule uses for this problem (direct: R = 1, K slices).
 void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
                 size_t *staging_stride);
+// Staging elements the program needs.
+size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cfg);
 
 // Builds rank `rank`'s program. in/out are that rank's buffers, staging its scratch.
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,

@@ -87,6 +87,10 @@ class CPPBackend:
         sig('ddl_allreduce_submit_batch', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
             ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, vp, DONE_FN, ctypes.POINTER(vp))
         sig('ddl_wait_all', ci, cid)
+        sig('ddl_tune_result', ci, cid, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
+            ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_float), ci)
+        sig('ddl_local_tune', ci, ci, sz, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci),
+            ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_float), ci)
         sig('ddl_kernel_timing', ci, cid, ci)
         sig('ddl_kernel_stats', ci, cid, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double),
             ctypes.POINTER(ctypes.c_double))

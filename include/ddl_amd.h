@@ -99,7 +99,12 @@ int ddl_control_negotiate(const char *keys, char *out, size_t len);
 int ddl_finalize(void);
 int ddl_is_initialized(void);
 
-/* Tunables: "slice_bytes", "rings", "fusion_threshold_bytes", "log_level". */
+/* Tunables: "algo" (0 multi-ring, 1 direct all-to-all), "slice_bytes", "rings", "max_slices",
+ * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune".
+ * With "tune" = 1 (default) a communicator of P > 1 ranks picks the schedule (algo, rings,
+ * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
+ * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
+ * Every rank must set the same tunables; any ddl_set_config drops the tuned choices. */
 int ddl_set_config(const char *key, long long value);
 long long ddl_get_config(const char *key);
 
@@ -131,6 +136,17 @@ int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, siz
  * variant 1 = RCCL's built-in ncclAllReduce on the same communicator. */
 int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements,
                           int dtype, int op, void *hip_stream, int variant);
+
+/* Autotuner record for the size class of `bucket_bytes` on communicator `id`: *chosen = index
+ * of the schedule in use (-1 = class not tuned yet), *count = candidates; for the first
+ * max_candidates of them configs[4i..4i+3] = {algo, rings, slice_bytes, max_slices} and
+ * ms[i] = mean time per allreduce (max over ranks). configs/ms may be NULL. */
+int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, int *count,
+                    long long *configs, float *ms, int max_candidates);
+/* The same tuning procedure on ddl_local_ring_allreduce's P virtual ranks (one GPU, copies
+ * for the transport; no cross-rank agreement needed): a test/diagnostic entry. */
+int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
+                   long long *configs, float *ms, int max_candidates);
 
 /* Keyed asynchronous request (TF op Allreduce semantics): registered under `key`,
  * negotiated across ranks, fused by dtype in lexicographic key order, then `done` fires.
@@ -193,6 +209,8 @@ int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slic
 /* Rank `rank`'s ring program as rows of 8 int64:
  *   send/recv: {tick, 0=send|1=recv, peer, ring, buffer(0 in, 1 out, 2 staging), offset, count, wait_tick}
  *   reduce:    {tick, 2, -1, segment, 1 (out), offset, count, staging offset}  (out = in + staging)
+ *   fold:      {tick, 3, nb, input i, 1 (out), offset, count, staging offset of input i}
+ *              (direct schedule: out = in + input 0 + ... + input nb-1, fp16/bf16 in fp32)
  * Offsets and counts in elements. Host only. */
 int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out,
                      size_t max_ops, size_t *nops);

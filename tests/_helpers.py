@@ -2,6 +2,7 @@
 
 The oracle is the checker only; nothing here is imported by the product.
 """
+import contextlib
 import ctypes
 import os
 
@@ -35,6 +36,9 @@ class Oracle:
                                          ctypes.c_void_p, SZ]
         L.ddlo_allreduce_ring.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, SZ]
+        L.ddlo_allreduce_direct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.c_void_p, SZ]
+        L.ddlo_fold.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, SZ]
         L.ddlo_chunk_range.argtypes = [SZ, SZ, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
         L.ddlo_make_plan.argtypes = [ctypes.POINTER(SZ), ctypes.POINTER(SZ), SZ, SZ, ctypes.POINTER(SZ), SZ]
@@ -72,6 +76,20 @@ class Oracle:
         assert self.lib.ddlo_allreduce_ring(dt, P, R, flat, arr, ptr(out), xs[0].size) == 0
         return out
 
+    def allreduce_direct(self, dt, xs):
+        xs = [np.ascontiguousarray(x) for x in xs]
+        out = np.empty_like(xs[0])
+        arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
+        assert self.lib.ddlo_allreduce_direct(dt, len(xs), arr, ptr(out), xs[0].size) == 0
+        return out
+
+    def fold(self, dt, xs):
+        xs = [np.ascontiguousarray(x) for x in xs]
+        out = np.empty_like(xs[0])
+        arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
+        assert self.lib.ddlo_fold(dt, ptr(out), arr, len(xs), xs[0].size) == 0
+        return out
+
     def chunk_range(self, n, esize, P, R, ring, chunk):
         b, e = SZ(), SZ()
         assert self.lib.ddlo_chunk_range(n, esize, P, R, ring, chunk, ctypes.byref(b), ctypes.byref(e)) == 0
@@ -85,6 +103,19 @@ class Oracle:
         k = self.lib.ddlo_make_plan(el, es, n, limit, out, max_plans)
         assert k >= 0
         return [tuple(out[4 * i:4 * i + 4]) for i in range(k)]
+
+
+@contextlib.contextmanager
+def config(lib, **kv):
+    """Temporarily set engine tunables (ddl_set_config) and restore them."""
+    old = {k: lib.ddl_get_config(k.encode()) for k in kv}
+    try:
+        for k, v in kv.items():
+            assert lib.ddl_set_config(k.encode(), v) == 0
+        yield
+    finally:
+        for k, v in old.items():
+            lib.ddl_set_config(k.encode(), v)
 
 
 def random_input(dt, n, seed, kind='randn'):
@@ -131,15 +162,19 @@ def ring_program(lib, rank, P, n, dt):
 
 
 def simulate_ring(oracle, lib, dt, xs):
-    """Execute every rank's ring program (from the engine's own schedule) on host buffers:
-    sends/recvs matched by (tick, peer, ring), reduces through the oracle's operator."""
+    """Execute every rank's ring (or direct) program, taken from the engine's own schedule, on
+    host buffers: sends/recvs matched by (tick, peer, tag), 2-input reduces and N-input folds
+    through the oracle's operators."""
     P, n = len(xs), xs[0].size
     progs = [ring_program(lib, r, P, n, dt) for r in range(P)]
-    R, _ = ring_shape(lib, n, dt, P)
-    stride = max((e - b for b, e in (oracle.chunk_range(n, xs[0].itemsize, P, R, j, c)
-                                     for j in range(R) for c in range(P))), default=0)
-    stride = (stride + 63) & ~63
-    bufs = [[x.copy(), np.zeros_like(x), np.zeros(max(2 * R * stride, 1), dtype=x.dtype)] for x in xs]
+    st_size = 1
+    for p in progs:
+        for row in p:
+            if row[1] in (0, 1) and row[4] == 2:
+                st_size = max(st_size, int(row[5] + row[6]))
+            elif row[1] in (2, 3):
+                st_size = max(st_size, int(row[7] + row[6]))
+    bufs = [[x.copy(), np.zeros_like(x), np.zeros(st_size, dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
     for t in range(T):
         sends = {}
@@ -147,6 +182,7 @@ def simulate_ring(oracle, lib, dt, xs):
             for row in progs[r][progs[r][:, 0] == t]:
                 if row[1] == 0:
                     _, _, peer, ring, b, off, cnt, _ = row
+                    assert (r, peer, ring) not in sends
                     sends[(r, peer, ring)] = bufs[r][b][off:off + cnt].copy()
         for r in range(P):
             for row in progs[r][progs[r][:, 0] == t]:
@@ -157,9 +193,17 @@ def simulate_ring(oracle, lib, dt, xs):
                     bufs[r][b][off:off + cnt] = data
         assert not sends, f'unmatched sends at tick {t}: {list(sends)}'
         for r in range(P):
-            for row in progs[r][progs[r][:, 0] == t]:
+            rows = progs[r][progs[r][:, 0] == t]
+            for row in rows:
                 if row[1] == 2:
                     _, _, _, _, b, off, cnt, soff = row
                     bufs[r][1][off:off + cnt] = oracle.sum2(dt, bufs[r][0][off:off + cnt],
                                                             bufs[r][2][soff:soff + cnt])
+            folds = rows[rows[:, 1] == 3]
+            if len(folds):
+                nb = int(folds[0, 2])
+                assert len(folds) == nb and list(folds[:, 3]) == list(range(nb))
+                off, cnt = int(folds[0, 5]), int(folds[0, 6])
+                ins = [bufs[r][0][off:off + cnt]] + [bufs[r][2][s:s + cnt] for s in folds[:, 7]]
+                bufs[r][1][off:off + cnt] = oracle.fold(dt, ins)
     return [b[1] for b in bufs]

@@ -1,9 +1,9 @@
 """Multi-process (world size 2 and 3) CPU coverage of the N>1 path, no GPU:
 
-* the engine's per-rank ring programs (ddl_ring_program) executed by separate processes that
+* the engine's per-rank ring and direct programs (ddl_ring_program) executed by separate processes that
   exchange every send/recv over torch.distributed gloo (one isend/irecv group per tick, like
   the RCCL group), reducing through the oracle — every rank must end with the oracle's
-  ring-order result bit for bit;
+  ring-order (or direct-fold) result bit for bit;
 * the control plane: the TCP token ring (ddl_control_connect_ranked) running the 2-lap
   negotiation (ddl_control_negotiate) — every rank must agree on the lexicographically ordered
   intersection of the registered keys (RingTokenCommunicateHandler.cc:133-318 semantics).
@@ -37,21 +37,23 @@ def _setup_paths():
             sys.path.insert(0, p)
 
 
-def _ring_worker(rank, world, port, dt, n, q):
+def _ring_worker(rank, world, port, dt, n, algo, q):
     try:
         _setup_paths()
         import _helpers as h
         from ddl.torch.cpp_backend import CPPBackend
         lib = CPPBackend.c_api()
         ora = h.Oracle()
+        assert lib.ddl_set_config(b'algo', algo) == 0
         dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
         xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
         prog = h.ring_program(lib, rank, world, n, dt)
         R, _ = h.ring_shape(lib, n, dt, world)
-        stride = max(e - b for b, e in (ora.chunk_range(n, xs[0].itemsize, world, R, j, c)
-                                        for j in range(R) for c in range(world)))
-        stride = (stride + 63) & ~63
-        bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(2 * R * stride + 1, dtype=xs[rank].dtype)]
+        st = 1
+        for row in prog:
+            if row[1] <= 1 and row[4] == 2 or row[1] >= 2:
+                st = max(st, int((row[5] if row[1] <= 1 else row[7]) + row[6]))
+        bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
         view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
         for t in sorted(set(prog[:, 0].tolist())):
             rows = prog[prog[:, 0] == t]
@@ -67,7 +69,13 @@ def _ring_worker(rank, world, port, dt, n, q):
             for row in rows[rows[:, 1] == 2]:
                 _, _, _, _, b, off, cnt, soff = row
                 bufs[1][off:off + cnt] = ora.sum2(dt, bufs[0][off:off + cnt], bufs[2][soff:soff + cnt])
-        want = ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R))
+            folds = rows[rows[:, 1] == 3]
+            if len(folds):
+                off, cnt = int(folds[0, 5]), int(folds[0, 6])
+                ins = [bufs[0][off:off + cnt]] + [bufs[2][o:o + cnt] for o in folds[:, 7]]
+                bufs[1][off:off + cnt] = ora.fold(dt, ins)
+        want = (ora.allreduce_direct(dt, xs) if algo == 1 else
+                ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
         ok = bufs[1].tobytes() == want.tobytes()
         dist.destroy_process_group()
         q.put((rank, ok, ''))
@@ -75,13 +83,14 @@ def _ring_worker(rank, world, port, dt, n, q):
         q.put((rank, False, repr(e)))
 
 
+@pytest.mark.parametrize('algo', [0, 1])
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('dt,n', [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)])
-def test_ring_program_over_gloo(world, dt, n):
+def test_ring_program_over_gloo(world, dt, n, algo):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, dt, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, dt, n, algo, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]

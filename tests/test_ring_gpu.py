@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, FROM_NP, NAME, random_input, ring_perms, ring_shape)
+from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, FROM_NP, NAME, config, random_input, ring_perms,
+                      ring_shape)
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -136,3 +137,90 @@ def test_repeated_calls_reuse_resources(lib, oracle, gpu):
         R, _ = ring_shape(lib, n, DT_FLOAT, 4)
         want = oracle.allreduce_ring(DT_FLOAT, xs, ring_perms(lib, 4, R))
         assert all(o.tobytes() == want.tobytes() for o in outs)
+
+
+# ---- direct (all-to-all) schedule: algo = 1 ------------------------------------------------
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 8])
+@pytest.mark.parametrize('dt', ALL_DTYPES, ids=lambda d: NAME[d])
+@pytest.mark.parametrize('n', [1, 257, 65_537, 1_000_003])
+def test_local_direct_matches_direct_oracle(lib, oracle, gpu, P, dt, n):
+    """The N-input fold kernel (fp32 accumulation for fp16/bf16, one rounding) over the direct
+    schedule's per-rank programs, bit-exact vs the oracle's direct fold."""
+    xs = [random_input(dt, n, 4321 + 17 * r) for r in range(P)]
+    with config(lib, algo=1):
+        if dt == 14:
+            ins = [torch.from_numpy(x.view(np.int16)).to(gpu) for x in xs]
+            outs = [torch.empty_like(t) for t in ins]
+            send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+            recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+            st = lib.ddl_local_ring_allreduce(P, send, recv, n, dt, 0, torch.cuda.current_stream().cuda_stream)
+            assert st == 0, lib.ddl_last_error()
+            torch.cuda.synchronize()
+            outs = [o.cpu().numpy().view(np.uint16) for o in outs]
+        else:
+            outs = run_local(lib, gpu, xs)
+    want = oracle.allreduce_direct(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+@pytest.mark.parametrize('P', [2, 8])
+def test_local_direct_in_place_and_slices(lib, oracle, gpu, P):
+    n = (3 << 20) + 5  # several slices per chunk at 64 KiB slices, ragged tail
+    xs = [random_input(DT_FLOAT, n, 77 + r) for r in range(P)]
+    with config(lib, algo=1, slice_bytes=64 << 10):
+        outs = run_local(lib, gpu, xs, in_place=True)
+    want = oracle.allreduce_direct(DT_FLOAT, xs)
+    for o in outs:
+        assert o.tobytes() == want.tobytes()
+
+
+def test_local_direct_full_size_256mib(lib, gpu):
+    """C3 shape (256 MiB fp32, P=8) through the direct schedule: exactly summable inputs, every
+    rank equals the fp64 sum."""
+    P, n = 8, 64 << 20
+    g = torch.Generator(device=gpu).manual_seed(6)
+    ins = [(torch.randint(-(2 ** 12) + 1, 2 ** 12, (n,), device=gpu, generator=g).float() * 2.0 ** -10)
+           for _ in range(P)]
+    want = torch.stack(ins).double().sum(0).float()
+    outs = [torch.empty_like(t) for t in ins]
+    send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+    recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+    with config(lib, algo=1):
+        assert lib.ddl_local_ring_allreduce(P, send, recv, n, DT_FLOAT, 0,
+                                            torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, want)
+
+
+def test_reduce_sumN_kernel_all_input_counts(lib, oracle, gpu):
+    """The N-input fold kernel alone for every supported input count (1..15 received inputs),
+    aligned and misaligned, through a P-rank direct run with P = nb + 1 up to 16 ranks."""
+    for P in (9, 12, 16):
+        n = 10_001
+        xs = [random_input(DT_HALF, n, 5 + r) for r in range(P)]
+        with config(lib, algo=1):
+            outs = run_local(lib, gpu, xs)
+        want = oracle.allreduce_direct(DT_HALF, xs)
+        assert outs[0].tobytes() == want.tobytes(), P
+
+
+@pytest.mark.parametrize('P,ncand', [(2, 3), (4, 7), (8, 7)])
+def test_local_autotune_candidates(lib, gpu, P, ncand):
+    """The autotuner's procedure on P virtual ranks: the configured schedule is candidate 0,
+    every candidate is timed, the chosen one is the fastest."""
+    chosen, count = ctypes.c_int(), ctypes.c_int()
+    cfgs = (ctypes.c_longlong * 64)()
+    ms = (ctypes.c_float * 16)()
+    st = lib.ddl_local_tune(P, 4 << 20, DT_FLOAT, torch.cuda.current_stream().cuda_stream,
+                            ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
+    assert st == 0, lib.ddl_last_error()
+    assert count.value == ncand
+    assert (cfgs[0], cfgs[1], cfgs[2]) == (lib.ddl_get_config(b'algo'), lib.ddl_get_config(b'rings'),
+                                           lib.ddl_get_config(b'slice_bytes'))
+    times = [ms[i] for i in range(count.value)]
+    assert all(t > 0 for t in times)
+    assert times[chosen.value] == min(times)
+    algos = {cfgs[4 * i] for i in range(count.value)}
+    assert algos == ({0, 1} if P > 2 else {0})

@@ -5,7 +5,7 @@ import itertools
 import numpy as np
 import pytest
 
-from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, DT_INT32, NP, random_input, ring_perms, ring_program,
+from _helpers import (ALL_DTYPES, DT_BFLOAT16, DT_FLOAT, DT_HALF, DT_INT32, config, NP, random_input, ring_perms, ring_program,
                       ring_shape, simulate_ring)
 
 SZ_OF = {1: 4, 2: 8, 3: 4, 9: 8, 14: 2, 19: 2, 23: 8}
@@ -25,6 +25,22 @@ def test_rings_are_edge_disjoint_hamiltonian_cycles(lib, P):
             e = (p[i], p[(i + 1) % P])
             if P > 2:
                 assert e not in edges
+            edges.add(e)
+
+
+@pytest.mark.parametrize('P', [9, 12, 16, 64])
+def test_rings_beyond_one_node_are_stride_cycles(lib, P):
+    """P > 8: rings r -> r + s for every s coprime to P (edge-disjoint Hamiltonian cycles),
+    built constructively — the exhaustive search would enumerate (P-1)! cycles."""
+    import math
+    R = lib.ddl_ring_count(P, 8)
+    assert R == min(8, sum(1 for s in range(1, P) if math.gcd(s, P) == 1))
+    edges = set()
+    for p in ring_perms(lib, P, R):
+        assert sorted(p) == list(range(P))
+        for i in range(P):
+            e = (p[i], p[(i + 1) % P])
+            assert e not in edges
             edges.add(e)
 
 
@@ -90,24 +106,24 @@ def _overlap(a0, a1, b0, b1):
     return a0 < b1 and b0 < a1
 
 
+@pytest.mark.parametrize('algo', [0, 1])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
 @pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
-def test_schedule_has_no_stream_races(lib, P, n, slice_bytes):
+def test_schedule_has_no_stream_races(lib, algo, P, n, slice_bytes):
     """Comm tick T runs after the reduce it waits on (W) and every earlier reduce (the compute
     stream is in order), but concurrently with the reduces of ticks W+1..T-1. None of T's
-    sends/recvs may touch a buffer range those reduces read or write."""
-    old = lib.ddl_get_config(b'slice_bytes')
-    lib.ddl_set_config(b'slice_bytes', slice_bytes)
-    try:
+    sends/recvs may touch a buffer range those reduces read or write — with in and out treated
+    as one buffer, since in-place allreduce (in == out) is allowed."""
+    with config(lib, slice_bytes=slice_bytes, algo=algo):
         for rank in range(P):
             prog = ring_program(lib, rank, P, n, DT_FLOAT)
             red = {}
-            for row in prog[prog[:, 1] == 2]:
+            for row in prog[(prog[:, 1] == 2) | (prog[:, 1] == 3)]:
                 red.setdefault(int(row[0]), []).append(row)
             w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
             for t in sorted(set(prog[:, 0].tolist())):
-                ops = prog[(prog[:, 0] == t) & (prog[:, 1] != 2)]
+                ops = prog[(prog[:, 0] == t) & (prog[:, 1] <= 1)]
                 if not len(ops):
                     continue
                 w = int(ops[0][7])
@@ -118,15 +134,49 @@ def test_schedule_has_no_stream_races(lib, P, n, slice_bytes):
                     _, kind, _, _, buf, off, cnt, _ = op
                     for r in running:
                         _, _, _, _, _, roff, rcnt, soff = r
-                        # reduce reads in[roff:+rcnt] and staging[soff:+rcnt], writes out[roff:+rcnt]
+                        # a reduce reads in[roff:+rcnt] and staging[soff:+rcnt], writes out[roff:+rcnt]
                         if buf == 2:
                             assert not _overlap(off, off + cnt, soff, soff + rcnt), (rank, t, 'staging')
-                        if buf == 1:
-                            assert not _overlap(off, off + cnt, roff, roff + rcnt), (rank, t, 'out')
+                        else:
+                            assert not _overlap(off, off + cnt, roff, roff + rcnt), (rank, t, 'in/out')
                         if buf == 0 and kind == 1:
                             raise AssertionError('recv into the input buffer')
-    finally:
-        lib.ddl_set_config(b'slice_bytes', old)
+
+
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 8])
+@pytest.mark.parametrize('n', [1, 100, 4099, 50_000])
+@pytest.mark.parametrize('dt', ALL_DTYPES)
+def test_direct_programs_compute_the_direct_fold(lib, oracle, P, n, dt):
+    """The direct (all-to-all) schedule: every rank's program, executed with matched
+    sends/recvs, gives the oracle's direct fold bit for bit; for fp32/fp64/integers that is also
+    the ring-0 order (fp16/bf16 accumulate in fp32 and round once)."""
+    xs = [random_input(dt, n, 99 + 31 * r) for r in range(P)]
+    with config(lib, algo=1):
+        outs = simulate_ring(oracle, lib, dt, xs)
+    want = oracle.allreduce_direct(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+    if dt not in (DT_HALF, DT_BFLOAT16):
+        assert want.tobytes() == oracle.allreduce_ring(dt, xs, [list(range(P))]).tobytes()
+
+
+def test_direct_program_shape(lib):
+    """Direct schedule at C3 (256 MiB fp32, P=8): K reduce-scatter ticks, each sending one slice
+    to every peer and folding P-1 received inputs, then K allgather ticks; each rank moves
+    2(P-1)/P * S bytes, like the ring, in 2K ticks instead of 2(P-1)K."""
+    P, n = 8, 256 << 20 >> 2
+    with config(lib, algo=1):
+        R, K = ring_shape(lib, n, DT_FLOAT, P)
+        assert R == 1 and K >= 2
+        for rank in range(P):
+            prog = ring_program(lib, rank, P, n, DT_FLOAT)
+            assert int(prog[:, 0].max()) + 1 == 2 * K
+            sent = prog[prog[:, 1] == 0][:, 6].sum()
+            assert abs(sent - 2 * (P - 1) * n / P) <= 2 * P * P * 64
+            folds = prog[prog[:, 1] == 3]
+            assert len(folds) == K * (P - 1) and set(folds[:, 2]) == {P - 1}
+            for row in prog[(prog[:, 1] == 0) & (prog[:, 0] >= K)]:
+                assert row[7] == row[0] - K  # allgather slice k waits the fold of slice k
 
 
 def test_plans_match_reference_plan_walk(lib, oracle):
@@ -167,3 +217,14 @@ def test_token_key_order_is_bytewise_lexicographic():
     sorting of bytes keys."""
     keys = [b'grad_00010', b'grad_9', b'Grad_1', b'grad_\xc3\xa9', b'grad_0001']
     assert sorted(keys) == [b'Grad_1', b'grad_0001', b'grad_00010', b'grad_9', b'grad_\xc3\xa9']
+
+
+def test_direct_program_sixteen_ranks(lib, oracle):
+    """The direct fold's widest case (15 received inputs, the kernel's limit) builds at once and
+    computes the direct-fold sum."""
+    P, n = 16, 5000
+    xs = [random_input(DT_HALF, n, 3 + r) for r in range(P)]
+    with config(lib, algo=1):
+        outs = simulate_ring(oracle, lib, DT_HALF, xs)
+    want = oracle.allreduce_direct(DT_HALF, xs)
+    assert all(o.tobytes() == want.tobytes() for o in outs)
