@@ -142,7 +142,7 @@ int ddl_control_negotiate(const char *keys, char *out, size_t len) {
         while (pos < s.size()) {
             size_t nl = s.find('\n', pos);
             if (nl == std::string::npos) nl = s.size();
-            if (nl > pos) mine.push_back(s.substr(pos, nl - pos));
+            if (nl > pos) mine.push_back(std::string(request_type_name(kReqAllreduce)) + "::" + s.substr(pos, nl - pos));
             pos = nl + 1;
         }
         std::sort(mine.begin(), mine.end());
@@ -161,7 +161,7 @@ int ddl_control_negotiate(const char *keys, char *out, size_t len) {
             });
         }
         std::string res;
-        for (const auto &k : agreed) res.append(k).append("\n");
+        for (const auto &k : agreed) res.append(k.substr(k.find("::") + 2)).append("\n");
         DDL_REQUIRE(res.size() < len, DDL_STATUS_INVALID_ARGUMENT, "output buffer too small");
         std::memcpy(out, res.c_str(), res.size() + 1);
     });
@@ -259,6 +259,33 @@ void py_error(const char *s) { DDL_LOG(0, "[py]: " << (s ? s : "")); }
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,
                   int op, void *hip_stream) {
     return guarded([&] { Registry::get().find(id)->allreduce(send, recv, elements, dtype, op, as_stream(hip_stream)); });
+}
+
+int ddl_broadcast(ddl_communicator_id id, void *buf, size_t elements, int dtype, int root, void *hip_stream) {
+    return guarded([&] { Registry::get().find(id)->broadcast(buf, elements, dtype, root, as_stream(hip_stream)); });
+}
+
+int ddl_allgatherv(ddl_communicator_id id, const void *send, size_t send_elements, void *recv,
+                   const size_t *recv_counts, const size_t *displs, int dtype, void *hip_stream) {
+    return guarded([&] {
+        auto c = Registry::get().find(id);
+        DDL_REQUIRE(recv_counts && displs, DDL_STATUS_INVALID_ARGUMENT, "null counts/displs");
+        DDL_REQUIRE(recv_counts[c->rank()] == send_elements, DDL_STATUS_INVALID_ARGUMENT,
+                    "send_elements " << send_elements << " != recv_counts[rank] " << recv_counts[c->rank()]);
+        c->allgatherv(send, recv, recv_counts, displs, dtype, as_stream(hip_stream));
+    });
+}
+
+int ddl_allgather(ddl_communicator_id id, const void *send, size_t send_elements, void *recv, size_t recv_elements,
+                  int dtype, void *hip_stream) {
+    return guarded([&] {
+        auto c = Registry::get().find(id);
+        DDL_REQUIRE(send_elements == recv_elements, DDL_STATUS_INVALID_ARGUMENT,
+                    "send_elements " << send_elements << " != recv_elements " << recv_elements);
+        std::vector<size_t> counts(c->size(), recv_elements), displs(c->size());
+        for (int q = 0; q < c->size(); ++q) displs[q] = (size_t)q * recv_elements;
+        c->allgatherv(send, recv, counts.data(), displs.data(), dtype, as_stream(hip_stream));
+    });
 }
 
 int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype, int op) {
@@ -376,6 +403,49 @@ int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in
     });
 }
 
+int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                         int dtype, int root, void *hip_stream, ddl_done_fn done, void *user) {
+    return guarded([&] {
+        DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
+        auto c = Registry::get().find(id);
+        DeviceGuard g(c->device());
+        Request r;
+        r.type = kReqBroadcast;
+        r.key = key;
+        r.in = in;
+        r.out = out;
+        r.n = elements;
+        r.dtype = dtype;
+        r.root = root;
+        r.done = done;
+        r.user = user;
+        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        c->handler().submit(r);
+    });
+}
+
+int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in, size_t first_dim, size_t row_elements,
+                         int dtype, void *hip_stream, ddl_alloc_fn alloc, ddl_done_fn done, void *user) {
+    return guarded([&] {
+        DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
+        auto c = Registry::get().find(id);
+        DeviceGuard g(c->device());
+        Request r;
+        r.type = kReqAllgather;
+        r.key = key;
+        r.in = in;
+        r.first_dim = first_dim;
+        r.row_elems = row_elements;
+        r.n = first_dim * row_elements;
+        r.dtype = dtype;
+        r.alloc = alloc;
+        r.done = done;
+        r.user = user;
+        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        c->handler().submit(r);
+    });
+}
+
 int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys, const void *const *ins,
                                void *const *outs, const size_t *elements, const int *dtypes, int op,
                                void *hip_stream, ddl_done_fn done, void *const *users) {
@@ -478,6 +548,26 @@ int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *
     });
 }
 
+int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        DDL_REQUIRE(root >= 0 && root < nranks, DDL_STATUS_INVALID_ARGUMENT, "root " << root);
+        DDL_REQUIRE(bufs, DDL_STATUS_INVALID_ARGUMENT, "null buffer array");
+        (void)current_device();
+        local_world(nranks).broadcast(bufs, elements, dtype, root, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                         const size_t *displs, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        DDL_REQUIRE(sends && recvs && counts && displs, DDL_STATUS_INVALID_ARGUMENT, "null argument");
+        (void)current_device();
+        local_world(nranks).allgatherv(sends, recvs, counts, displs, dtype, as_stream(hip_stream));
+    });
+}
+
 // ---- schedule introspection -----------------------------------------------------------------
 int ddl_ring_count(int nranks, int max_rings) {
     if (nranks < 1) return 0;
@@ -514,58 +604,99 @@ int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slic
     });
 }
 
+namespace {
+
+// Symbolic base addresses: every pointer of a program decodes to (buffer, element offset).
+char *sym_base(int i) { return (char *)(uintptr_t(i + 1) << 44); }
+
+void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t max_ops, size_t *nops) {
+    auto decode = [&](const void *p, long long *buf, long long *off) {
+        uintptr_t v = reinterpret_cast<uintptr_t>(p);
+        *buf = (long long)(v >> 44) - 1;
+        *off = (long long)((v & ((uintptr_t(1) << 44) - 1)) / es);
+    };
+    std::vector<long long> rows;
+    for (size_t t = 0; t < prog.ticks.size(); ++t) {
+        const Tick &tk = prog.ticks[t];
+        for (const CopyOp &c : tk.copies) {
+            long long dbuf, doff, sbuf, soff;
+            decode(c.dst, &dbuf, &doff);
+            decode(c.src, &sbuf, &soff);
+            DDL_REQUIRE(sbuf == 0, DDL_STATUS_ERROR_UNKNOWN, "copy source outside the input");
+            long long row[8] = {(long long)t, 4, -1, -1, dbuf, doff, (long long)(c.bytes / es), soff};
+            rows.insert(rows.end(), row, row + 8);
+        }
+        for (const P2POp &op : tk.ops) {
+            long long buf, off;
+            decode(op.ptr, &buf, &off);
+            long long row[8] = {(long long)t, op.send ? 0 : 1, op.peer, op.tag, buf, off, (long long)(op.bytes / es), tk.wait_reduce};
+            rows.insert(rows.end(), row, row + 8);
+        }
+        for (int sgi = 0; sgi < tk.reduce.count; ++sgi) {
+            long long obuf, ooff, abuf, aoff, bbuf, boff;
+            decode(tk.reduce.out[sgi], &obuf, &ooff);
+            decode(tk.reduce.a[sgi], &abuf, &aoff);
+            decode(tk.reduce.b[sgi], &bbuf, &boff);
+            DDL_REQUIRE(abuf == 0 && aoff == ooff && bbuf == 2 && obuf == 1, DDL_STATUS_ERROR_UNKNOWN,
+                        "unexpected reduce operands");
+            long long row[8] = {(long long)t, 2, -1, sgi, obuf, ooff, (long long)tk.reduce.n[sgi], boff};
+            rows.insert(rows.end(), row, row + 8);
+        }
+        if (tk.has_reduce && tk.multi) {  // N-input fold: one row per received input, in fold order
+            long long obuf, ooff, abuf, aoff;
+            decode(tk.reduceN.out, &obuf, &ooff);
+            decode(tk.reduceN.a, &abuf, &aoff);
+            DDL_REQUIRE(abuf == 0 && aoff == ooff && obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "unexpected fold operands");
+            for (int i = 0; i < tk.reduceN.nb; ++i) {
+                long long bbuf, boff;
+                decode(tk.reduceN.b[i], &bbuf, &boff);
+                DDL_REQUIRE(bbuf == 2, DDL_STATUS_ERROR_UNKNOWN, "fold input outside staging");
+                long long row[8] = {(long long)t, 3, tk.reduceN.nb, i, obuf, ooff, (long long)tk.reduceN.n, boff};
+                rows.insert(rows.end(), row, row + 8);
+            }
+        }
+    }
+    *nops = rows.size() / 8;
+    DDL_REQUIRE(*nops <= max_ops && (rows.empty() || ops_out), DDL_STATUS_INVALID_ARGUMENT,
+                "op buffer too small: need " << *nops);
+    std::copy(rows.begin(), rows.end(), ops_out);
+}
+
+}  // namespace
+
 int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out, size_t max_ops,
                      size_t *nops) {
     return guarded([&] {
         const size_t es = dtype_size(dtype);
         DDL_REQUIRE(es && nranks >= 1 && rank >= 0 && rank < nranks && nops, DDL_STATUS_INVALID_ARGUMENT,
                     "bad program query");
-        // symbolic base addresses: every pointer of the program decodes to (buffer, offset)
-        char *const bases[3] = {(char *)(uintptr_t(1) << 44), (char *)(uintptr_t(2) << 44), (char *)(uintptr_t(3) << 44)};
-        auto decode = [&](const void *p, long long *buf, long long *off) {
-            uintptr_t v = reinterpret_cast<uintptr_t>(p);
-            *buf = (long long)(v >> 44) - 1;
-            *off = (long long)((v & ((uintptr_t(1) << 44) - 1)) / es);
-        };
         RingProgram prog;
-        build_program(prog, rank, nranks, bases[0], bases[1], bases[2], elements, dtype, config().ring());
-        std::vector<long long> rows;
-        for (size_t t = 0; t < prog.ticks.size(); ++t) {
-            const Tick &tk = prog.ticks[t];
-            for (const P2POp &op : tk.ops) {
-                long long buf, off;
-                decode(op.ptr, &buf, &off);
-                long long row[8] = {(long long)t, op.send ? 0 : 1, op.peer, op.tag, buf, off, (long long)(op.bytes / es), tk.wait_reduce};
-                rows.insert(rows.end(), row, row + 8);
-            }
-            for (int sgi = 0; sgi < tk.reduce.count; ++sgi) {
-                long long obuf, ooff, abuf, aoff, bbuf, boff;
-                decode(tk.reduce.out[sgi], &obuf, &ooff);
-                decode(tk.reduce.a[sgi], &abuf, &aoff);
-                decode(tk.reduce.b[sgi], &bbuf, &boff);
-                DDL_REQUIRE(abuf == 0 && aoff == ooff && bbuf == 2 && obuf == 1, DDL_STATUS_ERROR_UNKNOWN,
-                            "unexpected reduce operands");
-                long long row[8] = {(long long)t, 2, -1, sgi, obuf, ooff, (long long)tk.reduce.n[sgi], boff};
-                rows.insert(rows.end(), row, row + 8);
-            }
-            if (tk.has_reduce && tk.multi) {  // N-input fold: one row per received input, in fold order
-                long long obuf, ooff, abuf, aoff;
-                decode(tk.reduceN.out, &obuf, &ooff);
-                decode(tk.reduceN.a, &abuf, &aoff);
-                DDL_REQUIRE(abuf == 0 && aoff == ooff && obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "unexpected fold operands");
-                for (int i = 0; i < tk.reduceN.nb; ++i) {
-                    long long bbuf, boff;
-                    decode(tk.reduceN.b[i], &bbuf, &boff);
-                    DDL_REQUIRE(bbuf == 2, DDL_STATUS_ERROR_UNKNOWN, "fold input outside staging");
-                    long long row[8] = {(long long)t, 3, tk.reduceN.nb, i, obuf, ooff, (long long)tk.reduceN.n, boff};
-                    rows.insert(rows.end(), row, row + 8);
-                }
-            }
-        }
-        *nops = rows.size() / 8;
-        DDL_REQUIRE(*nops <= max_ops && (rows.empty() || ops_out), DDL_STATUS_INVALID_ARGUMENT,
-                    "op buffer too small: need " << *nops);
-        std::copy(rows.begin(), rows.end(), ops_out);
+        build_program(prog, rank, nranks, sym_base(0), sym_base(1), sym_base(2), elements, dtype, config().ring());
+        dump_program(prog, es, ops_out, max_ops, nops);
+    });
+}
+
+int ddl_broadcast_program(int rank, int nranks, int root, size_t elements, int dtype, long long *ops_out,
+                          size_t max_ops, size_t *nops) {
+    return guarded([&] {
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es && nranks >= 1 && rank >= 0 && rank < nranks && nops, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad program query");
+        RingProgram prog;
+        build_broadcast(prog, rank, nranks, root, sym_base(1), elements, dtype, config().ring());
+        dump_program(prog, es, ops_out, max_ops, nops);
+    });
+}
+
+int ddl_allgather_program(int rank, int nranks, const size_t *counts, const size_t *displs, int dtype,
+                          long long *ops_out, size_t max_ops, size_t *nops) {
+    return guarded([&] {
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es && nranks >= 1 && rank >= 0 && rank < nranks && nops && counts && displs,
+                    DDL_STATUS_INVALID_ARGUMENT, "bad program query");
+        RingProgram prog;
+        build_allgatherv(prog, rank, nranks, sym_base(0), sym_base(1), counts, displs, dtype);
+        dump_program(prog, es, ops_out, max_ops, nops);
     });
 }
 

@@ -174,7 +174,7 @@ bool ControlChannel::recv(Token &t, int timeout_ms) {
 
 std::string encode_keys(const std::vector<std::string> &keys) {
     std::string s;
-    for (const auto &k : keys) s.append("Allreduce::").append(k).append("\n");
+    for (const auto &k : keys) s.append(k).append("\n");
     return s;
 }
 
@@ -184,9 +184,7 @@ std::vector<std::string> decode_keys(const std::string &msg) {
     while (pos < msg.size()) {
         size_t nl = msg.find('\n', pos);
         if (nl == std::string::npos) nl = msg.size();
-        std::string item = msg.substr(pos, nl - pos);
-        size_t sep = item.find("::");
-        keys.push_back(sep == std::string::npos ? item : item.substr(sep + 2));
+        keys.push_back(msg.substr(pos, nl - pos));
         pos = nl + 1;
     }
     return keys;

@@ -15,7 +15,8 @@ namespace ddl {
 
 // Token types / request types: reference rtc/Token.h:20-33.
 enum TokenType : uint8_t { TOKEN_READY = 0, TOKEN_SYNC = 1, TOKEN_COMMUNICATE = 2, TOKEN_SHUT_DOWN = 3 };
-enum TokenRequest : uint8_t { TOKEN_REQUEST_SHUTDOWN = 0, TOKEN_REQUEST_ALLREDUCE = 1 };
+enum TokenRequest : uint8_t { TOKEN_REQUEST_SHUTDOWN = 0, TOKEN_REQUEST_ALLREDUCE = 1, TOKEN_REQUEST_BROADCAST = 2,
+                            TOKEN_REQUEST_ALLGATHER = 3 };
 
 struct Token {
     uint8_t type = TOKEN_READY;
@@ -49,8 +50,8 @@ private:
     int rank_ = 0, size_ = 1;
 };
 
-// "Allreduce::<key>\n" per key — the reference's token message format
-// (RingTokenCommunicateHandler.cc:10-11, 140-147, 412-437).
+// One request id ("<Type>::<key>", e.g. "Allreduce::grad_0") per line — the reference's token
+// message format (RingTokenCommunicateHandler.cc:10-11, 140-147, 412-437).
 std::string encode_keys(const std::vector<std::string> &keys);
 std::vector<std::string> decode_keys(const std::string &msg);
 

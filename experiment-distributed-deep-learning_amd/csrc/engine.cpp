@@ -221,6 +221,28 @@ TuneResult Communicator::tune_result(size_t bytes) {
     return it->second;
 }
 
+void Communicator::broadcast(void *buf, size_t n, int dtype, int root, hipStream_t stream) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(root >= 0 && root < size_, DDL_STATUS_INVALID_ARGUMENT, "root " << root << " outside [0, " << size_ << ")");
+    DDL_REQUIRE(n == 0 || buf, DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    exec_->broadcast(buf, n, dtype, root, stream, config().ring());
+}
+
+void Communicator::allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
+                              hipStream_t stream) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(counts && displs, DDL_STATUS_INVALID_ARGUMENT, "null counts/displs");
+    DDL_REQUIRE(counts[rank_] == 0 || send, DDL_STATUS_INVALID_ARGUMENT, "null send buffer");
+    size_t total = 0;
+    for (int q = 0; q < size_; ++q) total += counts[q];
+    DDL_REQUIRE(total == 0 || recv, DDL_STATUS_INVALID_ARGUMENT, "null recv buffer");
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    exec_->allgatherv(send, recv, counts, displs, dtype, stream);
+}
+
 namespace {
 
 bool host_pinned(const void *p) {

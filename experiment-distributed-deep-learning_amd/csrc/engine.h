@@ -83,6 +83,13 @@ public:
     // MPI buffers): chunked pinned H2D -> device ring -> D2H pipeline; returns when recv holds
     // the result.
     void allreduce_host(const void *send, void *recv, size_t n, int dtype, int op);
+    // Communicator::broadcast (reference Communicator.h:81-92): root's n elements of `buf` into
+    // every rank's `buf`, stream-ordered.
+    void broadcast(void *buf, size_t n, int dtype, int root, hipStream_t stream);
+    // Communicator::allgather, per-rank counts (Communicator.h:50-66): rank q's counts[q]
+    // elements land at recv + displs[q] on every rank; `send` holds counts[rank()] elements.
+    void allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
+                    hipStream_t stream);
     std::shared_ptr<Communicator> split(int color, int key);
 
     // The schedule for an n-element bucket: the tuned choice for its size class (tuning it now,

@@ -1,6 +1,8 @@
 // executor.cpp — see executor.h.
 #include "executor.h"
 
+#include <map>
+
 namespace ddl {
 
 void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
@@ -120,8 +122,27 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
     }
     void *staging = res_.ensure_staging(program_staging_elems(n, es, size_, cfg) * es);
     build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
-    res_.ensure_events(prog_.ticks.size());
+    run_(dtype, user);
+}
 
+void RingExecutor::broadcast(void *buf, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(root >= 0 && root < size_, DDL_STATUS_INVALID_ARGUMENT, "root " << root << " outside [0, " << size_ << ")");
+    if (n == 0 || size_ == 1) return;
+    build_broadcast(prog_, rank_, size_, root, buf, n, dtype, cfg);
+    run_(dtype, user);
+}
+
+void RingExecutor::allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
+                              hipStream_t user) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    build_allgatherv(prog_, rank_, size_, send, recv, counts, displs, dtype);
+    run_(dtype, user);
+}
+
+void RingExecutor::run_(int dtype, hipStream_t user) {
+    if (prog_.ticks.empty()) return;
+    res_.ensure_events(prog_.ticks.size());
     DDL_HIP(hipEventRecord(res_.fork_ev, user));
     DDL_HIP(hipStreamWaitEvent(res_.comm, res_.fork_ev, 0));
     DDL_HIP(hipStreamWaitEvent(res_.compute, res_.fork_ev, 0));
@@ -131,7 +152,10 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
             int w = last_reduce_at_or_before(prog_, tk.wait_reduce);
             if (w >= 0) DDL_HIP(hipStreamWaitEvent(res_.comm, res_.red_ev[w], 0));
         }
-        transport_->group(tk.ops, res_.comm);
+        for (const CopyOp &c : tk.copies)
+            DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, res_.comm));
+        if (transport_) transport_->group(tk.ops, res_.comm);
+        else DDL_REQUIRE(tk.ops.empty(), DDL_STATUS_ERROR_UNKNOWN, "no transport for a multi-rank program");
         if (tk.has_reduce) {
             DDL_HIP(hipEventRecord(res_.comm_ev[t], res_.comm));
             DDL_HIP(hipStreamWaitEvent(res_.compute, res_.comm_ev[t], 0));
@@ -155,7 +179,8 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
             DDL_HIP(hipEventRecord(res_.red_ev[t], res_.compute));
         }
     }
-    // the allgather waited for the last reduce, so the comm stream's tail covers everything
+    // the last tick waited for the last reduce (allreduce) or there is none, so the comm
+    // stream's tail covers everything
     DDL_HIP(hipEventRecord(res_.join_ev, res_.comm));
     DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
 }
@@ -177,7 +202,30 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
     for (int r = 0; r < P_; ++r) {
         void *st = res_[r]->ensure_staging(program_staging_elems(n, es, P_, cfg) * es);
         build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
-        res_[r]->ensure_events(progs_[r].ticks.size());
+    }
+    run_(dtype, user);
+}
+
+void LocalWorld::broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (n == 0 || P_ == 1) return;
+    for (int r = 0; r < P_; ++r) build_broadcast(progs_[r], r, P_, root, bufs[r], n, dtype, cfg);
+    run_(dtype, user);
+}
+
+void LocalWorld::allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
+                            int dtype, hipStream_t user) {
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    for (int r = 0; r < P_; ++r) build_allgatherv(progs_[r], r, P_, sends[r], recvs[r], counts, displs, dtype);
+    run_(dtype, user);
+}
+
+void LocalWorld::run_(int dtype, hipStream_t user) {
+    const size_t T = progs_[0].ticks.size();
+    if (T == 0) return;
+    for (int r = 0; r < P_; ++r) {
+        DDL_REQUIRE(progs_[r].ticks.size() == T, DDL_STATUS_ERROR_UNKNOWN, "local world: tick counts differ");
+        res_[r]->ensure_events(T);
     }
     hipEvent_t fork = res_[0]->fork_ev;
     DDL_HIP(hipEventRecord(fork, user));
@@ -185,7 +233,6 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
         DDL_HIP(hipStreamWaitEvent(res_[r]->comm, fork, 0));
         DDL_HIP(hipStreamWaitEvent(res_[r]->compute, fork, 0));
     }
-    const size_t T = progs_[0].ticks.size();
     for (size_t t = 0; t < T; ++t) {
         // 1) each rank's comm stream reaches the tick (after its reduce dependency)
         for (int r = 0; r < P_; ++r) {
@@ -195,18 +242,27 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
                 int w = last_reduce_at_or_before(progs_[r], tk.wait_reduce);
                 if (w >= 0) DDL_HIP(hipStreamWaitEvent(rr.comm, rr.red_ev[w], 0));
             }
+            for (const CopyOp &c : tk.copies)
+                DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, rr.comm));
             DDL_HIP(hipEventRecord(rr.pre_ev[t], rr.comm));
         }
         // 2) receives: copy from the matching send of the peer, once the peer reached the tick
+        //    (the k-th recv from a peer with a tag matches the k-th send to us with that tag,
+        //    as RCCL matches p2p operations between a pair in posting order)
         for (int r = 0; r < P_; ++r) {
             RankResources &rr = *res_[r];
+            std::map<std::pair<int, int>, int> seen;
             for (const P2POp &op : progs_[r].ticks[t].ops) {
                 if (op.send) continue;
+                int skip = seen[std::make_pair(op.peer, op.tag)]++;
                 const P2POp *match = nullptr;
                 for (const P2POp &o : progs_[op.peer].ticks[t].ops)
-                    if (o.send && o.peer == r && o.tag == op.tag) { match = &o; break; }
+                    if (o.send && o.peer == r && o.tag == op.tag && skip-- == 0) {
+                        match = &o;
+                        break;
+                    }
                 DDL_REQUIRE(match && match->bytes == op.bytes, DDL_STATUS_ERROR_UNKNOWN,
-                            "local ring: unmatched recv rank " << r << " tick " << t << " ring " << op.tag);
+                            "local world: unmatched recv rank " << r << " tick " << t << " tag " << op.tag);
                 DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->pre_ev[t], 0));
                 DDL_HIP(hipMemcpyAsync(op.ptr, match->ptr, op.bytes, hipMemcpyDeviceToDevice, rr.comm));
             }

@@ -69,12 +69,17 @@ public:
     ~RingExecutor();
     void allreduce(const void *in, void *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
+    void broadcast(void *buf, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
+    void allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
+                    hipStream_t user);
     int rank() const { return rank_; }
     int size() const { return size_; }
     void set_timing(bool on);
     KernelStats collect_stats();  // synchronises the recorded timing events, then resets
 
 private:
+    void run_(int dtype, hipStream_t user);  // posts prog_ on the streams, forked from / joined to user
+
     int rank_, size_;
     std::unique_ptr<Transport> transport_;
     RankResources res_;
@@ -92,8 +97,13 @@ public:
     LocalWorld(int nranks, int device);
     void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
+    void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
+    void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
+                    int dtype, hipStream_t user);
 
 private:
+    void run_(int dtype, hipStream_t user);
+
     int P_;
     std::vector<std::unique_ptr<RankResources>> res_;
     std::vector<RingProgram> progs_;

@@ -47,6 +47,15 @@ std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vec
     return plans;
 }
 
+const char *request_type_name(int type) {
+    switch (type) {
+        case kReqAllreduce: return "Allreduce";  // TensorAllreduceRequest.cc:10
+        case kReqBroadcast: return "Broadcast";  // TensorBroadcastRequest.cc:10
+        case kReqAllgather: return "Allgather";  // TensorAllgatherRequest.cc:10
+        default: return "Unknown";
+    }
+}
+
 ReadyEvent::ReadyEvent(hipStream_t s) {
     DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipError_t r = hipEventRecord(e, s);
@@ -93,37 +102,58 @@ RequestHandler::~RequestHandler() {
     fail_all_(DDL_STATUS_COMM_ERROR);
     for (hipEvent_t e : plan_events_) (void)hipEventDestroy(e);
     if (fusion_) (void)hipFree(fusion_);
+    if (gather_) (void)hipFree(gather_);
+    if (dims_) (void)hipFree(dims_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
-void RequestHandler::submit(Request r) {
+namespace {
+void validate(const Request &r, int size) {
     DDL_REQUIRE(dtype_size(r.dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << r.dtype);
-    DDL_REQUIRE(r.op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported");
-    DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    switch (r.type) {
+        case kReqAllreduce:
+            DDL_REQUIRE(r.op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported");
+            DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+            break;
+        case kReqBroadcast:
+            DDL_REQUIRE(r.root >= 0 && r.root < size, DDL_STATUS_INVALID_ARGUMENT,
+                        "root " << r.root << " outside [0, " << size << ")");
+            DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+            break;
+        case kReqAllgather:
+            DDL_REQUIRE(r.alloc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "allgather needs an output allocator");
+            DDL_REQUIRE(r.row_elems > 0 && r.n == r.first_dim * r.row_elems, DDL_STATUS_INVALID_ARGUMENT,
+                        "allgather: elements " << r.n << " != first_dim " << r.first_dim << " x row " << r.row_elems);
+            DDL_REQUIRE(r.n == 0 || r.in, DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+            break;
+        default: fail(DDL_STATUS_INVALID_ARGUMENT, "unknown request type " + std::to_string(r.type));
+    }
+}
+}  // namespace
+
+void RequestHandler::submit(Request r) {
+    validate(r, owner_->size());
     {
         std::lock_guard<std::mutex> g(mu_);
         DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
-        DDL_REQUIRE(pending_.find(r.key) == pending_.end(), DDL_STATUS_DUPLICATE_KEY,
+        const std::string id = r.id();
+        DDL_REQUIRE(pending_.find(id) == pending_.end(), DDL_STATUS_DUPLICATE_KEY,
                     "a request with key '" << r.key << "' is already pending");
-        pending_.emplace(r.key, r);
+        pending_.emplace(id, r);
     }
     cv_.notify_all();
 }
 
 void RequestHandler::submit_batch(std::vector<Request> &rs) {
-    for (const Request &r : rs) {
-        DDL_REQUIRE(dtype_size(r.dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << r.dtype);
-        DDL_REQUIRE(r.op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported");
-        DDL_REQUIRE(r.n == 0 || (r.in && r.out), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
-    }
+    for (const Request &r : rs) validate(r, owner_->size());
     {
         std::lock_guard<std::mutex> g(mu_);
         DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
         std::set<std::string> seen;
         for (const Request &r : rs)
-            DDL_REQUIRE(pending_.find(r.key) == pending_.end() && seen.insert(r.key).second,
+            DDL_REQUIRE(pending_.find(r.id()) == pending_.end() && seen.insert(r.id()).second,
                         DDL_STATUS_DUPLICATE_KEY, "a request with key '" << r.key << "' is already pending");
-        for (Request &r : rs) pending_.emplace(r.key, r);
+        for (Request &r : rs) pending_.emplace(r.id(), r);
     }
     cv_.notify_all();
 }
@@ -162,7 +192,8 @@ void RequestHandler::main_() {
                     if (cycle_us > 0)
                         cv_.wait_for(lk, std::chrono::microseconds(cycle_us), [this] { return stop_; });
                     if (stop_) break;
-                    for (auto &kv : pending_) keys.push_back(kv.first);
+                    for (auto &kv : pending_)
+                        if (kv.second.type == pending_.begin()->second.type) keys.push_back(kv.first);
                 }
                 if (P == 1) execute_(keys);
                 else root_round_();
@@ -207,9 +238,11 @@ void RequestHandler::main_() {
     idle_cv_.notify_all();
 }
 
-std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine) {
+std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine,
+                                        int request_type) {
     Token t;
     t.type = TOKEN_SYNC;
+    t.request = (uint8_t)request_type;
     t.msg = encode_keys(mine);
     ch.send(t);
     Token back;
@@ -217,6 +250,7 @@ std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<st
     DDL_REQUIRE(back.type == TOKEN_SYNC, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)back.type);
     Token c;
     c.type = TOKEN_COMMUNICATE;
+    c.request = (uint8_t)request_type;
     c.msg = back.msg;
     ch.send(c);
     return decode_keys(back.msg);
@@ -249,12 +283,17 @@ std::vector<std::string> negotiate_member(
 // the agreed set (lap 2, COMMUNICATE) and run it.
 void RequestHandler::root_round_() {
     ControlChannel &ch = world_control();
+    // one request type per round (the token carries one RequestType): the type of the first
+    // registered id, as the reference proposes registeredRequest_.begin() (:184-190)
     std::vector<std::string> mine;
+    int type = kReqAllreduce;
     {
         std::lock_guard<std::mutex> g(mu_);
-        for (auto &kv : pending_) mine.push_back(kv.first);
+        if (!pending_.empty()) type = pending_.begin()->second.type;
+        for (auto &kv : pending_)
+            if (kv.second.type == type) mine.push_back(kv.first);
     }
-    std::vector<std::string> agreed = negotiate_root(ch, mine);
+    std::vector<std::string> agreed = negotiate_root(ch, mine, type);
     execute_(agreed);
     negotiate_root_finish(ch);
 }
@@ -274,114 +313,281 @@ void RequestHandler::member_round_(Token &t) {
     execute_(agreed);
 }
 
-void RequestHandler::execute_(const std::vector<std::string> &keys) {
-    if (keys.empty()) return;
+void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
+    if (need > cap) {
+        if (buf) {
+            DDL_HIP(hipStreamSynchronize(stream_));
+            DDL_HIP(hipFree(buf));
+            buf = nullptr;
+            cap = 0;
+        }
+        const size_t sz = need + need / 2;  // x1.5 growth (MPIRingTokenCommunication.cc:13, 480)
+        DDL_HIP(hipMalloc(&buf, sz));
+        cap = sz;
+    }
+    return buf;
+}
+
+size_t RequestHandler::record_plan_(size_t &nplans) {
+    if (plan_events_.size() <= nplans) {
+        hipEvent_t e;
+        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        plan_events_.push_back(e);
+    }
+    DDL_HIP(hipEventRecord(plan_events_[nplans], stream_));
+    return nplans++;
+}
+
+void RequestHandler::wait_inputs_(const Request &r, std::vector<hipEvent_t> &waited) {
+    if (!r.ready || std::find(waited.begin(), waited.end(), r.ready->e) != waited.end()) return;
+    DDL_HIP(hipStreamWaitEvent(stream_, r.ready->e, 0));
+    waited.push_back(r.ready->e);
+}
+
+namespace {
+// Element slice [b, e) of request q inside plan p.
+void plan_slice(const Plan &p, size_t q, size_t n, size_t *b, size_t *e) {
+    *b = q == p.req_begin ? p.elem_begin : 0;
+    *e = q == p.req_end ? p.elem_end : n;
+}
+}  // namespace
+
+// allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
+// ids lexicographic inside, plans capped at the fusion threshold.
+void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
+    std::map<int, std::vector<size_t>> groups;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        if (reqs[i].n == 0) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});  // nothing to reduce
+        else groups[reqs[i].dtype].push_back(i);
+    }
+    std::vector<hipEvent_t> waited;
+    for (auto &g : groups) {
+        const int dt = g.first;
+        const size_t es = dtype_size(dt);
+        std::vector<size_t> elems, esz;
+        for (size_t i : g.second) {
+            elems.push_back(reqs[i].n);
+            esz.push_back(es);
+        }
+        for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
+            for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
+            if (data_->size() == 1) {
+                // a one-rank world: the sum is the input; move bytes only where out != in
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    size_t b, e;
+                    plan_slice(p, q, r.n, &b, &e);
+                    if (r.in != r.out && e > b)
+                        DDL_HIP(hipMemcpyAsync(static_cast<char *>(r.out) + b * es,
+                                               static_cast<const char *>(r.in) + b * es, (e - b) * es,
+                                               hipMemcpyDeviceToDevice, stream_));
+                }
+            } else if (p.req_begin == p.req_end) {
+                const Request &r = reqs[g.second[p.req_begin]];
+                const size_t cnt = p.elem_end - p.elem_begin;
+                data_->allreduce(static_cast<const char *>(r.in) + p.elem_begin * es,
+                                 static_cast<char *>(r.out) + p.elem_begin * es, cnt, dt, r.op, stream_);
+            } else {
+                std::vector<const void *> srcs;
+                std::vector<void *> dsts;
+                std::vector<size_t> bytes;
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    size_t b, e;
+                    plan_slice(p, q, r.n, &b, &e);
+                    srcs.push_back(static_cast<const char *>(r.in) + b * es);
+                    dsts.push_back(static_cast<char *>(r.out) + b * es);
+                    bytes.push_back((e - b) * es);
+                }
+                const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
+                ensure_(fusion_, fusion_bytes_, total);
+                copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(), stream_);
+                data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+                copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
+            }
+            const size_t plan = record_plan_(nplans);
+            for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                const Request &r = reqs[g.second[q]];
+                const size_t e = q == p.req_end ? p.elem_end : r.n;
+                if (e == r.n) dones.push_back(Done{plan, g.second[q], DDL_STATUS_OK});
+            }
+        }
+    }
+}
+
+// broadcastRequests (MPIRingTokenCommunication.cc:367-419): dtype groups, plans, broadcast of
+// the packed plan from the root. The reference broadcasts every group from the first request's
+// root; requests are grouped by (dtype, root) here so mixed roots stay correct.
+void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
+    std::map<std::pair<int, int>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        if (reqs[i].n == 0) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});
+        else groups[std::make_pair(reqs[i].dtype, reqs[i].root)].push_back(i);
+    }
+    const int me = data_->rank();
+    std::vector<hipEvent_t> waited;
+    for (auto &g : groups) {
+        const int dt = g.first.first, root = g.first.second;
+        const size_t es = dtype_size(dt);
+        std::vector<size_t> elems, esz;
+        for (size_t i : g.second) {
+            elems.push_back(reqs[i].n);
+            esz.push_back(es);
+        }
+        for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
+            for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
+            if (p.req_begin == p.req_end) {
+                const Request &r = reqs[g.second[p.req_begin]];
+                const size_t cnt = p.elem_end - p.elem_begin;
+                char *out = static_cast<char *>(r.out) + p.elem_begin * es;
+                if (me == root && r.in != r.out)
+                    DDL_HIP(hipMemcpyAsync(out, static_cast<const char *>(r.in) + p.elem_begin * es, cnt * es,
+                                           hipMemcpyDeviceToDevice, stream_));
+                data_->broadcast(out, cnt, dt, root, stream_);
+            } else {
+                std::vector<const void *> srcs;
+                std::vector<void *> dsts;
+                std::vector<size_t> bytes;
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    size_t b, e;
+                    plan_slice(p, q, r.n, &b, &e);
+                    srcs.push_back(static_cast<const char *>(r.in) + b * es);
+                    dsts.push_back(static_cast<char *>(r.out) + b * es);
+                    bytes.push_back((e - b) * es);
+                }
+                const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
+                ensure_(fusion_, fusion_bytes_, total);
+                if (me == root)
+                    copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(),
+                                stream_);
+                data_->broadcast(fusion_, total / es, dt, root, stream_);
+                copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
+            }
+            const size_t plan = record_plan_(nplans);
+            for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                const Request &r = reqs[g.second[q]];
+                const size_t e = q == p.req_end ? p.elem_end : r.n;
+                if (e == r.n) dones.push_back(Done{plan, g.second[q], DDL_STATUS_OK});
+            }
+        }
+    }
+}
+
+// allgatherRequests (MPIRingTokenCommunication.cc:160-364), per dtype group: allgather every
+// rank's first dims (u64), allocate each output (first dim = sum over ranks), then one
+// allgatherv of the packed requests and an unpack into the outputs in rank order. A single
+// request gathers straight into its output (rank-major blocks are the concatenation).
+void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
+    std::map<int, std::vector<size_t>> groups;
+    for (size_t i = 0; i < reqs.size(); ++i) groups[reqs[i].dtype].push_back(i);
+    const int P = data_->size(), me = data_->rank();
+    std::vector<hipEvent_t> waited;
+    for (auto &g : groups) {
+        const int dt = g.first;
+        const size_t es = dtype_size(dt), m = g.second.size();
+        // 1) first dims of every rank: fd[q * m + j]
+        std::vector<uint64_t> fd(P * m);
+        for (size_t j = 0; j < m; ++j) fd[me * m + j] = reqs[g.second[j]].first_dim;
+        if (P > 1) {
+            ensure_(dims_, dims_bytes_, fd.size() * 8);
+            std::vector<size_t> cnt(P, m), dsp(P);
+            for (int q = 0; q < P; ++q) dsp[q] = q * m;
+            DDL_HIP(hipMemcpyAsync(static_cast<char *>(dims_) + me * m * 8, fd.data() + me * m, m * 8,
+                                   hipMemcpyHostToDevice, stream_));
+            data_->allgatherv(static_cast<char *>(dims_) + me * m * 8, dims_, cnt.data(), dsp.data(), DDL_UINT64,
+                              stream_);
+            DDL_HIP(hipMemcpyAsync(fd.data(), dims_, fd.size() * 8, hipMemcpyDeviceToHost, stream_));
+            DDL_HIP(hipStreamSynchronize(stream_));
+        }
+        // 2) outputs
+        std::vector<size_t> total_rows(m, 0);
+        for (size_t j = 0; j < m; ++j) {
+            Request &r = reqs[g.second[j]];
+            for (int q = 0; q < P; ++q) total_rows[j] += fd[q * m + j];
+            const size_t bytes = total_rows[j] * r.row_elems * es;
+            r.out = r.alloc(total_rows[j], bytes, r.user);
+            DDL_REQUIRE(bytes == 0 || r.out, DDL_STATUS_ERROR_UNKNOWN, "allgather output allocation failed for '" << r.key << "'");
+        }
+        for (size_t j = 0; j < m; ++j) wait_inputs_(reqs[g.second[j]], waited);
+        // 3) data
+        if (m == 1) {
+            const Request &r = reqs[g.second[0]];
+            std::vector<size_t> cnt(P), dsp(P);
+            size_t acc = 0;
+            for (int q = 0; q < P; ++q) {
+                cnt[q] = fd[q] * r.row_elems;
+                dsp[q] = acc;
+                acc += cnt[q];
+            }
+            if (acc) data_->allgatherv(r.in, r.out, cnt.data(), dsp.data(), dt, stream_);
+        } else {
+            // rank q's block: its m requests, each 256-byte aligned (the copier's flat layout)
+            std::vector<size_t> blk(P, 0);
+            std::vector<size_t> seg_bytes(P * m);
+            for (int q = 0; q < P; ++q)
+                for (size_t j = 0; j < m; ++j) {
+                    seg_bytes[q * m + j] = fd[q * m + j] * reqs[g.second[j]].row_elems * es;
+                    blk[q] += (seg_bytes[q * m + j] + 255) & ~size_t(255);
+                }
+            size_t all = 0;
+            std::vector<size_t> cnt(P), dsp(P);
+            for (int q = 0; q < P; ++q) {
+                cnt[q] = blk[q] / es;
+                dsp[q] = all / es;
+                all += blk[q];
+            }
+            if (all) {
+                ensure_(fusion_, fusion_bytes_, std::max<size_t>(blk[me], 256));
+                ensure_(gather_, gather_bytes_, all);
+                std::vector<const void *> srcs(m);
+                for (size_t j = 0; j < m; ++j) srcs[j] = reqs[g.second[j]].in;
+                copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), seg_bytes.data() + me * m, (int)m,
+                            stream_);
+                data_->allgatherv(fusion_, gather_, cnt.data(), dsp.data(), dt, stream_);
+                std::vector<void *> dsts(P * m);
+                std::vector<size_t> row_off(m, 0);  // rows of request j written so far
+                for (int q = 0; q < P; ++q)
+                    for (size_t j = 0; j < m; ++j) {
+                        const Request &r = reqs[g.second[j]];
+                        dsts[q * m + j] = static_cast<char *>(r.out) + row_off[j] * r.row_elems * es;
+                        row_off[j] += fd[q * m + j];
+                    }
+                copier_.run(1, gather_, dsts.data(), seg_bytes.data(), (int)(P * m), stream_);
+            }
+        }
+        const size_t plan = record_plan_(nplans);
+        for (size_t j = 0; j < m; ++j) dones.push_back(Done{plan, g.second[j], DDL_STATUS_OK});
+    }
+}
+
+void RequestHandler::execute_(const std::vector<std::string> &ids) {
+    if (ids.empty()) return;
     std::vector<Request> reqs;
     {
         std::lock_guard<std::mutex> g(mu_);
-        for (const auto &k : keys) {
+        for (const auto &k : ids) {
             auto it = pending_.find(k);
-            DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed key '" << k << "' is not registered");
+            DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed request '" << k << "' is not registered");
             reqs.push_back(it->second);
             pending_.erase(it);
         }
         inflight_ += reqs.size();
     }
-    // dtype groups in ascending enum order, keys lexicographic inside (std::map / sorted keys)
-    std::map<int, std::vector<size_t>> groups;
-    std::vector<size_t> empties;  // zero-element requests: nothing to reduce, done at once
-    for (size_t i = 0; i < reqs.size(); ++i) {
-        if (reqs[i].n == 0) empties.push_back(i);
-        else groups[reqs[i].dtype].push_back(i);
-    }
-    const size_t kNoPlan = (size_t)-1;
-
-    struct Done {
-        size_t plan;
-        size_t req;
-        int status;
-    };
     std::vector<Done> dones;
     size_t nplans = 0;
-    std::set<hipEvent_t> waited;
     int status = DDL_STATUS_OK;
     try {
-        for (auto &g : groups) {
-            const int dt = g.first;
-            const size_t es = dtype_size(dt);
-            std::vector<size_t> elems, esz;
-            for (size_t i : g.second) {
-                elems.push_back(reqs[i].n);
-                esz.push_back(es);
-            }
-            std::vector<Plan> plans = make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load());
-            for (const Plan &p : plans) {
-                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
-                    const Request &r = reqs[g.second[q]];
-                    if (r.ready && waited.insert(r.ready->e).second)
-                        DDL_HIP(hipStreamWaitEvent(stream_, r.ready->e, 0));
-                }
-                if (data_->size() == 1) {
-                    // a one-rank world: the sum is the input; move bytes only where out != in
-                    for (size_t q = p.req_begin; q <= p.req_end; ++q) {
-                        const Request &r = reqs[g.second[q]];
-                        const size_t b = q == p.req_begin ? p.elem_begin : 0;
-                        const size_t e = q == p.req_end ? p.elem_end : r.n;
-                        if (r.in != r.out && e > b)
-                            DDL_HIP(hipMemcpyAsync(static_cast<char *>(r.out) + b * es,
-                                                   static_cast<const char *>(r.in) + b * es, (e - b) * es,
-                                                   hipMemcpyDeviceToDevice, stream_));
-                    }
-                } else if (p.req_begin == p.req_end) {
-                    const Request &r = reqs[g.second[p.req_begin]];
-                    const size_t cnt = p.elem_end - p.elem_begin;
-                    data_->allreduce(static_cast<const char *>(r.in) + p.elem_begin * es,
-                                     static_cast<char *>(r.out) + p.elem_begin * es, cnt, dt, r.op, stream_);
-                } else {
-                    std::vector<const void *> srcs;
-                    std::vector<void *> dsts;
-                    std::vector<size_t> bytes;
-                    size_t total = 0;
-                    for (size_t q = p.req_begin; q <= p.req_end; ++q) {
-                        const Request &r = reqs[g.second[q]];
-                        const size_t b = q == p.req_begin ? p.elem_begin : 0;
-                        const size_t e = q == p.req_end ? p.elem_end : r.n;
-                        srcs.push_back(static_cast<const char *>(r.in) + b * es);
-                        dsts.push_back(static_cast<char *>(r.out) + b * es);
-                        bytes.push_back((e - b) * es);
-                        total += ((e - b) * es + 255) & ~size_t(255);
-                    }
-                    if (total > fusion_bytes_) {
-                        if (fusion_) {
-                            DDL_HIP(hipStreamSynchronize(stream_));
-                            DDL_HIP(hipFree(fusion_));
-                            fusion_ = nullptr;
-                        }
-                        fusion_bytes_ = total + total / 2;  // x1.5 growth (MPIRTC.cc:13, 480)
-                        DDL_HIP(hipMalloc(&fusion_, fusion_bytes_));
-                    }
-                    copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(),
-                                stream_);
-                    data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
-                    copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
-                }
-                if (plan_events_.size() <= nplans) {
-                    hipEvent_t e;
-                    DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                    plan_events_.push_back(e);
-                }
-                DDL_HIP(hipEventRecord(plan_events_[nplans], stream_));
-                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
-                    const Request &r = reqs[g.second[q]];
-                    const size_t e = q == p.req_end ? p.elem_end : r.n;
-                    if (e == r.n) dones.push_back(Done{nplans, g.second[q], DDL_STATUS_OK});
-                }
-                ++nplans;
-            }
+        for (const Request &r : reqs)
+            DDL_REQUIRE(r.type == reqs[0].type, DDL_STATUS_COMM_ERROR, "agreed requests of mixed types");
+        switch (reqs[0].type) {
+            case kReqAllreduce: allreduce_reqs_(reqs, dones, nplans); break;
+            case kReqBroadcast: broadcast_reqs_(reqs, dones, nplans); break;
+            case kReqAllgather: allgather_reqs_(reqs, dones, nplans); break;
+            default: fail(DDL_STATUS_ERROR_UNKNOWN, "unknown request type");
         }
-        for (size_t i : empties) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});
     } catch (const Error &e) {
-        DDL_LOG(0, "allreduce of agreed requests failed: " << e.msg);
+        DDL_LOG(0, "collective of agreed requests failed: " << e.msg);
         status = e.status;
     }
     // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725)
@@ -404,7 +610,7 @@ void RequestHandler::execute_(const std::vector<std::string> &keys) {
         inflight_ -= reqs.size();
     }
     idle_cv_.notify_all();
-    if (status != DDL_STATUS_OK) fail(status, "keyed allreduce failed");
+    if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
 }
 
 }  // namespace ddl

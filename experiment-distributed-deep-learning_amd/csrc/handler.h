@@ -1,4 +1,5 @@
-// handler.h — keyed asynchronous allreduce requests with cross-rank negotiation and fusion.
+// handler.h — keyed asynchronous collective requests (allreduce, broadcast, allgather) with
+// cross-rank negotiation and fusion.
 //
 // Replaces the reference's request path below the TF op:
 //   TensorAllreduceRequest (collective/request/TensorAllreduceRequest.h:13-41)
@@ -39,16 +40,28 @@ struct ReadyEvent {
     ReadyEvent &operator=(const ReadyEvent &) = delete;
 };
 
+// Request types, numbered as the reference's Token::RequestType (rtc/Token.h:23-29); the type
+// name prefixes the key on the wire and in the pending map ("Allreduce::grad_0", as
+// RingTokenCommunicateHandler.cc:140-146 builds its ready keys).
+enum RequestType : int { kReqAllreduce = 1, kReqBroadcast = 2, kReqAllgather = 3 };
+const char *request_type_name(int type);
+
 struct Request {
+    int type = kReqAllreduce;
     std::string key;
     const void *in = nullptr;
     void *out = nullptr;
-    size_t n = 0;
+    size_t n = 0;  // elements of `in`
     int dtype = 0;
     int op = 0;
+    int root = 0;                     // broadcast: TensorBroadcastRequest::rootRank()
+    size_t first_dim = 0;             // allgather: rows of `in` (n = first_dim * row_elems)
+    size_t row_elems = 1;             //   elements per row (the shape without its first dim)
+    ddl_alloc_fn alloc = nullptr;     //   output allocation once the gathered first dim is known
     std::shared_ptr<ReadyEvent> ready;
     ddl_done_fn done = nullptr;
     void *user = nullptr;
+    std::string id() const { return std::string(request_type_name(type)) + "::" + key; }
 };
 
 struct Plan {  // makeCollectiveCommunicatePlan's (requestBegin, elementBegin, requestEnd, elementEnd)
@@ -71,7 +84,8 @@ ControlChannel &world_control();
 //           After running the agreed set, negotiate_root_finish() drains COMMUNICATE.
 //   member: receives SYNC, `intersect` (may block until the first key is registered)
 //           forwards the intersection, then receives and forwards COMMUNICATE.
-std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine);
+std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine,
+                                        int request_type = kReqAllreduce);
 void negotiate_root_finish(ControlChannel &ch);
 std::vector<std::string> negotiate_member(
     ControlChannel &ch, const Token &sync,
@@ -91,21 +105,37 @@ private:
     void main_();
     void root_round_();
     void member_round_(Token &first);
-    void execute_(const std::vector<std::string> &keys);
+    void execute_(const std::vector<std::string> &ids);
+    struct Done {
+        size_t plan;  // index into plan_events_ (kNoPlan: nothing to wait for)
+        size_t req;
+        int status;
+    };
+    static constexpr size_t kNoPlan = (size_t)-1;
+    size_t record_plan_(size_t &nplans);  // records the next plan event on stream_
+    void wait_inputs_(const Request &r, std::vector<hipEvent_t> &waited);
+    void *ensure_(void *&buf, size_t &cap, size_t need);
+    void allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
+    void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
+    void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);
 
     Communicator *owner_;
     std::shared_ptr<Communicator> data_;  // private data-plane communicator
     hipStream_t stream_ = nullptr;
-    void *fusion_ = nullptr;
+    void *fusion_ = nullptr;  // packed requests (allreduce / broadcast / allgather send side)
     size_t fusion_bytes_ = 0;
+    void *gather_ = nullptr;  // allgather receive side
+    size_t gather_bytes_ = 0;
+    void *dims_ = nullptr;    // allgather first-dim exchange
+    size_t dims_bytes_ = 0;
     SegmentCopier copier_;
     std::vector<hipEvent_t> plan_events_;
 
     std::mutex mu_;
     std::condition_variable cv_;       // new registrations / stop
     std::condition_variable idle_cv_;  // completions
-    std::map<std::string, Request> pending_;  // sorted: lexicographic key order
+    std::map<std::string, Request> pending_;  // by id "Type::key": (type name, key) order
     size_t inflight_ = 0;
     bool stop_ = false;
     std::thread thread_;

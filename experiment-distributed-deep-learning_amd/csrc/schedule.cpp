@@ -315,4 +315,89 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     }
 }
 
+void build_broadcast(RingProgram &prog, int rank, int P, int root, void *buf, size_t n, int dtype,
+                     const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(root >= 0 && root < P, DDL_STATUS_INVALID_ARGUMENT, "root " << root << " outside [0, " << P << ")");
+    prog.P = P;
+    prog.rank = rank;
+    prog.n = n;
+    prog.esize = es;
+    prog.algo = kAlgoDirect;
+    prog.R = 1;
+    prog.staging_stride = 0;
+    prog.staging_slots = 0;
+    prog.ticks.clear();
+    size_t max_chunk = 0;
+    for (int c = 0; c < P; ++c) max_chunk = std::max(max_chunk, chunk_range(n, es, P, 1, 0, c).size());
+    int K = 1;
+    if (cfg.slice_bytes > 0) K = (int)std::max<size_t>(1, (max_chunk * es + cfg.slice_bytes - 1) / cfg.slice_bytes);
+    K = std::max(1, std::min(K, cfg.max_slices));
+    prog.K = K;
+    if (P <= 1 || n == 0) return;
+    char *b = static_cast<char *>(buf);
+    auto slice = [&](int c, int k) { return slice_range(chunk_range(n, es, P, 1, 0, c), es, K, k); };
+    for (int t = 0; t <= K; ++t) {
+        Tick tk;
+        tk.reduce.count = 0;
+        if (t < K) {  // scatter slice t
+            if (rank == root) {
+                for (int d = 1; d < P; ++d) {
+                    const int c = (root + d) % P;
+                    const Range r = slice(c, t);
+                    if (r.size()) tk.ops.push_back(P2POp{true, c, 0, b + r.begin * es, r.size() * es});
+                }
+            } else {
+                const Range r = slice(rank, t);
+                if (r.size()) tk.ops.push_back(P2POp{false, root, 0, b + r.begin * es, r.size() * es});
+            }
+        }
+        if (t >= 1) {  // allgather slice t-1: every chunk owner sends to every non-root peer
+            const int k = t - 1;
+            const Range mine = slice(rank, k);
+            for (int d = 1; d < P; ++d) {
+                const int q = (rank + d) % P;
+                if (q != root && mine.size()) tk.ops.push_back(P2POp{true, q, 1, b + mine.begin * es, mine.size() * es});
+            }
+            if (rank != root) {
+                for (int d = 1; d < P; ++d) {
+                    const int q = (rank + P - d) % P;
+                    const Range r = slice(q, k);
+                    if (r.size()) tk.ops.push_back(P2POp{false, q, 1, b + r.begin * es, r.size() * es});
+                }
+            }
+        }
+        prog.ticks.push_back(std::move(tk));
+    }
+}
+
+void build_allgatherv(RingProgram &prog, int rank, int P, const void *send, void *recv,
+                      const size_t *counts, const size_t *displs, int dtype) {
+    const size_t es = dtype_size(dtype);
+    prog.P = P;
+    prog.rank = rank;
+    prog.esize = es;
+    prog.algo = kAlgoDirect;
+    prog.R = 1;
+    prog.K = 1;
+    prog.staging_stride = 0;
+    prog.staging_slots = 0;
+    prog.ticks.clear();
+    prog.n = 0;
+    for (int q = 0; q < P; ++q) prog.n += counts[q];
+    if (prog.n == 0) return;
+    char *r = static_cast<char *>(recv);
+    Tick tk;
+    tk.reduce.count = 0;
+    const size_t mine = counts[rank] * es;
+    char *dst = r + displs[rank] * es;
+    if (mine && dst != send) tk.copies.push_back(CopyOp{send, dst, mine});
+    for (int d = 1; d < P; ++d) {
+        const int to = (rank + d) % P, from = (rank + P - d) % P;
+        if (mine) tk.ops.push_back(P2POp{true, to, 0, const_cast<void *>(send), mine});
+        if (counts[from]) tk.ops.push_back(P2POp{false, from, 0, r + displs[from] * es, counts[from] * es});
+    }
+    prog.ticks.push_back(std::move(tk));
+}
+
 }  // namespace ddl

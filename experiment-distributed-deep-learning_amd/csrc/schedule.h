@@ -44,7 +44,14 @@ struct P2POp {
     size_t bytes;
 };
 
+struct CopyOp {  // device-to-device copy posted on the comm stream before the tick's group
+    const void *src;
+    void *dst;
+    size_t bytes;
+};
+
 struct Tick {
+    std::vector<CopyOp> copies;
     std::vector<P2POp> ops;
     SegTable reduce;       // valid when has_reduce && !multi
     SegTableN reduceN;     // valid when has_reduce && multi (direct schedule)
@@ -85,5 +92,19 @@ size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cf
 // Builds rank `rank`'s program. in/out are that rank's buffers, staging its scratch.
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
                    size_t n, int dtype, const RingConfig &cfg);
+
+// Broadcast of `root`'s n elements into every rank's `buf` (MPICommunicator.cc:77-90 is
+// MPI_Bcast): scatter (root sends chunk c to rank c) + direct allgather of the chunks, K
+// slices pipelined so the allgather of slice k shares a tick with the scatter of slice k+1.
+// Every xGMI link out of the root carries 2S/P instead of S. Ticks 0..K; tag 0 scatter,
+// tag 1 allgather (within a tick, ops to one peer are posted tag 0 first on both sides).
+void build_broadcast(RingProgram &prog, int rank, int P, int root, void *buf, size_t n, int dtype,
+                     const RingConfig &cfg);
+
+// Allgatherv (MPICommunicator.cc:31-60 is MPI_Allgatherv): rank q's counts[q] elements land at
+// recv + displs[q] on every rank. One tick: a copy of the own block (unless already in
+// place) and, for every peer, one send of the own block and one recv of the peer's block.
+void build_allgatherv(RingProgram &prog, int rank, int P, const void *send, void *recv,
+                      const size_t *counts, const size_t *displs, int dtype);
 
 }  // namespace ddl

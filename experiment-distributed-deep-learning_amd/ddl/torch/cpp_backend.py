@@ -21,6 +21,8 @@ STATUS_NAMES = {0: 'OK', 1: 'COMM_ERROR', 2: 'ERROR_UNKNOWN', 3: 'INVALID_ARGUME
 OP_SUM = 0
 
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p)
+# ddl_alloc_fn: output allocation of a keyed allgather (first_dim, bytes, user) -> device pointer
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p)
 
 
 class DDLError(RuntimeError):
@@ -87,6 +89,18 @@ class CPPBackend:
         sig('ddl_allreduce_submit_batch', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
             ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, vp, DONE_FN, ctypes.POINTER(vp))
         sig('ddl_wait_all', ci, cid)
+        sig('ddl_broadcast_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
+        sig('ddl_allgather_submit', ci, cid, ctypes.c_char_p, vp, sz, sz, ci, vp, ALLOC_FN, DONE_FN, vp)
+        sig('ddl_broadcast', ci, cid, vp, sz, ci, ci, vp)
+        sig('ddl_allgatherv', ci, cid, vp, sz, vp, ctypes.POINTER(sz), ctypes.POINTER(sz), ci, vp)
+        sig('ddl_allgather', ci, cid, vp, sz, vp, sz, ci, vp)
+        sig('ddl_local_broadcast', ci, ci, ci, ctypes.POINTER(vp), sz, ci, vp)
+        sig('ddl_local_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
+            ctypes.POINTER(sz), ci, vp)
+        sig('ddl_broadcast_program', ci, ci, ci, ci, sz, ci, ctypes.POINTER(ctypes.c_longlong), sz,
+            ctypes.POINTER(sz))
+        sig('ddl_allgather_program', ci, ci, ci, ctypes.POINTER(sz), ctypes.POINTER(sz), ci,
+            ctypes.POINTER(ctypes.c_longlong), sz, ctypes.POINTER(sz))
         sig('ddl_tune_result', ci, cid, sz, ctypes.POINTER(ci), ctypes.POINTER(ci),
             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_float), ci)
         sig('ddl_local_tune', ci, ci, sz, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci),

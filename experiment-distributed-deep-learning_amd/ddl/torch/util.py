@@ -19,7 +19,7 @@ def ddl_dtype(t: torch.Tensor) -> int:
     try:
         return _DTYPES[t.dtype]
     except KeyError:
-        raise TypeError(f'allreduce: unsupported dtype {t.dtype} '
+        raise TypeError(f'ddl: unsupported dtype {t.dtype} '
                         f'(supported: {sorted(str(d) for d in _DTYPES)})') from None
 
 

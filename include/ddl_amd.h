@@ -72,6 +72,12 @@ typedef long long ddl_communicator_id;
  * (reference TensorCommunicateRequest.h:41). Runs on the communicator's engine thread. */
 typedef void (*ddl_done_fn)(int status, void *user);
 
+/* Output allocation of a keyed allgather, called on the engine thread once the gathered first
+ * dimension is known (the reference allocates through OpContext::allocateOutput,
+ * MPIRingTokenCommunication.cc:299-306): returns a device buffer of `bytes` for an output of
+ * `first_dim` rows, or NULL on failure (the request then completes with an error). */
+typedef void *(*ddl_alloc_fn)(size_t first_dim, size_t bytes, void *user);
+
 /* ---- library / lifecycle ------------------------------------------------------- */
 int ddl_version(void);
 const char *ddl_last_error(void);
@@ -124,6 +130,19 @@ void py_error(const char *log_str);
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements,
                   int dtype, int op, void *hip_stream);
 
+/* Communicator::broadcast (reference Communicator.h:81-92, MPI_Bcast at MPICommunicator.cc:77-90):
+ * root's `elements` of `buf` into every rank's `buf`. Scatter + direct allgather over RCCL
+ * send/recv (each xGMI link out of the root carries 2S/P, not S). Stream-ordered. */
+int ddl_broadcast(ddl_communicator_id id, void *buf, size_t elements, int dtype, int root, void *hip_stream);
+/* Communicator::allgather, per-rank counts (Communicator.h:50-66, MPI_Allgatherv at
+ * MPICommunicator.cc:31-60): rank q's recv_counts[q] elements land at recv + displs[q] (in
+ * elements) on every rank; send_elements must equal recv_counts[rank]. Stream-ordered. */
+int ddl_allgatherv(ddl_communicator_id id, const void *send, size_t send_elements, void *recv,
+                   const size_t *recv_counts, const size_t *displs, int dtype, void *hip_stream);
+/* Communicator::allgather, equal counts (Communicator.h:68-79): rank q's block at q*recv_elements. */
+int ddl_allgather(ddl_communicator_id id, const void *send, size_t send_elements, void *recv,
+                  size_t recv_elements, int dtype, void *hip_stream);
+
 /* Host-resident buckets (the reference's deployment case: CPU tensors behind the MPI buffers,
  * MPIRingTokenCommunication.cc:548-733): chunked H2D -> ddl_allreduce -> D2H pipeline on three
  * streams ("host_chunk_bytes", default 32 MiB, double-buffered in HBM). Pageable memory is
@@ -158,6 +177,20 @@ int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in
 /* Batch form: registers `count` keyed requests at once (one input-ready event on hip_stream,
  * one wake-up of the engine thread); users[i] (or NULL) is passed to done for request i.
  * All-or-nothing: a duplicate key rejects the whole batch. */
+/* Keyed broadcast (TF op Broadcast, op/tensorflow/BroadcastOp.cc; TensorBroadcastRequest.h:13-40):
+ * `out` on every rank receives root's `in`. Negotiated and fused like allreduce requests
+ * (dtype groups, plans, MPIRingTokenCommunication.cc:367-419); requests of different roots
+ * run as separate groups. */
+int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                         int dtype, int root, void *hip_stream, ddl_done_fn done, void *user);
+/* Keyed allgather (TF op Allgather, op/tensorflow/AllgatherOp.cc; TensorAllgatherRequest.h):
+ * `in` holds first_dim rows of row_elements; the output holds every rank's rows in rank order
+ * (first dims may differ per rank, row_elements may not). Once the gathered first dim is known
+ * `alloc(total_rows, bytes, user)` supplies the output buffer, then `done` fires
+ * (MPIRingTokenCommunication.cc:160-364). */
+int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in, size_t first_dim,
+                         size_t row_elements, int dtype, void *hip_stream, ddl_alloc_fn alloc,
+                         ddl_done_fn done, void *user);
 int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys,
                                const void *const *ins, void *const *outs, const size_t *elements,
                                const int *dtypes, int op, void *hip_stream, ddl_done_fn done,
@@ -197,6 +230,11 @@ int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int coun
 int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *recvs,
                              size_t elements, int dtype, int op, void *hip_stream);
 
+/* Broadcast / allgatherv of P virtual ranks on one GPU (as ddl_local_ring_allreduce). */
+int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream);
+int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                         const size_t *displs, int dtype, void *hip_stream);
+
 /* ---- schedule introspection (host only, no GPU needed) -------------------------------- */
 int ddl_ring_count(int nranks, int max_rings);
 /* perm_out[p] = rank at ring position p (length nranks). */
@@ -214,6 +252,13 @@ int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slic
  * Offsets and counts in elements. Host only. */
 int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out,
                      size_t max_ops, size_t *nops);
+/* Broadcast program of `rank` (buffer 1 = the broadcast buffer) and allgatherv program
+ * (buffer 0 = send, 1 = recv), same row format; copy rows: {tick, 4, -1, -1, 1, dst offset,
+ * count, src offset in buffer 0}. */
+int ddl_broadcast_program(int rank, int nranks, int root, size_t elements, int dtype, long long *ops_out,
+                          size_t max_ops, size_t *nops);
+int ddl_allgather_program(int rank, int nranks, const size_t *counts, const size_t *displs, int dtype,
+                          long long *ops_out, size_t max_ops, size_t *nops);
 /* Fusion plans (requestBegin, elementBegin, requestEnd, elementEnd) over `count` requests of
  * one dtype group, capped at `limit` bytes (makeCollectiveCommunicatePlan,
  * MPIRingTokenCommunication.cc:495-546). plans_out holds 4*max_plans entries. */

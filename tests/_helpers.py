@@ -39,6 +39,12 @@ class Oracle:
         L.ddlo_allreduce_direct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.c_void_p, SZ]
         L.ddlo_fold.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, SZ]
+        PV = ctypes.POINTER(ctypes.c_void_p)
+        L.ddlo_broadcast.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, PV, SZ]
+        L.ddlo_allgatherv.argtypes = [ctypes.c_int, ctypes.c_int, PV, ctypes.POINTER(SZ), ctypes.POINTER(SZ),
+                                      ctypes.c_void_p]
+        L.ddlo_allgather_requests.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(SZ),
+                                              ctypes.POINTER(SZ), PV, PV]
         L.ddlo_chunk_range.argtypes = [SZ, SZ, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(SZ), ctypes.POINTER(SZ)]
         L.ddlo_make_plan.argtypes = [ctypes.POINTER(SZ), ctypes.POINTER(SZ), SZ, SZ, ctypes.POINTER(SZ), SZ]
@@ -89,6 +95,40 @@ class Oracle:
         arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
         assert self.lib.ddlo_fold(dt, ptr(out), arr, len(xs), xs[0].size) == 0
         return out
+
+    def broadcast(self, dt, xs, root):
+        outs = [np.ascontiguousarray(x).copy() for x in xs]
+        arr = (ctypes.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+        assert self.lib.ddlo_broadcast(dt, len(outs), root, arr, outs[0].size) == 0
+        return outs
+
+    def allgatherv(self, dt, sends, displs=None, total=None):
+        """Every rank's recv buffer (identical): send_q at displs[q] (default: packed)."""
+        sends = [np.ascontiguousarray(x) for x in sends]
+        counts = [x.size for x in sends]
+        if displs is None:
+            displs = list(np.cumsum([0] + counts[:-1]))
+        if total is None:
+            total = max([d + c for d, c in zip(displs, counts)], default=0)
+        recv = np.zeros(total, dtype=sends[0].dtype)
+        arr = (ctypes.c_void_p * len(sends))(*[x.ctypes.data for x in sends])
+        assert self.lib.ddlo_allgatherv(dt, len(sends), arr, (SZ * len(sends))(*counts),
+                                        (SZ * len(sends))(*[int(d) for d in displs]), ptr(recv)) == 0
+        return recv
+
+    def allgather_requests(self, dt, per_rank):
+        """per_rank[q][j]: rank q's request j as a 2-D array (rows, row_elems)."""
+        P, nreq = len(per_rank), len(per_rank[0])
+        fd = [per_rank[q][j].shape[0] for q in range(P) for j in range(nreq)]
+        re = [int(np.prod(per_rank[0][j].shape[1:])) for j in range(nreq)]
+        ins = [np.ascontiguousarray(per_rank[q][j]) for q in range(P) for j in range(nreq)]
+        outs = [np.zeros((sum(per_rank[q][j].shape[0] for q in range(P)),) + per_rank[0][j].shape[1:],
+                         dtype=per_rank[0][j].dtype) for j in range(nreq)]
+        ia = (ctypes.c_void_p * len(ins))(*[x.ctypes.data for x in ins])
+        oa = (ctypes.c_void_p * max(1, nreq))(*[o.ctypes.data for o in outs])
+        assert self.lib.ddlo_allgather_requests(dt, P, nreq, (SZ * len(fd))(*fd), (SZ * max(1, nreq))(*re), ia,
+                                                oa) == 0
+        return outs
 
     def chunk_range(self, n, esize, P, R, ring, chunk):
         b, e = SZ(), SZ()
@@ -159,6 +199,42 @@ def ring_program(lib, rank, P, n, dt):
     st = lib.ddl_ring_program(rank, P, n, dt, buf, cap, ctypes.byref(nops))
     assert st == 0, lib.ddl_last_error()
     return np.frombuffer(buf, dtype=np.int64, count=8 * nops.value).reshape(-1, 8).copy()
+
+
+def program(lib, fn, *args):
+    """Rows of a program dump entry (ddl_ring_program / ddl_broadcast_program / ...)."""
+    cap = 1 << 16
+    buf = (ctypes.c_longlong * (8 * cap))()
+    nops = SZ()
+    st = getattr(lib, fn)(*args, buf, cap, ctypes.byref(nops))
+    assert st == 0, lib.ddl_last_error()
+    return np.frombuffer(buf, dtype=np.int64, count=8 * nops.value).reshape(-1, 8).copy()
+
+
+def simulate_moves(progs, bufs):
+    """Run data-movement-only programs (copies and matched sends/recvs, no reduces):
+    bufs[r] = [buffer 0, buffer 1] of rank r; a send and a recv match on (tick, pair, tag) in
+    posting order, as RCCL matches p2p operations of a group."""
+    P = len(progs)
+    T = int(max((p[:, 0].max() for p in progs if len(p)), default=-1)) + 1
+    for t in range(T):
+        for r in range(P):
+            for row in progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 4)]:
+                _, _, _, _, b, off, cnt, soff = row
+                bufs[r][b][off:off + cnt] = bufs[r][0][soff:soff + cnt]
+        sends = {}
+        for r in range(P):
+            for row in progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 0)]:
+                _, _, peer, tag, b, off, cnt, _ = row
+                sends.setdefault((r, peer, tag), []).append(bufs[r][b][off:off + cnt].copy())
+        for r in range(P):
+            for row in progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 1)]:
+                _, _, peer, tag, b, off, cnt, _ = row
+                data = sends[(peer, r, tag)].pop(0)
+                assert data.size == cnt
+                bufs[r][b][off:off + cnt] = data
+        assert all(not v for v in sends.values()), f'unmatched sends at tick {t}'
+    return bufs
 
 
 def simulate_ring(oracle, lib, dt, xs):

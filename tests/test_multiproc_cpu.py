@@ -158,3 +158,65 @@ def test_token_ring_negotiation(world):
             rounds, err = res[r]
             assert rounds is not None, f'rank {r}: {err}'
             assert rounds[rd] == want, f'rank {r} round {rd}'
+
+
+def _moves_worker(rank, world, port, kind, q):
+    """Broadcast / allgatherv programs over gloo: one isend/irecv set per tick."""
+    try:
+        _setup_paths()
+        import _helpers as h
+        from ddl.torch.cpp_backend import CPPBackend
+        lib = CPPBackend.c_api()
+        ora = h.Oracle()
+        dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+        dt = 1
+        if kind == 'broadcast':
+            n, root = 70_001, world - 1
+            xs = [h.random_input(dt, n, 11 + r) for r in range(world)]
+            assert lib.ddl_set_config(b'slice_bytes', 32 << 10) == 0
+            prog = h.program(lib, 'ddl_broadcast_program', rank, world, root, n, dt)
+            bufs = [np.zeros(0, np.float32), xs[rank].copy()]
+            want = ora.broadcast(dt, xs, root)[rank]
+        else:
+            counts = [1000 * (r + 1) + 3 for r in range(world)]
+            displs = list(np.cumsum([0] + counts[:-1]))
+            xs = [h.random_input(dt, c, 21 + r) for r, c in enumerate(counts)]
+            C, D = (h.SZ * world)(*counts), (h.SZ * world)(*[int(d) for d in displs])
+            prog = h.program(lib, 'ddl_allgather_program', rank, world, C, D, dt)
+            bufs = [xs[rank].copy(), np.zeros(sum(counts), np.float32)]
+            want = ora.allgatherv(dt, xs)
+        for t in sorted(set(prog[:, 0].tolist())):
+            rows = prog[prog[:, 0] == t]
+            for row in rows[rows[:, 1] == 4]:
+                _, _, _, _, b, off, cnt, soff = row
+                bufs[b][off:off + cnt] = bufs[0][soff:soff + cnt]
+            reqs = []
+            for row in rows[rows[:, 1] == 1]:
+                _, _, peer, tag, b, off, cnt, _ = row
+                reqs.append(dist.irecv(torch.from_numpy(bufs[b][off:off + cnt]), src=int(peer), tag=int(tag)))
+            for row in rows[rows[:, 1] == 0]:
+                _, _, peer, tag, b, off, cnt, _ = row
+                reqs.append(dist.isend(torch.from_numpy(bufs[b][off:off + cnt].copy()), dst=int(peer), tag=int(tag)))
+            for r in reqs:
+                r.wait()
+        ok = bufs[1].tobytes() == want.tobytes()
+        dist.destroy_process_group()
+        q.put((rank, ok, ''))
+    except Exception as e:
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('kind', ['broadcast', 'allgatherv'])
+def test_broadcast_allgather_programs_over_gloo(world, kind):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_moves_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok, f'rank {rank}: {err or "result differs from the oracle"}'
