@@ -44,6 +44,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe) measurement')
     ap.add_argument('--no-fusion', action='store_true', help='skip the C5 many-bucket fusion measurement')
+    ap.add_argument('--no-c4', action='store_true', help='N>1: skip the C4 fp16 64 x 16 MiB measurement')
+    ap.add_argument('--no-collectives', action='store_true', help='N>1: skip broadcast/allgather timing')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
     ap.add_argument('--watchdog-s', type=float, default=900.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
@@ -337,21 +339,24 @@ def multi_gpu(args):
         check(lib.ddl_allreduce_variant(comm.id, send.data_ptr(), recv.data_ptr(), n, DT_FLOAT, 0,
                                         stream.cuda_stream, variant), 'ddl_allreduce_variant')
 
-    def timed(variant, steps, warmup):
+    def timed_fn(fn, steps, warmup):
         for _ in range(warmup):
-            step(variant)
+            fn()
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            step(variant)
+            fn()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         dist.barrier()
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / steps
+
+    def timed(variant, steps, warmup):
+        return timed_fn(lambda: step(variant), steps, warmup)
 
     sec = timed(0, args.steps, args.warmup)
     # reduce-kernel roofline: time every reduce launch on the engine's compute stream
@@ -406,6 +411,37 @@ def multi_gpu(args):
     cs_max, cs_min = cs.clone(), cs.clone()
     dist.all_reduce(cs_max, op=dist.ReduceOp.MAX)
     dist.all_reduce(cs_min, op=dist.ReduceOp.MIN)
+    # C4: fp16, 1 GiB as 64 x 16 MiB buckets, one ddl_allreduce per bucket
+    c4 = None
+    if not args.no_c4:
+        nb = (16 << 20) // 2
+        c4_bufs = [torch.randn(nb, device=dev, generator=g).half() for _ in range(64)]
+
+        def c4_step():
+            for b in c4_bufs:
+                check(lib.ddl_allreduce(comm.id, b.data_ptr(), b.data_ptr(), nb, 19, 0, stream.cuda_stream),
+                      'ddl_allreduce')
+        t = timed_fn(c4_step, 3, 1)
+        c4 = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
+              'algbw_GiBs': round((1 << 30) / GiB / t, 2),
+              'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
+        del c4_bufs
+    # broadcast (root 0) and allgather of the same bucket size (§8f #3)
+    colls = None
+    if not args.no_collectives:
+        bc = recv.clone()
+        t_b = timed_fn(lambda: check(lib.ddl_broadcast(comm.id, bc.data_ptr(), n, DT_FLOAT, 0, stream.cuda_stream),
+                                     'ddl_broadcast'), max(5, args.steps // 4), 2)
+        per = n // world
+        t_g = timed_fn(lambda: check(lib.ddl_allgather(comm.id, send.data_ptr(), per, recv.data_ptr(), per, DT_FLOAT,
+                                                       stream.cuda_stream), 'ddl_allgather'),
+                       max(5, args.steps // 4), 2)
+        colls = {'broadcast': {'bytes': S, 'ms': round(t_b * 1e3, 4), 'algbw_GiBs': round(S / GiB / t_b, 2),
+                               'root_link_bytes': 2 * S // world},
+                 'allgather': {'bytes_out': per * world * 4, 'ms': round(t_g * 1e3, 4),
+                               'algbw_GiBs': round(per * world * 4 / GiB / t_g, 2),
+                               'busbw_GBs': round((world - 1) * per * 4 / t_g / 1e9, 2)}}
+        del bc
     host = None if args.no_host else host_resident_rate(lib, comm, S, reps=4)
     fusion = None if args.no_fusion else fusion_c5(lib, comm, dev, steps=3)
 
@@ -446,6 +482,8 @@ def multi_gpu(args):
                                     if tune and tune['chosen']['algo'] == 'direct' else
                                     'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
                          'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
+            'c4_fp16_64x16MiB': c4,
+            'broadcast_allgather': colls,
             'host_resident': host,
             'fusion_c5': fusion,
             'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
