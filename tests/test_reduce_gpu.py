@@ -121,3 +121,40 @@ def test_pack_unpack_roundtrip(lib, gpu):
         assert np.array_equal(f[off:off + s], src.cpu().numpy())
         assert torch.equal(out, src)
         off += (s + 255) // 256 * 256
+
+
+@pytest.mark.parametrize('case', ['dense_tiny', 'many_segments', 'unaligned', 'zero_lengths'])
+def test_pack_unpack_layouts(lib, gpu, case):
+    """Segment tables the span kernel must resolve: > 64 segments per 64 KiB span (global-walk
+    fallback), > 4096 segments (3 search rounds), byte-misaligned pointers (byte path), and
+    zero-length segments sharing an offset with their successor."""
+    rng = np.random.default_rng(hash(case) % 1000)
+    if case == 'dense_tiny':
+        sizes = [int(s) for s in rng.integers(1, 300, size=3000)]
+    elif case == 'many_segments':
+        sizes = [int(s) for s in rng.integers(1, 5000, size=9000)]
+    elif case == 'unaligned':
+        sizes = [int(s) for s in rng.integers(1, 40_000, size=200)]
+    else:
+        sizes = [0, 5, 0, 0, 300, 0, 70_000, 0, 17]
+    pool = torch.from_numpy(rng.integers(0, 255, size=sum(sizes) + 16 * len(sizes) + 64, dtype=np.uint8)).to(gpu)
+    outpool = torch.zeros_like(pool)
+    offs, o = [], 3 if case == 'unaligned' else 0
+    for s in sizes:
+        offs.append(o)
+        o += s + (int(rng.integers(1, 16)) if case == 'unaligned' else 0)
+    total = sum((s + 255) // 256 * 256 for s in sizes)
+    fused = torch.zeros(max(total, 1), dtype=torch.uint8, device=gpu)
+    P = ctypes.c_void_p * len(sizes)
+    S = ctypes.c_size_t * len(sizes)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert lib.ddl_pack(fused.data_ptr(), P(*[pool.data_ptr() + x for x in offs]), S(*sizes), len(sizes), stream) == 0
+    assert lib.ddl_unpack(P(*[outpool.data_ptr() + x for x in offs]), fused.data_ptr(), S(*sizes), len(sizes),
+                          stream) == 0
+    torch.cuda.synchronize()
+    f, src, dst = fused.cpu().numpy(), pool.cpu().numpy(), outpool.cpu().numpy()
+    off = 0
+    for s, x in zip(sizes, offs):
+        assert np.array_equal(f[off:off + s], src[x:x + s])
+        assert np.array_equal(dst[x:x + s], src[x:x + s])
+        off += (s + 255) // 256 * 256
