@@ -56,6 +56,35 @@ const char *request_type_name(int type) {
     }
 }
 
+int type_order(int type) {  // rank of the type name in byte order
+    switch (type) {
+        case kReqAllgather: return 0;
+        case kReqAllreduce: return 1;
+        case kReqBroadcast: return 2;
+        default: return 3;
+    }
+}
+
+ReqId req_id(const Request &r) { return ReqId{type_order(r.type), r.key}; }
+
+namespace {
+const int kTypeByOrder[3] = {kReqAllgather, kReqAllreduce, kReqBroadcast};
+}
+
+std::string wire_id(const ReqId &id) {
+    DDL_REQUIRE(id.order >= 0 && id.order < 3, DDL_STATUS_ERROR_UNKNOWN, "bad request id");
+    return std::string(request_type_name(kTypeByOrder[id.order])) + "::" + id.key;
+}
+
+ReqId parse_wire_id(const std::string &s) {
+    const size_t sep = s.find("::");
+    DDL_REQUIRE(sep != std::string::npos, DDL_STATUS_COMM_ERROR, "token: malformed request id '" << s << "'");
+    const std::string name = s.substr(0, sep);
+    for (int o = 0; o < 3; ++o)
+        if (name == request_type_name(kTypeByOrder[o])) return ReqId{o, s.substr(sep + 2)};
+    fail(DDL_STATUS_COMM_ERROR, "token: unknown request type '" + name + "'");
+}
+
 ReadyEvent::ReadyEvent(hipStream_t s) {
     DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipError_t r = hipEventRecord(e, s);
@@ -136,10 +165,10 @@ void RequestHandler::submit(Request r) {
     {
         std::lock_guard<std::mutex> g(mu_);
         DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
-        const std::string id = r.id();
+        ReqId id = req_id(r);
         DDL_REQUIRE(pending_.find(id) == pending_.end(), DDL_STATUS_DUPLICATE_KEY,
                     "a request with key '" << r.key << "' is already pending");
-        pending_.emplace(id, r);
+        pending_.emplace(std::move(id), std::move(r));
     }
     cv_.notify_all();
 }
@@ -149,11 +178,23 @@ void RequestHandler::submit_batch(std::vector<Request> &rs) {
     {
         std::lock_guard<std::mutex> g(mu_);
         DDL_REQUIRE(!stop_, DDL_STATUS_NOT_INITIALIZED, "handler is shutting down");
-        std::set<std::string> seen;
-        for (const Request &r : rs)
-            DDL_REQUIRE(pending_.find(r.id()) == pending_.end() && seen.insert(r.id()).second,
-                        DDL_STATUS_DUPLICATE_KEY, "a request with key '" << r.key << "' is already pending");
-        for (Request &r : rs) pending_.emplace(r.id(), r);
+        std::vector<ReqId> ids;
+        ids.reserve(rs.size());
+        for (const Request &r : rs) ids.push_back(req_id(r));
+        std::vector<size_t> order(rs.size());
+        for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ids[a] < ids[b]; });
+        for (size_t i = 0; i < order.size(); ++i) {
+            const ReqId &id = ids[order[i]];
+            DDL_REQUIRE(pending_.find(id) == pending_.end() && (i == 0 || ids[order[i - 1]] < id),
+                        DDL_STATUS_DUPLICATE_KEY, "a request with key '" << id.key << "' is already pending");
+        }
+        // sorted insertion with hints: amortised O(1) per request
+        auto hint = pending_.end();
+        for (size_t i = order.size(); i-- > 0;) {
+            const size_t j = order[i];
+            hint = pending_.emplace_hint(hint, std::move(ids[j]), std::move(rs[j]));
+        }
     }
     cv_.notify_all();
 }
@@ -164,7 +205,7 @@ void RequestHandler::wait_all() {
 }
 
 void RequestHandler::fail_all_(int status) {
-    std::map<std::string, Request> left;
+    std::map<ReqId, Request> left;
     {
         std::lock_guard<std::mutex> g(mu_);
         left.swap(pending_);
@@ -182,7 +223,7 @@ void RequestHandler::main_() {
         const int P = owner_->size(), rank = owner_->rank();
         for (;;) {
             if (P == 1 || rank == 0) {
-                std::vector<std::string> keys;
+                std::vector<ReqId> keys;
                 {
                     std::unique_lock<std::mutex> lk(mu_);
                     cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
@@ -193,7 +234,7 @@ void RequestHandler::main_() {
                         cv_.wait_for(lk, std::chrono::microseconds(cycle_us), [this] { return stop_; });
                     if (stop_) break;
                     for (auto &kv : pending_)
-                        if (kv.second.type == pending_.begin()->second.type) keys.push_back(kv.first);
+                        if (kv.first.order == pending_.begin()->first.order) keys.push_back(kv.first);
                 }
                 if (P == 1) execute_(keys);
                 else root_round_();
@@ -291,10 +332,12 @@ void RequestHandler::root_round_() {
         std::lock_guard<std::mutex> g(mu_);
         if (!pending_.empty()) type = pending_.begin()->second.type;
         for (auto &kv : pending_)
-            if (kv.second.type == type) mine.push_back(kv.first);
+            if (kv.second.type == type) mine.push_back(wire_id(kv.first));
     }
     std::vector<std::string> agreed = negotiate_root(ch, mine, type);
-    execute_(agreed);
+    std::vector<ReqId> ids;
+    for (const auto &w : agreed) ids.push_back(parse_wire_id(w));
+    execute_(ids);
     negotiate_root_finish(ch);
 }
 
@@ -303,14 +346,18 @@ void RequestHandler::root_round_() {
 // forward the intersection, then forward COMMUNICATE and run the agreed set (:302-310).
 void RequestHandler::member_round_(Token &t) {
     std::vector<std::string> agreed = negotiate_member(world_control(), t, [this](const std::vector<std::string> &keys) {
+        std::vector<ReqId> proposed;
+        for (const auto &w : keys) proposed.push_back(parse_wire_id(w));
         std::vector<std::string> mine;
         std::unique_lock<std::mutex> lk(mu_);
-        if (!keys.empty()) cv_.wait(lk, [&] { return stop_ || pending_.count(keys.front()) > 0; });
-        for (const auto &k : keys)
-            if (pending_.count(k)) mine.push_back(k);
+        if (!proposed.empty()) cv_.wait(lk, [&] { return stop_ || pending_.count(proposed.front()) > 0; });
+        for (size_t i = 0; i < proposed.size(); ++i)
+            if (pending_.count(proposed[i])) mine.push_back(keys[i]);
         return mine;
     });
-    execute_(agreed);
+    std::vector<ReqId> ids;
+    for (const auto &w : agreed) ids.push_back(parse_wire_id(w));
+    execute_(ids);
 }
 
 void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
@@ -561,15 +608,16 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
     }
 }
 
-void RequestHandler::execute_(const std::vector<std::string> &ids) {
+void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     if (ids.empty()) return;
     std::vector<Request> reqs;
+    reqs.reserve(ids.size());
     {
         std::lock_guard<std::mutex> g(mu_);
         for (const auto &k : ids) {
             auto it = pending_.find(k);
-            DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed request '" << k << "' is not registered");
-            reqs.push_back(it->second);
+            DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed request '" << k.key << "' is not registered");
+            reqs.push_back(std::move(it->second));
             pending_.erase(it);
         }
         inflight_ += reqs.size();

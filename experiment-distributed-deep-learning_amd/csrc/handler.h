@@ -61,8 +61,20 @@ struct Request {
     std::shared_ptr<ReadyEvent> ready;
     ddl_done_fn done = nullptr;
     void *user = nullptr;
-    std::string id() const { return std::string(request_type_name(type)) + "::" + key; }
 };
+
+// Request identity: (type, key), ordered as the reference's (typeName, key) pairs —
+// "Allgather" < "Allreduce" < "Broadcast", then the key bytewise. On the wire it is the string
+// "<TypeName>::<key>".
+struct ReqId {
+    int order;  // type_order(type)
+    std::string key;
+    bool operator<(const ReqId &o) const { return order != o.order ? order < o.order : key < o.key; }
+};
+int type_order(int type);
+ReqId req_id(const Request &r);
+std::string wire_id(const ReqId &id);
+ReqId parse_wire_id(const std::string &s);  // throws on an unknown type name
 
 struct Plan {  // makeCollectiveCommunicatePlan's (requestBegin, elementBegin, requestEnd, elementEnd)
     size_t req_begin, elem_begin, req_end, elem_end;
@@ -105,7 +117,7 @@ private:
     void main_();
     void root_round_();
     void member_round_(Token &first);
-    void execute_(const std::vector<std::string> &ids);
+    void execute_(const std::vector<ReqId> &ids);
     struct Done {
         size_t plan;  // index into plan_events_ (kNoPlan: nothing to wait for)
         size_t req;
@@ -135,7 +147,7 @@ private:
     std::mutex mu_;
     std::condition_variable cv_;       // new registrations / stop
     std::condition_variable idle_cv_;  // completions
-    std::map<std::string, Request> pending_;  // by id "Type::key": (type name, key) order
+    std::map<ReqId, Request> pending_;  // (type name, key) order
     size_t inflight_ = 0;
     bool stop_ = false;
     std::thread thread_;
