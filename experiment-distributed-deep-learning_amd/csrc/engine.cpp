@@ -108,14 +108,19 @@ std::vector<RingConfig> tune_candidates(int P, const RingConfig &base) {
         c.push_back(r);
     };
     const int R = (int)rings_for(P, kMaxRings).size();
+    // slices: 512 KiB (deep recv/reduce overlap) .. 64 MiB (one slice per chunk: fewest
+    // groups — an RCCL group of 7 send/recv pairs costs ~15-22 us of host enqueue and ~30 us
+    // of device latency on MI355X, tools/rccl_group_cost.py)
     add(kAlgoRing, kMaxRings, 2u << 20, 8);
     add(kAlgoRing, kMaxRings, 512u << 10, 16);
     add(kAlgoRing, kMaxRings, 8u << 20, 8);
+    add(kAlgoRing, kMaxRings, 64u << 20, 8);
     if (R > 1) add(kAlgoRing, 1, 2u << 20, 8);
     if (P > 2 && P - 1 <= kMaxInputs) {
         add(kAlgoDirect, 1, 2u << 20, 8);
         add(kAlgoDirect, 1, 512u << 10, 16);
         add(kAlgoDirect, 1, 8u << 20, 8);
+        add(kAlgoDirect, 1, 64u << 20, 8);
     }
     return c;
 }

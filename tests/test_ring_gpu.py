@@ -206,7 +206,7 @@ def test_reduce_sumN_kernel_all_input_counts(lib, oracle, gpu):
         assert outs[0].tobytes() == want.tobytes(), P
 
 
-@pytest.mark.parametrize('P,ncand', [(2, 3), (4, 7), (8, 7)])
+@pytest.mark.parametrize('P,ncand', [(2, 4), (4, 9), (8, 9)])
 def test_local_autotune_candidates(lib, gpu, P, ncand):
     """The autotuner's procedure on P virtual ranks: the configured schedule is candidate 0,
     every candidate is timed, the chosen one is the fastest."""
