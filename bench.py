@@ -189,6 +189,12 @@ def single_gpu(args):
             size *= 4
         extra['sweep_fp32'] = sweep
 
+    # the direct schedule's fold at P = 8 (chunk = S/8, 7 received inputs) and the per-hop
+    # reduce in the C4 dtypes, on the same rotating-buffer discipline
+    if not args.no_variants:
+        extra['fold_kernel'] = fold_roofline(lib, dev, sh, S)
+        extra['reduce_half_dtypes_achieved_GBs'] = half_dtypes(lib, dev, sh, S)
+
     traffic = pmc_traffic(f'reduce_fp32_{args.bucket_mib}MiB')
     out = {
         'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
@@ -223,6 +229,64 @@ def single_gpu(args):
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
         out['cpu_reference_path'] = cpu_reference_path(P=2)
     emit(out)
+
+
+def fold_roofline(lib, dev, sh, S, nb=7):
+    """k_sumN_tile<float, 7>: out = in + 7 received slices over one P=8 chunk (S/8 fp32), the
+    direct schedule's reduce; algorithmic bytes (nb + 2) * chunk."""
+    import torch
+    from ddl.torch.cpp_backend import check
+    n = S // 8 // 4
+    sets = [[torch.rand(n, device=dev) for _ in range(nb + 2)] for _ in range(2)]  # in, 7 inputs, out
+    P = ctypes.c_void_p * nb
+
+    def run(k):
+        b = sets[k % 2]
+        check(lib.ddl_reduce_fold(b[-1].data_ptr(), b[0].data_ptr(), P(*[t.data_ptr() for t in b[1:-1]]), nb, n,
+                                  DT_FLOAT, sh), 'ddl_reduce_fold')
+    for k in range(4):
+        run(k)
+    best = float('inf')
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(20):
+            run(k)
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
+    byts = (nb + 2) * n * 4
+    return {'kernel': f'k_sumN_tile<DDL_FLOAT,{nb}>', 'chunk_bytes': n * 4, 'us': round(best * 1e6, 1),
+            'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
+            'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def half_dtypes(lib, dev, sh, S):
+    """acc += in over S bytes of fp16 / bf16 (C4's dtype), 3 rotating sets."""
+    import torch
+    from ddl.torch.cpp_backend import check
+    res = {}
+    for name, td, code in (('fp16', torch.float16, 19), ('bf16', torch.bfloat16, 14)):
+        n = S // 2
+        sets = [(torch.rand(n, device=dev).to(td), torch.rand(n, device=dev).to(td)) for _ in range(NSETS)]
+
+        def run(k):
+            a, b = sets[k % NSETS]
+            check(lib.ddl_reduce_local(a.data_ptr(), b.data_ptr(), n, code, sh), 'ddl_reduce_local')
+        for k in range(3):
+            run(k)
+        best = float('inf')
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for k in range(12):
+                run(k)
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / 12 / 1e3)
+        res[name] = round(3 * S / best / 1e9, 1)
+        del sets
+    return res
 
 
 def fusion_c5(lib, comm, dev, steps, k=4096):

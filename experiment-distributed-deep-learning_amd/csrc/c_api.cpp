@@ -513,6 +513,20 @@ int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b
     });
 }
 
+int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
+                    void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nb >= 1 && nb <= kMaxInputs && ins, DDL_STATUS_INVALID_ARGUMENT, "fold inputs " << nb);
+        SegTableN t;
+        t.a = a;
+        t.out = out;
+        t.n = elements;
+        t.nb = nb;
+        for (int i = 0; i < nb; ++i) t.b[i] = ins[i];
+        launch_sumN(t, dtype, as_stream(hip_stream));
+    });
+}
+
 int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype, void *hip_stream) {
     return ddl_reduce_sum2_variant(-1, out, a, b, elements, dtype, hip_stream);
 }

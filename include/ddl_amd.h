@@ -216,6 +216,10 @@ int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, in
  * 8 = operand b staged through LDS by global_load_lds_dwordx4. */
 int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b,
                             size_t elements, int dtype, void *hip_stream);
+/* The direct schedule's fold: out[i] = a[i] + ins[0][i] + ... + ins[nb-1][i], 1 <= nb <= 15,
+ * left to right; fp16/bf16 accumulate in fp32 and round once. out may alias a. */
+int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
+                    void *hip_stream);
 
 /* Fusion pack/unpack (device): gathers `count` segments into one contiguous buffer and
  * scatters it back (executeCommunicatePlan_'s memcpy in/out, MPIRingTokenCommunication.cc:548-733). */

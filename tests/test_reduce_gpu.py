@@ -158,3 +158,25 @@ def test_pack_unpack_layouts(lib, gpu, case):
         assert np.array_equal(f[off:off + s], src[x:x + s])
         assert np.array_equal(dst[x:x + s], src[x:x + s])
         off += (s + 255) // 256 * 256
+
+
+@pytest.mark.parametrize('dt', [1, 2, 3, 9, 14, 19, 23])
+@pytest.mark.parametrize('nb', [1, 2, 7, 15])
+@pytest.mark.parametrize('n,misalign', [(1, 0), (4099, 0), (300_001, 0), (10_007, 1)])
+def test_reduce_fold_kernel(lib, oracle, gpu, dt, nb, n, misalign):
+    """k_sumN_tile / k_sumN_scalar alone: out = a + x_0 + ... + x_{nb-1} vs the oracle's fold
+    (fp16/bf16: fp32 accumulation, one rounding), vector and misaligned paths, ragged tails."""
+    from _helpers import random_input
+    xs = [random_input(dt, n + misalign, 900 + 13 * i + dt) for i in range(nb + 1)]
+    ts = [to_dev(x, gpu) for x in xs]
+    es = xs[0].itemsize
+    ptrs = [t.data_ptr() + misalign * es for t in ts]
+    out = torch.zeros_like(ts[0])
+    P = ctypes.c_void_p * nb
+    st = lib.ddl_reduce_fold(out.data_ptr() + misalign * es, ptrs[0], P(*ptrs[1:]), nb, n, dt,
+                             torch.cuda.current_stream().cuda_stream)
+    assert st == 0, lib.ddl_last_error()
+    torch.cuda.synchronize()
+    want = oracle.fold(dt, [x[misalign:] for x in xs])
+    got = out.cpu().numpy().view(xs[0].dtype)[misalign:]
+    assert got.tobytes() == want.tobytes()
