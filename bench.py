@@ -47,7 +47,7 @@ def parse():
     ap.add_argument('--no-c4', action='store_true', help='N>1: skip the C4 fp16 64 x 16 MiB measurement')
     ap.add_argument('--no-collectives', action='store_true', help='N>1: skip broadcast/allgather timing')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
-    ap.add_argument('--watchdog-s', type=float, default=900.0, help='N>1: abort a hung run after this')
+    ap.add_argument('--watchdog-s', type=float, default=420.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--variant', type=int, default=-1,
@@ -377,9 +377,22 @@ def multi_gpu(args):
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', rank))
 
-    def hung():  # a hung collective must not eat the driver's whole scaling run
-        sys.stderr.write(f'[bench rank {rank}] watchdog: no completion after {args.watchdog_s:.0f} s, aborting\n')
+    state = {'out': None, 'leg': 'main'}  # rank 0's result so far; the leg in progress
+
+    def hung():
+        # a hung collective must not eat the driver's whole scaling run: once the headline
+        # measurement exists, rank 0 prints it with the unfinished leg named, and every rank
+        # exits 0; before that, exit 3
+        sys.stderr.write(f'[bench rank {rank}] watchdog: leg {state["leg"]!r} not done after '
+                         f'{args.watchdog_s:.0f} s, aborting\n')
         sys.stderr.flush()
+        if state.get('printed'):
+            os._exit(0)
+        if state['out'] is not None:
+            if rank == 0:
+                state['out']['incomplete'] = f'watchdog after {args.watchdog_s:.0f} s in leg {state["leg"]}'
+                emit(state['out'])
+            os._exit(0)
         os._exit(3)
 
     dog = threading.Timer(args.watchdog_s, hung)
@@ -432,9 +445,6 @@ def multi_gpu(args):
     launches, kbytes, kms = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
     check(lib.ddl_kernel_stats(comm.id, ctypes.byref(launches), ctypes.byref(kbytes), ctypes.byref(kms)),
           'ddl_kernel_stats')
-    sec_rccl = timed(1, max(5, args.steps // 2), 3)
-    # ring configurations (every rank sets the same values in the same order: the schedule
-    # must be identical on all ranks)
     # the autotuner's record for this bucket (tuned during the first warmup call)
     tune = None
     chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
@@ -447,25 +457,6 @@ def multi_gpu(args):
                   'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
                   'ms': round(tms[i], 4)} for i in range(min(count.value, 16))]
         tune = {'chosen': cands[chosen.value], 'candidates': cands}
-    # fixed schedules, tuner off (every rank sets the same values in the same order: the
-    # schedule must be identical on all ranks)
-    sweep = []
-    if not args.no_config_sweep:
-        keys = ('algo', 'rings', 'slice_bytes', 'tune')
-        defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
-        lib.ddl_set_config(b'tune', 0)
-        for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
-                                       (1, 1, 2), (1, 1, 8)):
-            if algo == 1 and world < 3:
-                continue
-            lib.ddl_set_config(b'algo', algo)
-            lib.ddl_set_config(b'rings', rings)
-            lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
-            t = timed(0, max(5, args.steps // 4), 2)
-            sweep.append({'algo': ['ring', 'direct'][algo], 'rings': rings, 'slice_MiB': slice_mib,
-                          'ms': round(t * 1e3, 4), 'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
-        for k, v in defaults.items():
-            lib.ddl_set_config(k.encode(), v)
     # correctness spot check: every rank's sum must match (checksum of checksums)
     step(0)
     torch.cuda.synchronize()
@@ -475,8 +466,72 @@ def multi_gpu(args):
     cs_max, cs_min = cs.clone(), cs.clone()
     dist.all_reduce(cs_max, op=dist.ReduceOp.MAX)
     dist.all_reduce(cs_min, op=dist.ReduceOp.MIN)
+
+    ms = sec * 1e3
+    algbw = S / GiB / sec
+    busbw_gbs = 2 * (world - 1) / world * S / sec / 1e9
+    link_ceiling = min(HBM_PEAK_GBS * 2 / 7, 7 * XGMI_LINK_GBS)  # SURVEY §8d, L = 7 links
+    avg_kernel_ms = kms.value / max(1, launches.value)
+    achieved = kbytes.value / max(1e-9, kms.value / 1e3) / 1e9
+    out = {
+        'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
+        'value': round(world * S / GiB / sec, 2),
+        'unit': 'GiB/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic N(0,1) fp32 bucket per rank, resident in HBM',
+        'config': {'workload': f'C3: allreduce (autotuned multi-ring or direct RS+AG over RCCL send/recv, '
+                               f'HIP reduce), fp32 '
+                               f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
+                   'bucket_bytes': S, 'parallelism': f'dp{world}'},
+        'algbw_GiBs': round(algbw, 2),
+        'busbw_GBs': round(busbw_gbs, 2),
+        'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
+        'autotune': tune,
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'kernel': (f'k_sumN_tile<float,{world - 1}> (direct reduce-scatter fold)'
+                                if tune and tune['chosen']['algo'] == 'direct' else
+                                'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
+                     'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
+        'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
+                  'sum_of_inputs': ref.item()},
+    }
+    state['out'] = out  # from here on a hung optional leg still reports the headline result
+
+    state['leg'] = 'rccl_comparator'
+    sec_rccl = timed(1, max(5, args.steps // 2), 3)
+    out['rccl_allreduce_comparator'] = {'ms': round(sec_rccl * 1e3, 4),
+                                        'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
+    # fixed schedules, tuner off (every rank sets the same values in the same order: the
+    # schedule must be identical on all ranks)
+    state['leg'] = 'schedule_sweep'
+    sweep = []
+    if not args.no_config_sweep:
+        keys = ('algo', 'rings', 'slice_bytes', 'tune')
+        defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
+        lib.ddl_set_config(b'tune', 0)
+        for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
+                                       (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64)):
+            if algo == 1 and world < 3:
+                continue
+            lib.ddl_set_config(b'algo', algo)
+            lib.ddl_set_config(b'rings', rings)
+            lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
+            t = timed(0, max(5, args.steps // 4), 2)
+            sweep.append({'algo': ['ring', 'direct'][algo], 'rings': rings, 'slice_MiB': slice_mib,
+                          'ms': round(t * 1e3, 4), 'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
+            out['schedule_sweep'] = sweep
+        for k, v in defaults.items():
+            lib.ddl_set_config(k.encode(), v)
     # C4: fp16, 1 GiB as 64 x 16 MiB buckets, one ddl_allreduce per bucket
-    c4 = None
+    state['leg'] = 'c4'
     if not args.no_c4:
         nb = (16 << 20) // 2
         c4_bufs = [torch.randn(nb, device=dev, generator=g).half() for _ in range(64)]
@@ -486,12 +541,12 @@ def multi_gpu(args):
                 check(lib.ddl_allreduce(comm.id, b.data_ptr(), b.data_ptr(), nb, 19, 0, stream.cuda_stream),
                       'ddl_allreduce')
         t = timed_fn(c4_step, 3, 1)
-        c4 = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
-              'algbw_GiBs': round((1 << 30) / GiB / t, 2),
-              'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
+        out['c4_fp16_64x16MiB'] = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
+                                   'algbw_GiBs': round((1 << 30) / GiB / t, 2),
+                                   'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
         del c4_bufs
     # broadcast (root 0) and allgather of the same bucket size (§8f #3)
-    colls = None
+    state['leg'] = 'broadcast_allgather'
     if not args.no_collectives:
         bc = recv.clone()
         t_b = timed_fn(lambda: check(lib.ddl_broadcast(comm.id, bc.data_ptr(), n, DT_FLOAT, 0, stream.cuda_stream),
@@ -500,60 +555,23 @@ def multi_gpu(args):
         t_g = timed_fn(lambda: check(lib.ddl_allgather(comm.id, send.data_ptr(), per, recv.data_ptr(), per, DT_FLOAT,
                                                        stream.cuda_stream), 'ddl_allgather'),
                        max(5, args.steps // 4), 2)
-        colls = {'broadcast': {'bytes': S, 'ms': round(t_b * 1e3, 4), 'algbw_GiBs': round(S / GiB / t_b, 2),
-                               'root_link_bytes': 2 * S // world},
-                 'allgather': {'bytes_out': per * world * 4, 'ms': round(t_g * 1e3, 4),
-                               'algbw_GiBs': round(per * world * 4 / GiB / t_g, 2),
-                               'busbw_GBs': round((world - 1) * per * 4 / t_g / 1e9, 2)}}
+        out['broadcast_allgather'] = {
+            'broadcast': {'bytes': S, 'ms': round(t_b * 1e3, 4), 'algbw_GiBs': round(S / GiB / t_b, 2),
+                          'root_link_bytes': 2 * S // world},
+            'allgather': {'bytes_out': per * world * 4, 'ms': round(t_g * 1e3, 4),
+                          'algbw_GiBs': round(per * world * 4 / GiB / t_g, 2),
+                          'busbw_GBs': round((world - 1) * per * 4 / t_g / 1e9, 2)}}
         del bc
-    host = None if args.no_host else host_resident_rate(lib, comm, S, reps=4)
-    fusion = None if args.no_fusion else fusion_c5(lib, comm, dev, steps=3)
-
-    ms = sec * 1e3
-    algbw = S / GiB / sec
-    busbw_gbs = 2 * (world - 1) / world * S / sec / 1e9
-    link_ceiling = min(HBM_PEAK_GBS * 2 / 7, 7 * XGMI_LINK_GBS)  # SURVEY §8d, L = 7 links
-    avg_kernel_ms = kms.value / max(1, launches.value)
-    achieved = kbytes.value / max(1e-9, kms.value / 1e3) / 1e9
+    state['leg'] = 'host_resident'
+    if not args.no_host:
+        out['host_resident'] = host_resident_rate(lib, comm, S, reps=4)
+    state['leg'] = 'fusion_c5'
+    if not args.no_fusion:
+        out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
+    state['leg'] = 'finalize'
     if rank == 0:
-        out = {
-            'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
-            'value': round(world * S / GiB / sec, 2),
-            'unit': 'GiB/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': round(ms, 4),
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': 'f32',
-            'data': 'synthetic N(0,1) fp32 bucket per rank, resident in HBM',
-            'config': {'workload': f'C3: allreduce (autotuned multi-ring or direct RS+AG over RCCL send/recv, '
-                                   f'HIP reduce), fp32 '
-                                   f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
-                       'bucket_bytes': S, 'parallelism': f'dp{world}'},
-            'algbw_GiBs': round(algbw, 2),
-            'busbw_GBs': round(busbw_gbs, 2),
-            'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
-            'rccl_allreduce_comparator': {'ms': round(sec_rccl * 1e3, 4),
-                                          'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)},
-            'autotune': tune,
-            'schedule_sweep': sweep,
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                         'kernel': (f'k_sumN_tile<float,{world - 1}> (direct reduce-scatter fold)'
-                                    if tune and tune['chosen']['algo'] == 'direct' else
-                                    'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
-                         'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
-            'c4_fp16_64x16MiB': c4,
-            'broadcast_allgather': colls,
-            'host_resident': host,
-            'fusion_c5': fusion,
-            'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
-                      'sum_of_inputs': ref.item()},
-        }
         emit(out)
+    state['printed'] = True  # a hang in teardown must not print a second line
     dist.barrier()
     from ddl.torch.communicator import finalize
     finalize()

@@ -131,6 +131,14 @@ int ddl_control_connect_ranked(int rank, int size, const char *endpoints) {
     });
 }
 
+int ddl_control_stats(long long *string_rounds, long long *cached_rounds) {
+    return guarded([&] {
+        DDL_REQUIRE(string_rounds && cached_rounds, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        *string_rounds = world_control().string_rounds;
+        *cached_rounds = world_control().cached_rounds;
+    });
+}
+
 int ddl_control_negotiate(const char *keys, char *out, size_t len) {
     return guarded([&] {
         DDL_REQUIRE(keys && out && len > 0, DDL_STATUS_INVALID_ARGUMENT, "bad negotiate args");
@@ -146,19 +154,49 @@ int ddl_control_negotiate(const char *keys, char *out, size_t len) {
             pos = nl + 1;
         }
         std::sort(mine.begin(), mine.end());
-        std::vector<std::string> agreed;
+        mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+        // this rank's ids by table index, as the handler keeps them
+        std::vector<uint8_t> held(ch.cache.size(), 0);
+        std::vector<uint32_t> idx;
+        bool cached = !mine.empty();
+        for (const auto &k : mine) {
+            uint32_t i;
+            if (ch.cache.lookup(k, &i)) {
+                held[i] = 1;
+                idx.push_back(i);
+            } else {
+                cached = false;
+            }
+        }
+        Agreed a;
         if (ch.rank() == 0) {
-            agreed = negotiate_root(ch, mine);
+            a = negotiate_root(ch, cached, idx, mine);
             negotiate_root_finish(ch);
         } else {
             Token t;
             ch.recv(t, -1);
-            agreed = negotiate_member(ch, t, [&](const std::vector<std::string> &proposed) {
-                std::vector<std::string> both;
-                for (const auto &k : proposed)
-                    if (std::binary_search(mine.begin(), mine.end(), k)) both.push_back(k);
-                return both;
-            });
+            a = negotiate_member(
+                ch, t,
+                [&](const std::vector<std::string> &proposed) {
+                    std::vector<std::string> both;
+                    for (const auto &k : proposed)
+                        if (std::binary_search(mine.begin(), mine.end(), k)) both.push_back(k);
+                    return both;
+                },
+                [&](const std::vector<uint32_t> &proposed) {
+                    std::vector<uint32_t> both;
+                    for (uint32_t i : proposed)
+                        if (i < held.size() && held[i]) both.push_back(i);
+                    return both;
+                });
+        }
+        std::vector<std::string> agreed;
+        if (a.cached) {
+            for (uint32_t i : a.idx) agreed.push_back(ch.cache.at(i));
+            std::sort(agreed.begin(), agreed.end());
+        } else {
+            agreed = a.wire;
+            ch.cache.learn(agreed);
         }
         std::string res;
         for (const auto &k : agreed) res.append(k.substr(k.find("::") + 2)).append("\n");

@@ -60,6 +60,7 @@ void tune(int fd) {
 ControlChannel::~ControlChannel() { close_all(); }
 
 void ControlChannel::close_all() {
+    cache.clear();
     for (int *fd : {&listen_fd_, &send_fd_, &recv_fd_}) {
         if (*fd >= 0) ::close(*fd);
         *fd = -1;
@@ -92,6 +93,7 @@ void ControlChannel::connect(int rank, int size, const std::vector<std::string> 
                 DDL_STATUS_INVALID_ARGUMENT, "control connect: " << eps.size() << " endpoints for size " << size);
     rank_ = rank;
     size_ = size;
+    cache.clear();
     if (size == 1) return;
     DDL_REQUIRE(listen_fd_ >= 0, DDL_STATUS_INVALID_ARGUMENT, "ddl_control_listen must come first");
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
@@ -170,6 +172,72 @@ bool ControlChannel::recv(Token &t, int timeout_ms) {
     t.msg.assign(len, '\0');
     if (len) read_all(recv_fd_, &t.msg[0], len);
     return true;
+}
+
+bool IdCache::lookup(const std::string &id, uint32_t *idx) const {
+    auto it = index_.find(id);
+    if (it == index_.end()) return false;
+    *idx = it->second;
+    return true;
+}
+
+const std::string &IdCache::at(uint32_t i) const {
+    DDL_REQUIRE(i < ids_.size(), DDL_STATUS_COMM_ERROR, "token: cached id " << i << " out of range " << ids_.size());
+    return ids_[i];
+}
+
+bool IdCache::learn(const std::vector<std::string> &agreed) {
+    const bool cleared = ids_.size() + agreed.size() > kMax;  // same decision on every rank
+    if (cleared) clear();
+    for (const auto &id : agreed) {
+        if (index_.count(id)) continue;
+        index_.emplace(id, (uint32_t)ids_.size());
+        ids_.push_back(id);
+    }
+    return cleared;
+}
+
+void IdCache::clear() {
+    index_.clear();
+    ids_.clear();
+}
+
+// msg[0] = 0: bitmap over the table; 1: little-endian u32 indices
+std::string IdCache::encode(const std::vector<uint32_t> &idx) const {
+    const size_t bitmap = (ids_.size() + 7) / 8, list = 4 * idx.size();
+    std::string m;
+    if (bitmap <= list) {
+        m.assign(1 + bitmap, '\0');
+        for (uint32_t i : idx) m[1 + i / 8] = (char)((unsigned char)m[1 + i / 8] | (1u << (i % 8)));
+    } else {
+        m.assign(1 + list, '\0');
+        m[0] = 1;
+        for (size_t k = 0; k < idx.size(); ++k) std::memcpy(&m[1 + 4 * k], &idx[k], 4);
+    }
+    return m;
+}
+
+std::vector<uint32_t> IdCache::decode(const std::string &msg) const {
+    std::vector<uint32_t> out;
+    DDL_REQUIRE(!msg.empty(), DDL_STATUS_COMM_ERROR, "token: empty cached-id message");
+    if (msg[0] == 0) {
+        DDL_REQUIRE(msg.size() - 1 <= (ids_.size() + 7) / 8, DDL_STATUS_COMM_ERROR, "token: bitmap beyond the id table");
+        for (size_t b = 1; b < msg.size(); ++b) {
+            const unsigned char v = (unsigned char)msg[b];
+            if (!v) continue;
+            for (int k = 0; k < 8; ++k)
+                if (v & (1u << k)) out.push_back((uint32_t)((b - 1) * 8 + k));
+        }
+    } else {
+        DDL_REQUIRE(msg[0] == 1 && (msg.size() - 1) % 4 == 0, DDL_STATUS_COMM_ERROR, "token: bad cached-id message");
+        for (size_t p = 1; p < msg.size(); p += 4) {
+            uint32_t i;
+            std::memcpy(&i, &msg[p], 4);
+            out.push_back(i);
+        }
+    }
+    for (uint32_t i : out) DDL_REQUIRE(i < ids_.size(), DDL_STATUS_COMM_ERROR, "token: cached id out of range");
+    return out;
 }
 
 std::string encode_keys(const std::vector<std::string> &keys) {

@@ -9,12 +9,15 @@
 
 #include <cstdint>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace ddl {
 
-// Token types / request types: reference rtc/Token.h:20-33.
-enum TokenType : uint8_t { TOKEN_READY = 0, TOKEN_SYNC = 1, TOKEN_COMMUNICATE = 2, TOKEN_SHUT_DOWN = 3 };
+// Token types / request types: reference rtc/Token.h:20-33, plus the two cached-id forms of
+// SYNC / COMMUNICATE (the key set as indices into IdCache instead of strings).
+enum TokenType : uint8_t { TOKEN_READY = 0, TOKEN_SYNC = 1, TOKEN_COMMUNICATE = 2, TOKEN_SHUT_DOWN = 3,
+                           TOKEN_SYNC_CACHED = 4, TOKEN_COMMUNICATE_CACHED = 5 };
 enum TokenRequest : uint8_t { TOKEN_REQUEST_SHUTDOWN = 0, TOKEN_REQUEST_ALLREDUCE = 1, TOKEN_REQUEST_BROADCAST = 2,
                             TOKEN_REQUEST_ALLGATHER = 3 };
 
@@ -22,6 +25,29 @@ struct Token {
     uint8_t type = TOKEN_READY;
     uint8_t request = TOKEN_REQUEST_ALLREDUCE;
     std::string msg;
+};
+
+// Request ids agreed in earlier rounds, in agreement order. Every rank appends the same agreed
+// lists in the same order, so the tables are identical across ranks and a proposal made only
+// of known ids can travel as indices (a bitmap or a u32 list, whichever is shorter) instead of
+// "Type::key" strings — for a training step's 4096 gradient keys, ~0.5 KB instead of ~100 KB
+// per hop.
+class IdCache {
+public:
+    bool lookup(const std::string &id, uint32_t *idx) const;
+    const std::string &at(uint32_t i) const;
+    size_t size() const { return ids_.size(); }
+    // Appends the unseen ids of an agreed list (in list order). Past kMax entries the table is
+    // cleared first — the same decision on every rank; returns true then.
+    bool learn(const std::vector<std::string> &agreed);
+    std::string encode(const std::vector<uint32_t> &idx) const;
+    std::vector<uint32_t> decode(const std::string &msg) const;
+    void clear();
+    static constexpr size_t kMax = 1u << 20;
+
+private:
+    std::unordered_map<std::string, uint32_t> index_;
+    std::vector<std::string> ids_;
 };
 
 class ControlChannel {
@@ -44,6 +70,10 @@ public:
     int rank() const { return rank_; }
     int size() const { return size_; }
     void close_all();
+
+    IdCache cache;                 // see IdCache; reset by connect / close_all
+    long long string_rounds = 0;   // negotiation rounds by token form (ddl_control_stats)
+    long long cached_rounds = 0;
 
 private:
     int listen_fd_ = -1, send_fd_ = -1, recv_fd_ = -1;

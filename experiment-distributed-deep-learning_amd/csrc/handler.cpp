@@ -160,6 +160,16 @@ void validate(const Request &r, int size) {
 }
 }  // namespace
 
+// A request whose id was agreed before gets its id-table index (under mu_).
+void RequestHandler::mark_cached_(const ReqId &id, Request &r) {
+    r.cidx = -1;
+    if (id.order < 0 || id.order >= 3) return;
+    auto it = cache_by_key_[id.order].find(id.key);
+    if (it == cache_by_key_[id.order].end()) return;
+    r.cidx = it->second;
+    pend_flag_[it->second] = 1;
+}
+
 void RequestHandler::submit(Request r) {
     validate(r, owner_->size());
     {
@@ -168,6 +178,7 @@ void RequestHandler::submit(Request r) {
         ReqId id = req_id(r);
         DDL_REQUIRE(pending_.find(id) == pending_.end(), DDL_STATUS_DUPLICATE_KEY,
                     "a request with key '" << r.key << "' is already pending");
+        mark_cached_(id, r);
         pending_.emplace(std::move(id), std::move(r));
     }
     cv_.notify_all();
@@ -193,6 +204,7 @@ void RequestHandler::submit_batch(std::vector<Request> &rs) {
         auto hint = pending_.end();
         for (size_t i = order.size(); i-- > 0;) {
             const size_t j = order[i];
+            mark_cached_(ids[j], rs[j]);
             hint = pending_.emplace_hint(hint, std::move(ids[j]), std::move(rs[j]));
         }
     }
@@ -209,6 +221,7 @@ void RequestHandler::fail_all_(int status) {
     {
         std::lock_guard<std::mutex> g(mu_);
         left.swap(pending_);
+        std::fill(pend_flag_.begin(), pend_flag_.end(), 0);
     }
     for (auto &kv : left) {
         if (kv.second.done) kv.second.done(status, kv.second.user);
@@ -279,85 +292,166 @@ void RequestHandler::main_() {
     idle_cv_.notify_all();
 }
 
-std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine,
-                                        int request_type) {
+Agreed negotiate_root(ControlChannel &ch, bool cached, const std::vector<uint32_t> &idx,
+                      const std::vector<std::string> &strs, int request_type) {
     Token t;
-    t.type = TOKEN_SYNC;
+    t.type = cached ? TOKEN_SYNC_CACHED : TOKEN_SYNC;
     t.request = (uint8_t)request_type;
-    t.msg = encode_keys(mine);
+    t.msg = cached ? ch.cache.encode(idx) : encode_keys(strs);
     ch.send(t);
     Token back;
     ch.recv(back, -1);
-    DDL_REQUIRE(back.type == TOKEN_SYNC, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)back.type);
+    DDL_REQUIRE(back.type == t.type, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)back.type);
     Token c;
-    c.type = TOKEN_COMMUNICATE;
+    c.type = cached ? TOKEN_COMMUNICATE_CACHED : TOKEN_COMMUNICATE;
     c.request = (uint8_t)request_type;
     c.msg = back.msg;
     ch.send(c);
-    return decode_keys(back.msg);
+    Agreed a;
+    a.cached = cached;
+    if (cached) {
+        a.idx = ch.cache.decode(back.msg);
+        ++ch.cached_rounds;
+    } else {
+        a.wire = decode_keys(back.msg);
+        std::sort(a.wire.begin(), a.wire.end());
+        ++ch.string_rounds;
+    }
+    return a;
 }
 
 void negotiate_root_finish(ControlChannel &ch) {
     Token drain;
     ch.recv(drain, -1);
-    DDL_REQUIRE(drain.type == TOKEN_COMMUNICATE, DDL_STATUS_COMM_ERROR,
+    DDL_REQUIRE(drain.type == TOKEN_COMMUNICATE || drain.type == TOKEN_COMMUNICATE_CACHED, DDL_STATUS_COMM_ERROR,
                 "token protocol: expected COMMUNICATE, got " << (int)drain.type);
 }
 
-std::vector<std::string> negotiate_member(
-    ControlChannel &ch, const Token &sync,
-    const std::function<std::vector<std::string>(const std::vector<std::string> &)> &intersect) {
-    DDL_REQUIRE(sync.type == TOKEN_SYNC, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)sync.type);
+Agreed negotiate_member(ControlChannel &ch, const Token &sync,
+                        const std::function<std::vector<std::string>(const std::vector<std::string> &)> &by_string,
+                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index) {
+    DDL_REQUIRE(sync.type == TOKEN_SYNC || sync.type == TOKEN_SYNC_CACHED, DDL_STATUS_COMM_ERROR,
+                "token protocol: expected SYNC, got " << (int)sync.type);
+    const bool cached = sync.type == TOKEN_SYNC_CACHED;
     Token s;
-    s.type = TOKEN_SYNC;
-    s.msg = encode_keys(intersect(decode_keys(sync.msg)));
+    s.type = sync.type;
+    s.request = sync.request;
+    s.msg = cached ? ch.cache.encode(by_index(ch.cache.decode(sync.msg))) : encode_keys(by_string(decode_keys(sync.msg)));
     ch.send(s);
     Token c;
     ch.recv(c, -1);
-    DDL_REQUIRE(c.type == TOKEN_COMMUNICATE, DDL_STATUS_COMM_ERROR,
+    DDL_REQUIRE(c.type == (cached ? TOKEN_COMMUNICATE_CACHED : TOKEN_COMMUNICATE), DDL_STATUS_COMM_ERROR,
                 "token protocol: expected COMMUNICATE, got " << (int)c.type);
     ch.send(c);  // forward first, then communicate (RingTokenCommunicateHandler.cc:302-310)
-    return decode_keys(c.msg);
+    Agreed a;
+    a.cached = cached;
+    if (cached) {
+        a.idx = ch.cache.decode(c.msg);
+        ++ch.cached_rounds;
+    } else {
+        a.wire = decode_keys(c.msg);
+        std::sort(a.wire.begin(), a.wire.end());
+        ++ch.string_rounds;
+    }
+    return a;
 }
 
-// Rank 0: propose every registered key (lap 1, SYNC — each rank intersects), then announce
-// the agreed set (lap 2, COMMUNICATE) and run it.
+void RequestHandler::forget_ids_() {
+    cache_req_.clear();
+    for (auto &m : cache_by_key_) m.clear();
+    pend_flag_.clear();
+    for (auto &kv : pending_) kv.second.cidx = -1;
+}
+
+// The agreed ids in execution order. A string round teaches the id table the new ids (every
+// rank learns the same list in the same order); the pending requests among them get their
+// index, so the next round with the same key set goes by index.
+std::vector<ReqId> RequestHandler::agreed_ids_(const Agreed &a) {
+    std::vector<ReqId> ids;
+    std::lock_guard<std::mutex> g(mu_);
+    if (a.cached) {
+        ids.reserve(a.idx.size());
+        for (uint32_t i : a.idx) {
+            DDL_REQUIRE(i < cache_req_.size(), DDL_STATUS_COMM_ERROR, "token: id index out of range");
+            ids.push_back(cache_req_[i]);
+        }
+        std::sort(ids.begin(), ids.end());
+        return ids;
+    }
+    ControlChannel &ch = world_control();
+    const size_t first = ch.cache.size();
+    const bool cleared = ch.cache.learn(a.wire);
+    if (cleared) forget_ids_();
+    for (size_t j = cleared ? 0 : first; j < ch.cache.size(); ++j) {
+        ReqId rid = parse_wire_id(ch.cache.at((uint32_t)j));
+        cache_by_key_[rid.order][rid.key] = (uint32_t)j;
+        pend_flag_.push_back(0);
+        auto it = pending_.find(rid);
+        if (it != pending_.end()) {
+            it->second.cidx = (int64_t)j;
+            pend_flag_[j] = 1;
+        }
+        cache_req_.push_back(std::move(rid));
+    }
+    ids.reserve(a.wire.size());
+    for (const auto &w : a.wire) ids.push_back(parse_wire_id(w));
+    return ids;
+}
+
+// Rank 0: propose every registered id of one type (lap 1, SYNC — each rank intersects), then
+// announce the agreed set (lap 2, COMMUNICATE) and run it.
 void RequestHandler::root_round_() {
     ControlChannel &ch = world_control();
     // one request type per round (the token carries one RequestType): the type of the first
     // registered id, as the reference proposes registeredRequest_.begin() (:184-190)
-    std::vector<std::string> mine;
+    std::vector<std::string> strs;
+    std::vector<uint32_t> idx;
+    bool cached = true;
     int type = kReqAllreduce;
     {
         std::lock_guard<std::mutex> g(mu_);
         if (!pending_.empty()) type = pending_.begin()->second.type;
-        for (auto &kv : pending_)
-            if (kv.second.type == type) mine.push_back(wire_id(kv.first));
+        for (auto &kv : pending_) {
+            if (kv.second.type != type) continue;
+            if (kv.second.cidx < 0) cached = false;
+            if (cached) idx.push_back((uint32_t)kv.second.cidx);
+        }
+        if (!cached)
+            for (auto &kv : pending_)
+                if (kv.second.type == type) strs.push_back(wire_id(kv.first));
+        cached = cached && !idx.empty();
     }
-    std::vector<std::string> agreed = negotiate_root(ch, mine, type);
-    std::vector<ReqId> ids;
-    for (const auto &w : agreed) ids.push_back(parse_wire_id(w));
-    execute_(ids);
+    const Agreed a = negotiate_root(ch, cached, idx, strs, type);
+    execute_(agreed_ids_(a));
     negotiate_root_finish(ch);
 }
 
-// Other ranks: join the SYNC lap once the first proposed key is registered here (the
-// reference parks the READY token the same way, RingTokenCommunicateHandler.cc:225-250),
-// forward the intersection, then forward COMMUNICATE and run the agreed set (:302-310).
+// Other ranks: join the SYNC lap once the first proposed id is registered here (the reference
+// parks the READY token the same way, RingTokenCommunicateHandler.cc:225-250), forward the
+// intersection, then forward COMMUNICATE and run the agreed set (:302-310).
 void RequestHandler::member_round_(Token &t) {
-    std::vector<std::string> agreed = negotiate_member(world_control(), t, [this](const std::vector<std::string> &keys) {
-        std::vector<ReqId> proposed;
-        for (const auto &w : keys) proposed.push_back(parse_wire_id(w));
-        std::vector<std::string> mine;
-        std::unique_lock<std::mutex> lk(mu_);
-        if (!proposed.empty()) cv_.wait(lk, [&] { return stop_ || pending_.count(proposed.front()) > 0; });
-        for (size_t i = 0; i < proposed.size(); ++i)
-            if (pending_.count(proposed[i])) mine.push_back(keys[i]);
-        return mine;
-    });
-    std::vector<ReqId> ids;
-    for (const auto &w : agreed) ids.push_back(parse_wire_id(w));
-    execute_(ids);
+    const Agreed a = negotiate_member(
+        world_control(), t,
+        [this](const std::vector<std::string> &keys) {
+            std::vector<ReqId> proposed;
+            for (const auto &w : keys) proposed.push_back(parse_wire_id(w));
+            std::vector<std::string> mine;
+            std::unique_lock<std::mutex> lk(mu_);
+            if (!proposed.empty()) cv_.wait(lk, [&] { return stop_ || pending_.count(proposed.front()) > 0; });
+            for (size_t i = 0; i < proposed.size(); ++i)
+                if (pending_.count(proposed[i])) mine.push_back(keys[i]);
+            return mine;
+        },
+        [this](const std::vector<uint32_t> &proposed) {
+            std::vector<uint32_t> mine;
+            std::unique_lock<std::mutex> lk(mu_);
+            auto held = [&](uint32_t i) { return i < pend_flag_.size() && pend_flag_[i]; };
+            if (!proposed.empty()) cv_.wait(lk, [&] { return stop_ || held(proposed.front()); });
+            for (uint32_t i : proposed)
+                if (held(i)) mine.push_back(i);
+            return mine;
+        });
+    execute_(agreed_ids_(a));
 }
 
 void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
@@ -617,6 +711,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
         for (const auto &k : ids) {
             auto it = pending_.find(k);
             DDL_REQUIRE(it != pending_.end(), DDL_STATUS_COMM_ERROR, "agreed request '" << k.key << "' is not registered");
+            if (it->second.cidx >= 0) pend_flag_[it->second.cidx] = 0;
             reqs.push_back(std::move(it->second));
             pending_.erase(it);
         }

@@ -24,6 +24,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "control.h"
@@ -58,6 +59,7 @@ struct Request {
     size_t first_dim = 0;             // allgather: rows of `in` (n = first_dim * row_elems)
     size_t row_elems = 1;             //   elements per row (the shape without its first dim)
     ddl_alloc_fn alloc = nullptr;     //   output allocation once the gathered first dim is known
+    int64_t cidx = -1;                // index in the control channel's id table, once agreed before
     std::shared_ptr<ReadyEvent> ready;
     ddl_done_fn done = nullptr;
     void *user = nullptr;
@@ -92,16 +94,23 @@ std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vec
 ControlChannel &world_control();
 
 // One negotiation round of the 2-lap token protocol.
-//   root:   SYNC(mine) -> ... -> SYNC(intersection) back; COMMUNICATE(agreed) sent.
+//   root:   SYNC(proposal) -> ... -> SYNC(intersection) back; COMMUNICATE(agreed) sent.
 //           After running the agreed set, negotiate_root_finish() drains COMMUNICATE.
-//   member: receives SYNC, `intersect` (may block until the first key is registered)
-//           forwards the intersection, then receives and forwards COMMUNICATE.
-std::vector<std::string> negotiate_root(ControlChannel &ch, const std::vector<std::string> &mine,
-                                        int request_type = kReqAllreduce);
+//   member: receives SYNC, intersects with what it holds (may block until the first proposed
+//           id is registered), forwards, then receives and forwards COMMUNICATE.
+// A proposal made only of ids agreed in earlier rounds travels as indices into the channel's
+// IdCache (TOKEN_*_CACHED) and is intersected by index; otherwise as "Type::key" strings.
+struct Agreed {
+    bool cached = false;
+    std::vector<uint32_t> idx;      // cached round: indices into ch.cache
+    std::vector<std::string> wire;  // string round: ids, sorted (their (type, key) order)
+};
+Agreed negotiate_root(ControlChannel &ch, bool cached, const std::vector<uint32_t> &idx,
+                      const std::vector<std::string> &strs, int request_type = kReqAllreduce);
 void negotiate_root_finish(ControlChannel &ch);
-std::vector<std::string> negotiate_member(
-    ControlChannel &ch, const Token &sync,
-    const std::function<std::vector<std::string>(const std::vector<std::string> &)> &intersect);
+Agreed negotiate_member(ControlChannel &ch, const Token &sync,
+                        const std::function<std::vector<std::string>(const std::vector<std::string> &)> &by_string,
+                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index);
 
 class RequestHandler {
 public:
@@ -118,6 +127,9 @@ private:
     void root_round_();
     void member_round_(Token &first);
     void execute_(const std::vector<ReqId> &ids);
+    std::vector<ReqId> agreed_ids_(const Agreed &a);  // learns new ids (string rounds)
+    void forget_ids_();                                 // the id table was cleared
+    void mark_cached_(const ReqId &id, Request &r);
     struct Done {
         size_t plan;  // index into plan_events_ (kNoPlan: nothing to wait for)
         size_t req;
@@ -148,6 +160,11 @@ private:
     std::condition_variable cv_;       // new registrations / stop
     std::condition_variable idle_cv_;  // completions
     std::map<ReqId, Request> pending_;  // (type name, key) order
+    // id table mirror (indices of world_control().cache): parsed ids, key -> index per type,
+    // and which indices are pending here — a cached round is intersected by index
+    std::vector<ReqId> cache_req_;
+    std::unordered_map<std::string, uint32_t> cache_by_key_[3];
+    std::vector<uint8_t> pend_flag_;
     size_t inflight_ = 0;
     bool stop_ = false;
     std::thread thread_;

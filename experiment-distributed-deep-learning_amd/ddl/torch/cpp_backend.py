@@ -67,6 +67,7 @@ class CPPBackend:
         sig('ddl_control_connect', ci, ctypes.c_char_p)
         sig('ddl_control_connect_ranked', ci, ci, ci, ctypes.c_char_p)
         sig('ddl_control_negotiate', ci, ctypes.c_char_p, ctypes.c_char_p, sz)
+        sig('ddl_control_stats', ci, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong))
         sig('ddl_allreduce_variant', ci, cid, vp, vp, sz, ci, ci, vp, ci)
         sig('ddl_allreduce_host', ci, cid, vp, vp, sz, ci, ci)
         sig('ddl_ring_program', ci, ci, ci, sz, ci, ctypes.POINTER(ctypes.c_longlong), sz, ctypes.POINTER(sz))

@@ -102,6 +102,9 @@ int ddl_control_connect_ranked(int rank, int size, const char *endpoints);
  * writes the agreed keys ('\n'-separated, lexicographic) to out. Same protocol as the
  * keyed-request handler, without the data plane. */
 int ddl_control_negotiate(const char *keys, char *out, size_t len);
+/* Negotiation rounds so far by token form: ids as strings, or as indices into the table of ids
+ * agreed in earlier rounds (a repeated key set, e.g. every training step's gradients). */
+int ddl_control_stats(long long *string_rounds, long long *cached_rounds);
 int ddl_finalize(void);
 int ddl_is_initialized(void);
 

@@ -116,6 +116,9 @@ def _control_worker(rank, world, keysets, eps_q, go_q, out_q):
             st = lib.ddl_control_negotiate('\n'.join(keys).encode(), out, len(out))
             assert st == 0, lib.ddl_last_error()
             rounds.append([k for k in out.value.decode().split('\n') if k])
+        sr, cr = ctypes.c_longlong(), ctypes.c_longlong()
+        assert lib.ddl_control_stats(ctypes.byref(sr), ctypes.byref(cr)) == 0
+        rounds.append((sr.value, cr.value))
         out_q.put((rank, rounds, ''))
     except Exception as e:
         out_q.put((rank, None, repr(e)))
@@ -149,7 +152,11 @@ def test_token_ring_negotiation(world):
     res = dict((r, (rounds, err)) for r, rounds, err in (out_q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=30)
-    for rd in range(3):
+    _check_rounds(keysets, res, world, 3)
+
+
+def _check_rounds(keysets, res, world, nrounds):
+    for rd in range(nrounds):
         inter = set(keysets[0][rd])
         for r in range(1, world):
             inter &= set(keysets[r][rd])
@@ -158,6 +165,43 @@ def test_token_ring_negotiation(world):
             rounds, err = res[r]
             assert rounds is not None, f'rank {r}: {err}'
             assert rounds[rd] == want, f'rank {r} round {rd}'
+
+
+def _run_control(world, keysets):
+    ctx = mp.get_context('spawn')
+    eps_q, out_q = ctx.Queue(), ctx.Queue()
+    go = [ctx.Queue() for _ in range(world)]
+    procs = [ctx.Process(target=_control_worker, args=(r, world, keysets, eps_q, go[r], out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    eps = dict(eps_q.get(timeout=60) for _ in range(world))
+    joined = ';'.join(eps[r] for r in range(world))
+    for q in go:
+        q.put(joined)
+    res = dict((r, (rounds, err)) for r, rounds, err in (out_q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=30)
+    return res
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_token_ring_cached_ids(world):
+    """Rounds whose proposal holds only ids agreed before travel as indices into the shared id
+    table (TOKEN_SYNC_CACHED); the agreed sets must be exactly the string protocol's."""
+    base = [f'grad_{i:05d}' for i in range(4096)]
+    rng = np.random.default_rng(7)
+    keysets = []
+    for r in range(world):
+        sub = [k for k in base if rng.random() < 0.9] if r == world - 1 else base
+        extra = base + ['new_a', 'new_b']
+        keysets.append([base, list(base), sub, extra, list(base)])
+    res = _run_control(world, keysets)
+    _check_rounds(keysets, res, world, 5)
+    for r in range(world):
+        string_rounds, cached_rounds = res[r][0][-1]
+        # rounds 0 (first sight) and 3 (new keys) go as strings; 1, 2 and 4 as cached ids
+        assert (string_rounds, cached_rounds) == (2, 3), (r, string_rounds, cached_rounds)
 
 
 def _moves_worker(rank, world, port, kind, q):
