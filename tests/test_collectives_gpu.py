@@ -98,3 +98,40 @@ def test_world_broadcast_allgather_size1(lib, gpu):
     torch.cuda.synchronize()
     assert torch.equal(y, x) and torch.equal(out, x)
     assert lib.ddl_broadcast(comm.id, y.data_ptr(), 1000, DT_FLOAT, 1, s) == 3  # root outside the world
+
+
+@pytest.mark.parametrize('P', [4, 5, 8])
+def test_reference_broadcast_known_answer(lib, gpu, P):
+    """broadcast_test.py:5-17: fp32[16] = rank + 1 on every rank, broadcast from root 3 ->
+    every rank holds 4."""
+    ts = [torch.full((16,), float(r + 1), device=gpu) for r in range(P)]
+    arr = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ts])
+    assert lib.ddl_local_broadcast(P, 3, arr, 16, DT_FLOAT, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    for t in ts:
+        assert torch.all(t == 4.0)
+
+
+@pytest.mark.parametrize('P', [2, 3, 4])
+def test_reference_allgather_known_answer(lib, oracle, gpu, P):
+    """allgather_test.py:5-26: IndexedSlices values = arange(4 + rank) + rank (first dims differ
+    per rank), indices = [[0,0],[1,1],[2,2],[3,3]] + rank; both allgathered -> the rank-ordered
+    concatenations (the keyed layout of MPIRingTokenCommunication.cc:338-356)."""
+    values = [np.arange(4 + r, dtype=np.float32) + r for r in range(P)]
+    indices = [(np.array([[0, 0], [1, 1], [2, 2], [3, 3]]) + r).astype(np.float32) for r in range(P)]
+    for parts in (values, [x.reshape(-1) for x in indices]):
+        counts = [x.size for x in parts]
+        displs = list(np.cumsum([0] + counts[:-1]))
+        sends = [torch.from_numpy(x).to(gpu) for x in parts]
+        recvs = [torch.zeros(sum(counts), device=gpu) for _ in range(P)]
+        S = (ctypes.c_void_p * P)(*[s.data_ptr() for s in sends])
+        R = (ctypes.c_void_p * P)(*[r.data_ptr() for r in recvs])
+        assert lib.ddl_local_allgatherv(P, S, R, (SZ * P)(*counts), (SZ * P)(*[int(d) for d in displs]), DT_FLOAT,
+                                        torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        want = np.concatenate(parts)
+        for r in recvs:
+            assert np.array_equal(r.cpu().numpy(), want)
+    got = oracle.allgather_requests(DT_FLOAT, [[v, i] for v, i in zip(values, indices)])
+    assert np.array_equal(got[0], np.concatenate(values))
+    assert np.array_equal(got[1], np.concatenate(indices))

@@ -224,3 +224,23 @@ def test_local_autotune_candidates(lib, gpu, P, ncand):
     assert times[chosen.value] == min(times)
     algos = {cfgs[4 * i] for i in range(count.value)}
     assert algos == ({0, 1} if P > 2 else {0})
+
+
+@pytest.mark.parametrize('algo', [0, 1])
+def test_bucket_beyond_2pow31_elements(lib, gpu, algo):
+    """Maximum-size bucket: 2^31 + 4099 fp16 elements per rank (4 GiB; the reference's
+    MPI_Allreduce takes `(int) elements` and cannot express it, MPICommunicator.cc:19). Two
+    virtual ranks, exactly summable inputs, so every element must equal the torch sum; checks
+    64-bit indexing in the partition, the tick programs and the kernels."""
+    P, n = 2, (1 << 31) + 4099
+    base = (torch.arange(n, device=gpu, dtype=torch.int32) % 7).half()
+    ins = [base + float(r) for r in range(P)]
+    want = base * P + float(sum(range(P)))
+    send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+    with config(lib, algo=algo):
+        assert lib.ddl_local_ring_allreduce(P, send, send, n, DT_HALF, 0, torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+    for t in ins:
+        assert torch.equal(t, want)
+    del ins, base, want
+    torch.cuda.empty_cache()
