@@ -379,10 +379,8 @@ std::vector<ReqId> RequestHandler::agreed_ids_(const Agreed &a) {
         return ids;
     }
     ControlChannel &ch = world_control();
-    const size_t first = ch.cache.size();
-    const bool cleared = ch.cache.learn(a.wire);
-    if (cleared) forget_ids_();
-    for (size_t j = cleared ? 0 : first; j < ch.cache.size(); ++j) {
+    if (ch.cache.learn(a.wire)) forget_ids_();
+    for (size_t j = cache_req_.size(); j < ch.cache.size(); ++j) {  // mirror every new table entry
         ReqId rid = parse_wire_id(ch.cache.at((uint32_t)j));
         cache_by_key_[rid.order][rid.key] = (uint32_t)j;
         pend_flag_.push_back(0);
