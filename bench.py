@@ -343,8 +343,10 @@ def fusion_c5(lib, comm, dev, steps, k=4096):
     e1.record()
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / (2 * steps)
+    g, sc = pmc_traffic('pack_c5_gather'), pmc_traffic('pack_c5_scatter')
     res['pack_unpack'] = {'us_per_launch': round(t * 1e6, 1), 'hbm_GBs': round(2 * total / t / 1e9, 1),
-                          'algorithmic_bytes_per_launch': 2 * int(total)}
+                          'algorithmic_bytes_per_launch': 2 * int(total),
+                          'traffic': (g + sc) // 2 if g and sc else None}
     return res
 
 

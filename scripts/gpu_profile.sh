@@ -18,4 +18,5 @@ if [ -x tools/bin/reduce_tune ]; then
   timeout -k 10 300 tools/bin/reduce_tune 1024 3 > $OUT/tune_1024.txt 2>&1; echo "tune1024 rc=$?"
   cat $OUT/tune_256.txt | head -50
 fi
-find $OUT -name "*.csv" | head -20
+python3 scripts/prof_summarize.py $OUT
+find $OUT -type f | head -30
