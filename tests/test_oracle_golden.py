@@ -98,3 +98,38 @@ def test_half_and_bf16_rounding(oracle):
     rne = ((u.astype(np.uint64) + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
     got_bf = np.array([oracle.lib.ddlo_float_to_bf16(float(v)) for v in f[:5000]], dtype=np.uint16)
     assert np.array_equal(got_bf, rne[:5000])
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_direct_order_vs_mpich(oracle, case):
+    """The direct-schedule restatement (ddlo_allreduce_direct) against MPICH: bit-exact where
+    the sum is order-free, within the summation bound otherwise (for fp16/bf16, which MPICH
+    cannot reduce, the fold rounds once, so its error is the fp32 accumulation's)."""
+    meta = MANIFEST['cases'][case]
+    xs, y = GOLD[case + '__inputs'], GOLD[case + '__output']
+    dt = FROM_NP[meta['dtype']]
+    out = oracle.allreduce_direct(dt, list(xs))
+    exact = (np.issubdtype(xs.dtype, np.integer) or meta['P'] == 2 or meta['kind'] in
+             ('exact', 'fill_rank', 'survey_probe'))
+    if exact:
+        assert out.tobytes() == y.tobytes(), case
+    else:
+        err = np.abs(out.astype(np.float64) - y.astype(np.float64))
+        assert np.all(err <= _bound(xs, xs.dtype)), case
+
+
+def test_reference_broadcast_and_allgather_known_answers(oracle):
+    """broadcast_test.py:5-17 (fp32[16] = rank + 1, root 3 -> 4 everywhere) and
+    allgather_test.py:5-26 (IndexedSlices rows arange(4 + rank) + rank and
+    [[0,0],..,[3,3]] + rank, gathered in rank order) through the oracle's restatements."""
+    for P in (4, 8):
+        xs = [np.full(16, r + 1, np.float32) for r in range(P)]
+        for out in oracle.broadcast(1, xs, 3):
+            assert np.all(out == 4)
+    P = 3
+    values = [np.arange(4 + r, dtype=np.float32) + r for r in range(P)]
+    indices = [(np.array([[0, 0], [1, 1], [2, 2], [3, 3]]) + r).astype(np.float32) for r in range(P)]
+    v, i = oracle.allgather_requests(1, [[a, b] for a, b in zip(values, indices)])
+    assert v.tolist() == [0, 1, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 5, 6, 7]
+    assert i.tolist() == [[r + k, r + k] for r in range(P) for k in range(4)]
+    assert np.array_equal(oracle.allgatherv(1, values), v)
