@@ -116,11 +116,12 @@ __device__ __forceinline__ u32x4 load_v(const u32x4 *p) {
 
 // out = a + b, one 4 KiB tile per workgroup. out may alias a or b (no __restrict__): each lane
 // reads its own 16 bytes of a and b before it writes the same 16 bytes of out.
-template <int DT, int VARIANT>
-__global__ void __launch_bounds__(kThreads) k_sum2_tile(SegTable t) {
+template <int DT, int VARIANT, int THREADS>
+__global__ void __launch_bounds__(THREADS) k_sum2_tile(SegTable t) {
     using A = Add<DT>;
     using S = typename A::S;
     constexpr uint64_t V = 16 / sizeof(S);
+    constexpr uint64_t kTileVec = THREADS;  // 16-byte vectors per tile
     const int seg = blockIdx.y;
     const uint64_t n = t.n[seg];
     const uint64_t nv = n / V;
@@ -132,7 +133,7 @@ __global__ void __launch_bounds__(kThreads) k_sum2_tile(SegTable t) {
 
     if constexpr ((VARIANT & kLdsStageB) != 0) {
         // operand b through LDS by LDS-DMA: each wave owns a 1 KiB slot, lane l lands at 16*l
-        __shared__ __attribute__((aligned(16))) u32x4 stage[kThreads];
+        __shared__ __attribute__((aligned(16))) u32x4 stage[THREADS];
         if (tile * kTileVec > nv) return;  // (uniform) past this segment's tiles
         const int wave = threadIdx.x >> 6;
         if (i < nv)
@@ -189,13 +190,36 @@ struct Acc<DDL_BFLOAT16> {
     __device__ static T add(T a, T b) { return a + b; }
 };
 
+// Lanes per workgroup (one tile of THREADS x 16 B) of the two-input reduce (DDL_REDUCE_THREADS:
+// 64, 128 or 256; measurement). Default 128 (2 KiB tiles): 6.72-6.77 TB/s vs 6.37-6.55 with
+// 256 lanes on the N=1 bench (256 MiB fp32, 3 rotating sets, interleaved rounds).
+int reduce_threads() {
+    static const int v = [] {
+        const char *e = std::getenv("DDL_REDUCE_THREADS");
+        const int t = e ? std::atoi(e) : 128;
+        return t == 64 || t == 256 ? t : 128;
+    }();
+    return v;
+}
+
+// Fold cache policy (DDL_FOLD_VARIANT, measurement): bit 0 non-temporal loads of the received
+// inputs, bit 1 non-temporal store. Default 3 (every operand streams once): 5.77 TB/s vs 5.50
+// plain on a P=8 chunk (32 MiB fp32, 7 inputs, rotating buffers).
+int fold_variant() {
+    static const int v = [] {
+        const char *e = std::getenv("DDL_FOLD_VARIANT");
+        return e ? std::atoi(e) & 3 : 3;
+    }();
+    return v;
+}
+
 // One 4 KiB tile of the output per workgroup: each lane folds its 16 bytes across a and the nb
 // received inputs (loads of all inputs issued before the adds), one store. HBM bytes per
 // element: (nb + 2) * sizeof(T).
 // NB (received inputs) is a template parameter: every load is unconditional and all of them
 // are in flight before the first add (a runtime "load or skip" per input makes hipcc wait
 // vmcnt(0) per input).
-template <int DT, int NB>
+template <int DT, int NB, int FV>
 __global__ void __launch_bounds__(kThreads) k_sumN_tile(SegTableN t) {
     using A = Acc<DT>;
     using S = typename Add<DT>::S;
@@ -207,7 +231,10 @@ __global__ void __launch_bounds__(kThreads) k_sumN_tile(SegTableN t) {
         u32x4 raw[NB + 1];
         raw[0] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.a) + i);
 #pragma unroll
-        for (int k = 0; k < NB; ++k) raw[k + 1] = static_cast<const u32x4 *>(t.b[k])[i];
+        for (int k = 0; k < NB; ++k) {
+            if (FV & 1) raw[k + 1] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.b[k]) + i);
+            else raw[k + 1] = static_cast<const u32x4 *>(t.b[k])[i];
+        }
         const S *s0 = reinterpret_cast<const S *>(&raw[0]);
         T acc[V];
 #pragma unroll
@@ -222,7 +249,8 @@ __global__ void __launch_bounds__(kThreads) k_sumN_tile(SegTableN t) {
         S *rs = reinterpret_cast<S *>(&res);
 #pragma unroll
         for (int e = 0; e < V; ++e) rs[e] = A::narrow(acc[e]);
-        static_cast<u32x4 *>(t.out)[i] = res;
+        if (FV & 2) __builtin_nontemporal_store(res, static_cast<u32x4 *>(t.out) + i);
+        else static_cast<u32x4 *>(t.out)[i] = res;
     }
     const uint64_t rem = t.n - nv * V;
     if (rem && blockIdx.x == nv / kTileVec && threadIdx.x < rem) {
@@ -238,8 +266,16 @@ void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
     if constexpr (NB > kMaxInputs) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
     } else {
-        if (t.nb == NB) hipLaunchKernelGGL((k_sumN_tile<DT, NB>), dim3(tiles), dim3(kThreads), 0, stream, t);
-        else launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
+        if (t.nb == NB) {
+            switch (fold_variant()) {
+                case 1: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 1>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
+                case 2: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 2>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
+                case 3: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 3>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
+                default: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 0>), dim3(tiles), dim3(kThreads), 0, stream, t);
+            }
+        } else {
+            launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
+        }
     }
 }
 
@@ -277,8 +313,15 @@ void launch_variant(const SegTable &t, hipStream_t stream, int variant, dim3 gri
     if constexpr (V > kVariantMask) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant");
     } else {
-        if (variant == V) hipLaunchKernelGGL((k_sum2_tile<DT, V>), grid, dim3(kThreads), 0, stream, t);
-        else launch_variant<DT, V + 1>(t, stream, variant, grid);
+        if (variant == V) {
+            switch (reduce_threads()) {
+                case 64: hipLaunchKernelGGL((k_sum2_tile<DT, V, 64>), grid, dim3(64), 0, stream, t); break;
+                case 256: hipLaunchKernelGGL((k_sum2_tile<DT, V, 256>), grid, dim3(256), 0, stream, t); break;
+                default: hipLaunchKernelGGL((k_sum2_tile<DT, V, 128>), grid, dim3(128), 0, stream, t);
+            }
+        } else {
+            launch_variant<DT, V + 1>(t, stream, variant, grid);
+        }
     }
 }
 
@@ -292,7 +335,8 @@ void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned,
         return;
     }
     constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
-    const uint64_t tiles = (max_n / V + kTileVec) / kTileVec;  // +1 vector of room for the tail
+    const uint64_t tv = (uint64_t)reduce_threads();
+    const uint64_t tiles = (max_n / V + tv) / tv;  // +1 vector of room for the tail
     DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << max_n << " elements");
     launch_variant<DT, 0>(t, stream, variant, dim3((unsigned)tiles, t.count));
 }

@@ -205,6 +205,12 @@ int main(int argc, char **argv) {
     TILE1(2, 256, 0, 0, 1)
     TILE1(4, 256, 0, 0, 1)
     TILE1(2, 256, 1, 0, 0)
+    TILE1(2, 256, 1, 1, 0)
+    TILE1(4, 256, 1, 1, 0)
+    TILE1(1, 512, 1, 1, 0)
+    TILE1(2, 128, 1, 1, 0)
+    TILE1(1, 128, 1, 1, 0)
+    TILE1(4, 64, 1, 1, 0)
     add3("tile1_lds NT256", [=](hipStream_t s) { hipLaunchKernelGGL((k_tile1_lds<256>), dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, O, A, B, nv); });
     add3("tile1 inplace U1 NT256", [=](hipStream_t s) { hipLaunchKernelGGL((k_tile1<1, 256, 0, 0, 0>), dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, A, A, B, nv); });
     add3("tiles U1 NT256 grid=all tiles", [=](hipStream_t s) { hipLaunchKernelGGL((k_tiles<1, 256>), dim3((unsigned)(nv / 256)), dim3(256), 0, s, O, A, B, nv); });
