@@ -38,7 +38,6 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 using h16x8 = _Float16 __attribute__((ext_vector_type(8)));
 
 constexpr int kThreads = 256;
-constexpr uint64_t kTileVec = kThreads;  // 16-byte vectors per tile (4 KiB)
 
 template <int DT>
 struct Add;
@@ -219,8 +218,10 @@ int fold_variant() {
 // NB (received inputs) is a template parameter: every load is unconditional and all of them
 // are in flight before the first add (a runtime "load or skip" per input makes hipcc wait
 // vmcnt(0) per input).
+constexpr int kFoldThreads = 128;
 template <int DT, int NB, int FV>
-__global__ void __launch_bounds__(kThreads) k_sumN_tile(SegTableN t) {
+__global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
+    constexpr uint64_t kTileVec = kFoldThreads;
     using A = Acc<DT>;
     using S = typename Add<DT>::S;
     using T = typename A::T;
@@ -268,10 +269,10 @@ void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
     } else {
         if (t.nb == NB) {
             switch (fold_variant()) {
-                case 1: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 1>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
-                case 2: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 2>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
-                case 3: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 3>), dim3(tiles), dim3(kThreads), 0, stream, t); break;
-                default: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 0>), dim3(tiles), dim3(kThreads), 0, stream, t);
+                case 1: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 1>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
+                case 2: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 2>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
+                case 3: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 3>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
+                default: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 0>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
             }
         } else {
             launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
@@ -372,7 +373,7 @@ void launch_sumN_dt(const SegTableN &t, hipStream_t stream) {
         hipLaunchKernelGGL(k_sumN_scalar<DT>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, t);
         return;
     }
-    const uint64_t tiles = (t.n / V + kTileVec) / kTileVec;
+    const uint64_t tiles = (t.n / V + kFoldThreads) / kFoldThreads;
     DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << t.n << " elements");
     launch_sumN_nb<DT, 1>(t, stream, (unsigned)tiles);
 }
