@@ -258,7 +258,8 @@ def fold_roofline(lib, dev, sh, S, nb=7):
     byts = (nb + 2) * n * 4
     return {'kernel': f'k_sumN_tile<DDL_FLOAT,{nb}>', 'chunk_bytes': n * 4, 'us': round(best * 1e6, 1),
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
-            'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4)}
+            'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
+            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 else None}
 
 
 def half_dtypes(lib, dev, sh, S):
@@ -317,17 +318,35 @@ def fusion_c5(lib, comm, dev, steps, k=4096):
         check(lib.ddl_allreduce_submit_batch(comm.id, *args), 'ddl_allreduce_submit_batch')
         check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
 
-    step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    def timed():
         step()
-    dt = (time.perf_counter() - t0) / steps
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        return (time.perf_counter() - t0) / steps
+
+    dt = timed()
     res = {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3),
            'bucket_GiBs': round(total / GiB / dt, 2),
-           'path': 'keyed batch -> token negotiation -> dtype groups -> plans -> pack -> ring -> unpack (in place)'}
-    if comm.size == 1:
-        res['note'] = 'one-rank world: the engine skips pack/ring/unpack (out = in), so this is host overhead'
+           'path': 'keyed batch -> token negotiation -> dtype groups -> plans -> pack -> ring -> unpack (in place)',
+           'fusion_pipeline_bytes': int(lib.ddl_get_config(b'fusion_pipeline_bytes'))}
+    # the same batch with the fusion pipeline off (one pack, one allreduce, one unpack per plan);
+    # at one rank both forms run the data plane for real (one_rank_shortcut = 0), where the
+    # allreduce itself is the identity and only pack / unpack / host work remain
+    keys_set = (b'fusion_pipeline_bytes', b'one_rank_shortcut')
+    old = {kk: lib.ddl_get_config(kk) for kk in keys_set}
+    try:
+        if comm.size == 1:
+            res['note'] = 'one-rank world: the engine skips pack/ring/unpack (out = in), so `ms` is host overhead'
+            check(lib.ddl_set_config(b'one_rank_shortcut', 0), 'ddl_set_config')
+            res['data_plane_forced_ms'] = round(timed() * 1e3, 3)
+        check(lib.ddl_set_config(b'fusion_pipeline_bytes', 0), 'ddl_set_config')
+        key = 'data_plane_forced_unpipelined_ms' if comm.size == 1 else 'unpipelined_ms'
+        res[key] = round(timed() * 1e3, 3)
+    finally:
+        for kk, v in old.items():
+            lib.ddl_set_config(kk, v)
     # the fusion gather/scatter kernels on the same buckets (one launch each, device segment table)
     fused = torch.empty(sum((t.numel() * t.element_size() + 255) // 256 * 256 for t in tensors), dtype=torch.uint8,
                         device=dev)

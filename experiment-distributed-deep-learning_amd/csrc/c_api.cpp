@@ -235,6 +235,10 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
             c.host_chunk_bytes = value;
         } else if (k == "tune") c.tune = value ? 1 : 0;
+        else if (k == "fusion_pipeline_bytes") {
+            DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
+            c.fusion_pipeline_bytes = value;
+        } else if (k == "one_rank_shortcut") c.one_rank_shortcut = value ? 1 : 0;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
     });
@@ -253,6 +257,8 @@ long long ddl_get_config(const char *key) {
     if (k == "cycle_time_us") return c.cycle_time_us;
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
     if (k == "tune") return c.tune;
+    if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
+    if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     return -1;
 }
 

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <string>
 #include <sstream>
+#include <vector>
 
 #include "ddl_amd.h"
 
@@ -145,9 +146,10 @@ private:
         size_t cap = 0;
         hipEvent_t ready = nullptr;
     };
-    static constexpr int kSlots = 4;
-    Slot slots_[kSlots];
-    int next_ = 0;
+    Slot &free_slot_();  // a slot whose last table copy has been consumed (grows the pool)
+    static constexpr size_t kMaxSlots = 64;
+    std::vector<Slot> slots_;
+    size_t next_ = 0;
 };
 
 }  // namespace ddl

@@ -37,6 +37,13 @@ struct Config {
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};
+    // keyed fusion: a multi-request plan larger than this runs as a pipeline of sub-plans of at
+    // most this many bytes — pack of sub-plan j+1 and unpack of j-1 overlap the allreduce of j
+    // (0 = one pack, one allreduce, one unpack per plan)
+    std::atomic<long long> fusion_pipeline_bytes{256ll << 20};
+    // a one-rank world skips the keyed data plane (the sum is the input); 0 runs pack ->
+    // allreduce -> unpack anyway (tests of the fusion path on one GPU)
+    std::atomic<long long> one_rank_shortcut{1};
     // bumped by every ddl_set_config: tuned choices are dropped when the tunables change
     std::atomic<long long> epoch{0};
     RingConfig ring() const {

@@ -130,7 +130,10 @@ RequestHandler::~RequestHandler() {
     if (thread_.joinable()) thread_.join();
     fail_all_(DDL_STATUS_COMM_ERROR);
     for (hipEvent_t e : plan_events_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : pipe_events_) (void)hipEventDestroy(e);
     if (fusion_) (void)hipFree(fusion_);
+    if (fusion2_) (void)hipFree(fusion2_);
+    if (side_) (void)hipStreamDestroy(side_);
     if (gather_) (void)hipFree(gather_);
     if (dims_) (void)hipFree(dims_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -510,7 +513,7 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
-            if (data_->size() == 1) {
+            if (data_->size() == 1 && config().one_rank_shortcut.load()) {
                 // a one-rank world: the sum is the input; move bytes only where out != in
                 for (size_t q = p.req_begin; q <= p.req_end; ++q) {
                     const Request &r = reqs[g.second[q]];
@@ -538,11 +541,7 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     dsts.push_back(static_cast<char *>(r.out) + b * es);
                     bytes.push_back((e - b) * es);
                 }
-                const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
-                ensure_(fusion_, fusion_bytes_, total);
-                copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(), stream_);
-                data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
-                copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
+                fused_allreduce_(srcs, dsts, bytes, dt);
             }
             const size_t plan = record_plan_(nplans);
             for (size_t q = p.req_begin; q <= p.req_end; ++q) {
@@ -552,6 +551,93 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
             }
         }
     }
+}
+
+hipEvent_t RequestHandler::pipe_event_(size_t i) {
+    while (pipe_events_.size() <= i) {
+        hipEvent_t e;
+        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pipe_events_.push_back(e);
+    }
+    return pipe_events_[i];
+}
+
+// The reference copies every request of a plan into one MPI buffer, reduces it and copies it
+// back (executeCommunicatePlan_, MPIRingTokenCommunication.cc:548-733). Here the copies are the
+// pack / unpack kernels, and a plan above fusion_pipeline_bytes is cut into sub-plans J of at
+// most that size (segments split at 256-byte multiples) over two fusion buffers:
+//   side_:   pack 0, pack 1, unpack 0, pack 2, unpack 1, ...   (unpack j waits allreduce j)
+//   stream_:         ar 0,   ar 1,     ar 2, ...               (ar j waits pack j)
+// so the pack of j+1 and the unpack of j-1 run under the allreduce of j. Buffer j%2 is reused
+// by pack j+2, issued on side_ after unpack j. Each sub-plan is an allreduce of its own (its
+// ring chunks follow the sub-plan), so fp sums are in a ring order of the sub-plan.
+void RequestHandler::fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
+                                      const std::vector<size_t> &bytes, int dt) {
+    const size_t es = dtype_size(dt);
+    const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
+    size_t cap = (size_t)config().fusion_pipeline_bytes.load();
+    cap &= ~size_t(255);
+    if (cap == 0 || total <= cap) {
+        ensure_(fusion_, fusion_bytes_, total);
+        copier_.run(0, fusion_, const_cast<void *const *>(reinterpret_cast<const void *const *>(srcs.data())),
+                    bytes.data(), (int)srcs.size(), stream_);
+        data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+        copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
+        return;
+    }
+    struct Sub {
+        std::vector<const void *> src;
+        std::vector<void *> dst;
+        std::vector<size_t> bytes;
+        size_t flat = 0;
+    };
+    std::vector<Sub> subs(1);
+    for (size_t i = 0; i < bytes.size(); ++i) {
+        size_t off = 0;
+        do {
+            Sub *cur = &subs.back();
+            if (cur->flat >= cap) {
+                subs.emplace_back();
+                cur = &subs.back();
+            }
+            // a piece fills the sub-plan up to cap; every cut is a multiple of 256 bytes (and so of
+            // the element size) from the segment start
+            const size_t room = cap - cur->flat, left = bytes[i] - off;
+            const size_t len = left <= room ? left : room;
+            cur->src.push_back(static_cast<const char *>(srcs[i]) + off);
+            cur->dst.push_back(static_cast<char *>(dsts[i]) + off);
+            cur->bytes.push_back(len);
+            cur->flat += (len + 255) & ~size_t(255);
+            off += len;
+        } while (off < bytes[i]);
+    }
+    size_t maxflat = 0;
+    for (const Sub &sb : subs) maxflat = sb.flat > maxflat ? sb.flat : maxflat;
+    void *buf[2] = {ensure_(fusion_, fusion_bytes_, maxflat), ensure_(fusion2_, fusion2_bytes_, maxflat)};
+    if (!side_) DDL_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    const size_t J = subs.size();
+    // events: [0] fork, [1 + 2j] pack j done, [2 + 2j] allreduce j done, [1 + 2J] join
+    hipEvent_t fork = pipe_event_(0);
+    for (size_t k = 1; k <= 2 * J + 1; ++k) pipe_event_(k);
+    DDL_HIP(hipEventRecord(fork, stream_));  // inputs ready (wait_inputs_ ran on stream_)
+    DDL_HIP(hipStreamWaitEvent(side_, fork, 0));
+    auto unpack = [&](size_t j) {
+        DDL_HIP(hipStreamWaitEvent(side_, pipe_events_[2 + 2 * j], 0));
+        copier_.run(1, buf[j % 2], subs[j].dst.data(), subs[j].bytes.data(), (int)subs[j].dst.size(), side_);
+    };
+    for (size_t j = 0; j < J; ++j) {
+        Sub &sb = subs[j];
+        copier_.run(0, buf[j % 2], const_cast<void *const *>(reinterpret_cast<const void *const *>(sb.src.data())),
+                    sb.bytes.data(), (int)sb.src.size(), side_);
+        DDL_HIP(hipEventRecord(pipe_events_[1 + 2 * j], side_));
+        DDL_HIP(hipStreamWaitEvent(stream_, pipe_events_[1 + 2 * j], 0));
+        data_->allreduce(buf[j % 2], buf[j % 2], sb.flat / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+        DDL_HIP(hipEventRecord(pipe_events_[2 + 2 * j], stream_));
+        if (j >= 1) unpack(j - 1);
+    }
+    unpack(J - 1);
+    DDL_HIP(hipEventRecord(pipe_events_[1 + 2 * J], side_));
+    DDL_HIP(hipStreamWaitEvent(stream_, pipe_events_[1 + 2 * J], 0));
 }
 
 // broadcastRequests (MPIRingTokenCommunication.cc:367-419): dtype groups, plans, broadcast of

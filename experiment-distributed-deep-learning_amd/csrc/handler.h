@@ -140,6 +140,11 @@ private:
     void wait_inputs_(const Request &r, std::vector<hipEvent_t> &waited);
     void *ensure_(void *&buf, size_t &cap, size_t need);
     void allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
+    // pack -> allreduce -> unpack of one multi-request plan's segments (src[i] -> dst[i], bytes[i]);
+    // above fusion_pipeline_bytes as a two-buffer pipeline of sub-plans (pack / unpack on side_)
+    void fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
+                          const std::vector<size_t> &bytes, int dtype);
+    hipEvent_t pipe_event_(size_t i);
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);
@@ -149,6 +154,10 @@ private:
     hipStream_t stream_ = nullptr;
     void *fusion_ = nullptr;  // packed requests (allreduce / broadcast / allgather send side)
     size_t fusion_bytes_ = 0;
+    void *fusion2_ = nullptr;  // second buffer of the fusion pipeline
+    size_t fusion2_bytes_ = 0;
+    hipStream_t side_ = nullptr;  // pack / unpack of the fusion pipeline
+    std::vector<hipEvent_t> pipe_events_;
     void *gather_ = nullptr;  // allgather receive side
     size_t gather_bytes_ = 0;
     void *dims_ = nullptr;    // allgather first-dim exchange

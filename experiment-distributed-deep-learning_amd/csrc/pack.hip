@@ -159,6 +159,32 @@ SegmentCopier::~SegmentCopier() {
     }
 }
 
+// Table slots rotate; a slot is rewritten only after the copy that read it has run (its event).
+// A slot still in use is skipped and the pool grows, so a pipeline of pack / unpack launches
+// queued behind allreduces never blocks the host; at kMaxSlots the oldest slot is waited for.
+SegmentCopier::Slot &SegmentCopier::free_slot_() {
+    for (size_t k = 0; k < slots_.size(); ++k) {
+        Slot &sl = slots_[(next_ + k) % slots_.size()];
+        if (!sl.ready) continue;
+        const hipError_t q = hipEventQuery(sl.ready);
+        if (q == hipErrorNotReady) continue;
+        DDL_HIP(q);
+        next_ = (next_ + k + 1) % slots_.size();
+        return sl;
+    }
+    if (slots_.size() < kMaxSlots) {
+        slots_.emplace_back();
+        Slot &sl = slots_.back();
+        DDL_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+        next_ = 0;
+        return sl;
+    }
+    Slot &sl = slots_[next_];
+    next_ = (next_ + 1) % slots_.size();
+    DDL_HIP(hipEventSynchronize(sl.ready));
+    return sl;
+}
+
 size_t SegmentCopier::flat_bytes(const size_t *bytes, int count) {
     size_t off = 0;
     for (int i = 0; i < count; ++i) off += (bytes[i] + 255) & ~size_t(255);
@@ -170,12 +196,7 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     if (count <= 0) return;
     DDL_REQUIRE(flat && segs && bytes, DDL_STATUS_INVALID_ARGUMENT, "null pack arguments");
     const size_t need = (size_t)count * sizeof(SegDesc);
-    // table slots rotate; a slot is rewritten only after the kernel that read it has finished
-    // (its event), so consecutive pack / unpack launches never wait on each other on the host
-    Slot &sl = slots_[next_];
-    next_ = (next_ + 1) % kSlots;
-    if (sl.ready) DDL_HIP(hipEventSynchronize(sl.ready));
-    else DDL_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+    Slot &sl = free_slot_();
     if (need > sl.cap) {
         if (sl.host) DDL_HIP(hipHostFree(sl.host));
         if (sl.dev) DDL_HIP(hipFree(sl.dev));

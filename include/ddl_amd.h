@@ -109,7 +109,10 @@ int ddl_finalize(void);
 int ddl_is_initialized(void);
 
 /* Tunables: "algo" (0 multi-ring, 1 direct all-to-all), "slice_bytes", "rings", "max_slices",
- * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune".
+ * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
+ * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
+ * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
+ * one-rank world skips the keyed data plane; 0: runs it, for tests).
  * With "tune" = 1 (default) a communicator of P > 1 ranks picks the schedule (algo, rings,
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.

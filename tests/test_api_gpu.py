@@ -210,3 +210,56 @@ def test_rccl_comparator_entry_size1(world, lib):
                                      torch.cuda.current_stream().cuda_stream, 1) == 0
     torch.cuda.synchronize()
     assert torch.equal(x, y)
+
+
+@pytest.fixture
+def data_plane_at_one_rank(lib):
+    """Runs the keyed data plane (pack -> allreduce -> unpack) in the one-rank world instead of
+    the shortcut, so the fusion path's composition is exercised on one GPU."""
+    keys = (b'one_rank_shortcut', b'fusion_pipeline_bytes', b'fusion_threshold_bytes')
+    old = {k: lib.ddl_get_config(k) for k in keys}
+    assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
+    yield
+    for k, v in old.items():
+        assert lib.ddl_set_config(k, v) == 0
+
+
+@pytest.mark.parametrize('pipeline', [0, 256, 4096, 1 << 20, 256 << 20])
+@pytest.mark.parametrize('threshold', [(1 << 31) - 1, 3 << 20])
+def test_keyed_fusion_pipeline_data_plane(world, lib, data_plane_at_one_rank, pipeline, threshold):
+    """Multi-request plans through pack -> allreduce -> unpack, pipelined over sub-plans of at
+    most `pipeline` bytes (segments cut at 256-byte multiples; two fusion buffers; pack/unpack
+    on a side stream), plans capped at `threshold`: every output equals its input (P = 1), in
+    place and out of place, for every dtype and ragged sizes."""
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    assert lib.ddl_set_config(b'fusion_pipeline_bytes', pipeline) == 0
+    assert lib.ddl_set_config(b'fusion_threshold_bytes', threshold) == 0
+    rng = np.random.default_rng(pipeline ^ threshold)
+    dts = [torch.float32, torch.float16, torch.int32, torch.bfloat16, torch.float64, torch.int64]
+    tensors, names, outputs = [], [], []
+    for i in rng.permutation(150):
+        n = int(np.exp(rng.uniform(0, np.log(300_000))))
+        dt = dts[i % len(dts)]
+        t = (torch.randn(n, device='cuda') * 1000).to(dt)
+        tensors.append(t)
+        names.append(f'pipe_{i:04d}')
+        outputs.append(t if i % 3 == 0 else torch.full_like(t, 7))
+    want = [t.clone() for t in tensors]
+    hs = allreduce_async_batch(tensors, names, world, outputs=outputs)
+    for w, h in zip(want, hs):
+        got = h.wait(timeout=60)
+        assert torch.equal(got, w)
+
+
+def test_keyed_fusion_pipeline_large_segment(world, lib, data_plane_at_one_rank):
+    """One segment larger than several sub-plans next to small ones: the big tensor is cut
+    across sub-plans and both fusion buffers are reused many times."""
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    assert lib.ddl_set_config(b'fusion_pipeline_bytes', 1 << 20) == 0
+    big = torch.randn(5_000_003, device='cuda')
+    small = [torch.randn(k, device='cuda') for k in (1, 17, 4099)]
+    ts = [small[0], big, small[1], small[2]]
+    want = [t.clone() for t in ts]
+    hs = allreduce_async_batch(ts, ['a', 'b', 'c', 'd'], world)
+    for w, h in zip(want, hs):
+        assert torch.equal(h.wait(timeout=60), w)
