@@ -47,6 +47,7 @@ def parse():
     ap.add_argument('--no-c4', action='store_true', help='N>1: skip the C4 fp16 64 x 16 MiB measurement')
     ap.add_argument('--no-collectives', action='store_true', help='N>1: skip broadcast/allgather timing')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
+    ap.add_argument('--no-size-sweep', action='store_true', help='N>1: skip the bucket-size sweep (ours vs RCCL)')
     ap.add_argument('--watchdog-s', type=float, default=420.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
@@ -474,7 +475,7 @@ def multi_gpu(args):
     check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
           'ddl_tune_result')
     if chosen.value >= 0:
-        cands = [{'algo': ['ring', 'direct'][cfgs[4 * i]], 'rings': cfgs[4 * i + 1],
+        cands = [{'algo': ['ring', 'direct', 'oneshot'][cfgs[4 * i]], 'rings': cfgs[4 * i + 1],
                   'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
                   'ms': round(tms[i], 4)} for i in range(min(count.value, 16))]
         tune = {'chosen': cands[chosen.value], 'candidates': cands}
@@ -546,7 +547,7 @@ def multi_gpu(args):
             lib.ddl_set_config(b'rings', rings)
             lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
             t = timed(0, max(5, args.steps // 4), 2)
-            sweep.append({'algo': ['ring', 'direct'][algo], 'rings': rings, 'slice_MiB': slice_mib,
+            sweep.append({'algo': ['ring', 'direct', 'oneshot'][algo], 'rings': rings, 'slice_MiB': slice_mib,
                           'ms': round(t * 1e3, 4), 'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
             out['schedule_sweep'] = sweep
         for k, v in defaults.items():
@@ -589,6 +590,36 @@ def multi_gpu(args):
     state['leg'] = 'fusion_c5'
     if not args.no_fusion:
         out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
+    # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
+    # size class) next to RCCL's own ncclAllReduce on the same buffers
+    state['leg'] = 'size_sweep'
+    if not args.no_size_sweep:
+        curve = []
+        for sz in (4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+            m = sz // 4
+            a = torch.randn(m, device=dev, generator=g)
+            b = torch.empty_like(a)
+            reps = int(min(200, max(5, (64 << 20) // sz)))
+
+            def one(variant, a=a, b=b, m=m):
+                check(lib.ddl_allreduce_variant(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0,
+                                                stream.cuda_stream, variant), 'ddl_allreduce_variant')
+            t_ours = timed_fn(lambda: one(0), reps, 3)
+            t_rccl = timed_fn(lambda: one(1), reps, 3)
+            chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
+            check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
+                  'ddl_tune_result')
+            pick = None
+            if chosen.value >= 0:
+                i = chosen.value
+                pick = f"{['ring', 'direct', 'oneshot'][cfgs[4 * i]]}/r{cfgs[4 * i + 1]}/s{cfgs[4 * i + 2] >> 10}K"
+            curve.append({'bytes': sz, 'us': round(t_ours * 1e6, 1), 'algbw_GiBs': round(sz / GiB / t_ours, 3),
+                          'busbw_GBs': round(2 * (world - 1) / world * sz / t_ours / 1e9, 2),
+                          'rccl_us': round(t_rccl * 1e6, 1),
+                          'rccl_busbw_GBs': round(2 * (world - 1) / world * sz / t_rccl / 1e9, 2),
+                          'schedule': pick})
+            out['size_sweep_fp32'] = curve
+            del a, b
     state['leg'] = 'finalize'
     if rank == 0:
         emit(out)

@@ -221,8 +221,8 @@ int ddl_set_config(const char *key, long long value) {
         Config &c = config();
         if (k == "slice_bytes") c.slice_bytes = value;
         else if (k == "algo") {
-            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect, DDL_STATUS_INVALID_ARGUMENT,
-                        "algo must be 0 (ring) or 1 (direct)");
+            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect || value == kAlgoOneShot,
+                        DDL_STATUS_INVALID_ARGUMENT, "algo must be 0 (ring), 1 (direct) or 2 (one-shot)");
             c.algo = value;
         } else if (k == "rings") c.rings = value;
         else if (k == "max_slices") c.max_slices = value;
@@ -700,11 +700,30 @@ void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t
             long long row[8] = {(long long)t, 2, -1, sgi, obuf, ooff, (long long)tk.reduce.n[sgi], boff};
             rows.insert(rows.end(), row, row + 8);
         }
-        if (tk.has_reduce && tk.multi) {  // N-input fold: one row per received input, in fold order
+        if (tk.has_reduce && tk.multi) {
             long long obuf, ooff, abuf, aoff;
             decode(tk.reduceN.out, &obuf, &ooff);
             decode(tk.reduceN.a, &abuf, &aoff);
-            DDL_REQUIRE(abuf == 0 && aoff == ooff && obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "unexpected fold operands");
+            DDL_REQUIRE(obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "fold output outside the output buffer");
+            bool staged = abuf == 0 && aoff == ooff;
+            for (int i = 0; i < tk.reduceN.nb; ++i) {
+                long long bbuf, boff;
+                decode(tk.reduceN.b[i], &bbuf, &boff);
+                staged = staged && bbuf == 2;
+            }
+            if (!staged) {
+                // general fold (one-shot): one row per input in fold order, input 0 = a:
+                // {tick, 5, inputs, i, source buffer, source offset, count, output offset}
+                const int ni = tk.reduceN.nb + 1;
+                for (int i = 0; i < ni; ++i) {
+                    long long sbuf, soff;
+                    decode(i == 0 ? tk.reduceN.a : tk.reduceN.b[i - 1], &sbuf, &soff);
+                    long long row[8] = {(long long)t, 5, ni, i, sbuf, soff, (long long)tk.reduceN.n, ooff};
+                    rows.insert(rows.end(), row, row + 8);
+                }
+                continue;
+            }
+            // direct fold (a = in at the output offset): one row per received input, in fold order
             for (int i = 0; i < tk.reduceN.nb; ++i) {
                 long long bbuf, boff;
                 decode(tk.reduceN.b[i], &bbuf, &boff);

@@ -92,8 +92,8 @@ int size_class(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned lon
 namespace {
 
 // Candidate schedules for a P-rank communicator (the configured one first). Every rank builds
-// the same list: it depends on P and the shared config only.
-std::vector<RingConfig> tune_candidates(int P, const RingConfig &base) {
+// the same list: it depends on P, the bucket size and the shared config only.
+std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &base) {
     std::vector<RingConfig> c{base};
     auto add = [&](int algo, int rings, size_t slice, int max_slices) {
         RingConfig r;
@@ -122,6 +122,9 @@ std::vector<RingConfig> tune_candidates(int P, const RingConfig &base) {
         add(kAlgoDirect, 1, 8u << 20, 8);
         add(kAlgoDirect, 1, 64u << 20, 8);
     }
+    // latency-bound buckets: one group (whole bucket to every peer) instead of two or more;
+    // costs (P-1) x the bucket in wire bytes and staging, so only small buckets
+    if (P - 1 <= kMaxInputs && bytes <= kOneShotMaxBytes) add(kAlgoOneShot, 1, 0, 1);
     return c;
 }
 
@@ -131,7 +134,7 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
                       const std::function<void(const RingConfig &)> &run,
                       const std::function<void(float *, int)> &agree_max) {
     TuneResult res;
-    res.candidates = tune_candidates(P, base);
+    res.candidates = tune_candidates(P, bytes, base);
     const int nc = (int)res.candidates.size();
     const int warm = 2, reps = bytes >= (64u << 20) ? 5 : (bytes >= (4u << 20) ? 10 : 20);
     hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -143,6 +143,12 @@ Range slice_range(const Range &chunk, size_t esize, int K, int k) {
 
 void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
                 size_t *staging_stride) {
+    if (cfg.algo == kAlgoOneShot) {  // one tick, whole bucket per peer
+        *R = 1;
+        *K = 1;
+        *staging_stride = (n + 63) & ~size_t(63);
+        return;
+    }
     int r = cfg.algo == kAlgoDirect ? 1 : (int)rings_for(P, cfg.rings).size();
     // Small buckets: fewer rings so every message stays >= 64 KiB (latency-bound regime).
     const size_t bytes = n * esize;
@@ -169,7 +175,7 @@ size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cf
     int R, K;
     size_t stride;
     ring_shape(n, esize, P, cfg, &R, &K, &stride);
-    const size_t slots = cfg.algo == kAlgoDirect ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)R;
+    const size_t slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)R;
     return slots * stride;
 }
 
@@ -231,6 +237,38 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
     }
 }
 
+// One-shot allreduce for latency-bound buckets: tick 0 sends the whole input to every peer and
+// receives every peer's whole input into staging slot (peer - me - 1) mod P, then folds the P
+// inputs in rank order 0, 1, ..., P-1 (in for me, a slot otherwise), so every rank computes the
+// same sum bit for bit (fp16/bf16 accumulated in fp32, rounded once). Tick 1 only waits for the
+// fold, so the comm stream's tail covers it (the executor joins the caller on the comm stream).
+// In place is safe: the fold runs after the group, i.e. after every send has read `in`.
+void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
+                   size_t es) {
+    DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "one-shot schedule supports up to "
+                                                                       << kMaxInputs + 1 << " ranks");
+    auto slot = [&](int q) { return stb + (size_t)((q - rank + P) % P - 1) * prog.staging_stride * es; };
+    Tick t;
+    t.reduce.count = 0;
+    for (int d = 1; d < P; ++d) {
+        const int to = (rank + d) % P, from = (rank + P - d) % P;
+        t.ops.push_back(P2POp{true, to, d, const_cast<char *>(inb), n * es});
+        t.ops.push_back(P2POp{false, from, d, slot(from), n * es});
+    }
+    t.has_reduce = true;
+    t.multi = true;
+    t.reduceN.a = rank == 0 ? static_cast<const void *>(inb) : slot(0);
+    t.reduceN.out = outb;
+    t.reduceN.n = n;
+    t.reduceN.nb = P - 1;
+    for (int q = 1; q < P; ++q) t.reduceN.b[q - 1] = q == rank ? static_cast<const void *>(inb) : slot(q);
+    prog.ticks.push_back(std::move(t));
+    Tick join;
+    join.reduce.count = 0;
+    join.wait_reduce = 0;
+    prog.ticks.push_back(std::move(join));
+}
+
 }  // namespace
 
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
@@ -243,8 +281,13 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     prog.algo = cfg.algo;
     prog.ticks.clear();
     ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
-    prog.staging_slots = cfg.algo == kAlgoDirect ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)prog.R;
+    prog.staging_slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)prog.R;
     if (P <= 1 || n == 0) return;
+    if (cfg.algo == kAlgoOneShot) {
+        build_oneshot(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
+                      static_cast<char *>(staging), n, es);
+        return;
+    }
     if (cfg.algo == kAlgoDirect) {
         build_direct(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
                      static_cast<char *>(staging), n, es);

@@ -63,7 +63,12 @@ struct Tick {
 enum Algo : int {
     kAlgoRing = 0,    // multi-ring reduce-scatter + allgather (edge-disjoint Hamiltonian cycles)
     kAlgoDirect = 1,  // every rank exchanges with every peer at once (fully connected mesh)
+    kAlgoOneShot = 2, // small buckets: every rank sends its whole bucket to every peer in one
+                      // group and folds all P inputs in rank order (one group instead of 2)
 };
+
+// Largest bucket the autotuner tries the one-shot schedule on.
+constexpr size_t kOneShotMaxBytes = 1u << 20;
 
 struct RingConfig {
     int algo = kAlgoRing;
@@ -79,7 +84,7 @@ struct RingProgram {
     int P = 1, R = 1, K = 1, rank = 0, algo = kAlgoRing;
     size_t n = 0, esize = 0;
     size_t staging_stride = 0;  // elements per staging slot
-    size_t staging_slots = 0;   // ring: 2 per ring (step parity); direct: P-1 (one per peer)
+    size_t staging_slots = 0;   // ring: 2 per ring (step parity); direct / one-shot: P-1 (one per peer)
     std::vector<Tick> ticks;
 };
 

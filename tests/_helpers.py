@@ -250,6 +250,8 @@ def simulate_ring(oracle, lib, dt, xs):
                 st_size = max(st_size, int(row[5] + row[6]))
             elif row[1] in (2, 3):
                 st_size = max(st_size, int(row[7] + row[6]))
+            elif row[1] == 5 and row[4] == 2:
+                st_size = max(st_size, int(row[5] + row[6]))
     bufs = [[x.copy(), np.zeros_like(x), np.zeros(st_size, dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
     for t in range(T):
@@ -281,5 +283,12 @@ def simulate_ring(oracle, lib, dt, xs):
                 assert len(folds) == nb and list(folds[:, 3]) == list(range(nb))
                 off, cnt = int(folds[0, 5]), int(folds[0, 6])
                 ins = [bufs[r][0][off:off + cnt]] + [bufs[r][2][s:s + cnt] for s in folds[:, 7]]
+                bufs[r][1][off:off + cnt] = oracle.fold(dt, ins)
+            gen = rows[rows[:, 1] == 5]  # general fold (one-shot): every input named
+            if len(gen):
+                ni = int(gen[0, 2])
+                assert len(gen) == ni and list(gen[:, 3]) == list(range(ni))
+                cnt, off = int(gen[0, 6]), int(gen[0, 7])
+                ins = [bufs[r][int(b)][int(s):int(s) + cnt].copy() for b, s in zip(gen[:, 4], gen[:, 5])]
                 bufs[r][1][off:off + cnt] = oracle.fold(dt, ins)
     return [b[1] for b in bufs]

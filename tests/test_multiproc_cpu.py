@@ -51,8 +51,10 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
         R, _ = h.ring_shape(lib, n, dt, world)
         st = 1
         for row in prog:
-            if row[1] <= 1 and row[4] == 2 or row[1] >= 2:
-                st = max(st, int((row[5] if row[1] <= 1 else row[7]) + row[6]))
+            if row[1] <= 1 and row[4] == 2 or row[1] == 5 and row[4] == 2:
+                st = max(st, int(row[5] + row[6]))
+            elif row[1] in (2, 3):
+                st = max(st, int(row[7] + row[6]))
         bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
         view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
         for t in sorted(set(prog[:, 0].tolist())):
@@ -74,7 +76,12 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
                 off, cnt = int(folds[0, 5]), int(folds[0, 6])
                 ins = [bufs[0][off:off + cnt]] + [bufs[2][o:o + cnt] for o in folds[:, 7]]
                 bufs[1][off:off + cnt] = ora.fold(dt, ins)
-        want = (ora.allreduce_direct(dt, xs) if algo == 1 else
+            gen = rows[rows[:, 1] == 5]  # one-shot fold: every input named (buffer, offset)
+            if len(gen):
+                cnt, off = int(gen[0, 6]), int(gen[0, 7])
+                ins = [bufs[int(b)][int(o):int(o) + cnt].copy() for b, o in zip(gen[:, 4], gen[:, 5])]
+                bufs[1][off:off + cnt] = ora.fold(dt, ins)
+        want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo == 2 else
                 ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
         ok = bufs[1].tobytes() == want.tobytes()
         dist.destroy_process_group()
@@ -83,7 +90,7 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize('algo', [0, 1])
+@pytest.mark.parametrize('algo', [0, 1, 2])
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('dt,n', [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)])
 def test_ring_program_over_gloo(world, dt, n, algo):

@@ -226,6 +226,46 @@ def test_local_autotune_candidates(lib, gpu, P, ncand):
     assert algos == ({0, 1} if P > 2 else {0})
 
 
+# ---- one-shot schedule: algo = 2 --------------------------------------------------------------
+@pytest.mark.parametrize('P', [2, 3, 5, 8])
+@pytest.mark.parametrize('dt', [d for d in ALL_DTYPES if d != 14], ids=lambda d: NAME[d])
+@pytest.mark.parametrize('n', [1, 257, 65_537, 300_001])
+@pytest.mark.parametrize('in_place', [False, True])
+def test_local_oneshot_matches_rank_order_fold(lib, oracle, gpu, P, dt, n, in_place):
+    """One group of whole-bucket exchanges, then the N-input fold in rank order on every rank:
+    every rank equals the oracle's rank-order fold bit for bit, in and out of place."""
+    xs = [random_input(dt, n, 97 + 3 * r) for r in range(P)]
+    with config(lib, algo=2):
+        outs = run_local(lib, gpu, xs, in_place=in_place)
+    want = oracle.fold(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_local_oneshot_repeated_calls(lib, oracle, gpu):
+    """Back-to-back one-shot calls reuse staging: the next call's receives must not land while
+    the previous call's fold still reads (the caller joins on the fold)."""
+    P, n = 8, 1 << 18
+    with config(lib, algo=2):
+        for it in range(6):
+            xs = [random_input(DT_FLOAT, n, 1000 * it + r) for r in range(P)]
+            outs = run_local(lib, gpu, xs)
+            want = oracle.fold(DT_FLOAT, xs)
+            assert all(o.tobytes() == want.tobytes() for o in outs), it
+
+
+def test_local_autotune_small_bucket_tries_oneshot(lib, gpu):
+    chosen, count = ctypes.c_int(), ctypes.c_int()
+    cfgs = (ctypes.c_longlong * 64)()
+    ms = (ctypes.c_float * 16)()
+    st = lib.ddl_local_tune(8, 64 << 10, DT_FLOAT, torch.cuda.current_stream().cuda_stream,
+                            ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
+    assert st == 0, lib.ddl_last_error()
+    assert 2 in {cfgs[4 * i] for i in range(count.value)}
+    times = [ms[i] for i in range(count.value)]
+    assert times[chosen.value] == min(times)
+
+
 @pytest.mark.parametrize('algo', [0, 1])
 def test_bucket_beyond_2pow31_elements(lib, gpu, algo):
     """Maximum-size bucket: 2^31 + 4099 fp16 elements per rank (4 GiB; the reference's

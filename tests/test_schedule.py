@@ -106,7 +106,7 @@ def _overlap(a0, a1, b0, b1):
     return a0 < b1 and b0 < a1
 
 
-@pytest.mark.parametrize('algo', [0, 1])
+@pytest.mark.parametrize('algo', [0, 1, 2])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
 @pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
@@ -121,6 +121,9 @@ def test_schedule_has_no_stream_races(lib, algo, P, n, slice_bytes):
             red = {}
             for row in prog[(prog[:, 1] == 2) | (prog[:, 1] == 3)]:
                 red.setdefault(int(row[0]), []).append(row)
+            for row in prog[prog[:, 1] == 5]:  # general fold: reads (buf, off), writes out
+                t_, _, _, _, sb, so, c_, oo = row
+                red.setdefault(int(t_), []).append(('gen', int(sb), int(so), int(c_), int(oo)))
             w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
             for t in sorted(set(prog[:, 0].tolist())):
                 ops = prog[(prog[:, 0] == t) & (prog[:, 1] <= 1)]
@@ -133,6 +136,16 @@ def test_schedule_has_no_stream_races(lib, algo, P, n, slice_bytes):
                 for op in ops:
                     _, kind, _, _, buf, off, cnt, _ = op
                     for r in running:
+                        if isinstance(r, tuple):  # general fold input: (tag, buffer, offset, count, out offset)
+                            _, sb, so, c_, oo = r
+                            rng_ = (so, so + c_) if sb == 2 else None
+                            if buf == 2 and rng_:
+                                assert not _overlap(off, off + cnt, *rng_), (rank, t, 'staging')
+                            if buf != 2:
+                                assert not _overlap(off, off + cnt, oo, oo + c_), (rank, t, 'in/out')
+                                if sb != 2:
+                                    assert not _overlap(off, off + cnt, so, so + c_), (rank, t, 'in/out')
+                            continue
                         _, _, _, _, _, roff, rcnt, soff = r
                         # a reduce reads in[roff:+rcnt] and staging[soff:+rcnt], writes out[roff:+rcnt]
                         if buf == 2:
@@ -228,3 +241,32 @@ def test_direct_program_sixteen_ranks(lib, oracle):
         outs = simulate_ring(oracle, lib, DT_HALF, xs)
     want = oracle.allreduce_direct(DT_HALF, xs)
     assert all(o.tobytes() == want.tobytes() for o in outs)
+
+
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 8, 16])
+@pytest.mark.parametrize('n', [1, 100, 4099, 50_000])
+@pytest.mark.parametrize('dt', ALL_DTYPES)
+def test_oneshot_programs_compute_the_rank_order_fold(lib, oracle, P, n, dt):
+    """One-shot schedule (algo 2): one group exchanging whole buckets with every peer, then a
+    fold of the P inputs in rank order 0..P-1 on every rank: every rank holds the oracle's
+    rank-order fold bit for bit (identical on all ranks; fp16/bf16 accumulated in fp32)."""
+    xs = [random_input(dt, n, 7 + 13 * r) for r in range(P)]
+    with config(lib, algo=2):
+        outs = simulate_ring(oracle, lib, dt, xs)
+    want = oracle.fold(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_oneshot_program_shape(lib):
+    """One tick of 2(P-1) whole-bucket p2p ops, one (P-1)-input fold, and a trailing tick that
+    waits for the fold (so the caller's join covers it); staging of P-1 buckets."""
+    P, n = 8, 1 << 16
+    with config(lib, algo=2):
+        for rank in range(P):
+            prog = ring_program(lib, rank, P, n, DT_FLOAT)
+            ops = prog[prog[:, 1] <= 1]
+            assert set(ops[:, 0]) == {0} and len(ops) == 2 * (P - 1) and set(ops[:, 6]) == {n}
+            assert sorted(ops[ops[:, 1] == 0][:, 2]) == sorted(set(range(P)) - {rank})
+            folds = prog[(prog[:, 1] == 3) | (prog[:, 1] == 5)]
+            assert set(folds[:, 0]) == {0}
