@@ -89,11 +89,12 @@ def cpu_baseline(n_bytes_sample, seconds):
                       f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM on the reference data plane'}
 
 
-def cpu_reference_path(P=2):
+def cpu_reference_path():
     """The reference's whole CPU+MPI loopback path (3-lap token ring over MPI p2p, fusion memcpy,
     MPI_Allreduce) as a labelled C restatement (oracle/ref_path_port.c; the reference itself is
-    unbuildable here), under MPICH with P ranks on the host cores: C1 (fp32[1024]) and the C3
-    bucket shape (256 MiB fp32). Bounded to a few seconds."""
+    unbuildable here), under MPICH with P ranks on the host cores: C1 (fp32[1024])
+    at P = 2 and 8, the C3 bucket shape (256 MiB fp32) at P = 2 and 8, and a bounded C5-like
+    many-tensor sample (fp32 only: the reference rejects fp16) at P = 8. About 10-20 s."""
     import shutil
     import subprocess
     exe = os.path.join(ROOT, 'oracle', 'build', 'ref_path_port')
@@ -102,13 +103,18 @@ def cpu_reference_path(P=2):
         return {'value': None, 'reason': 'MPICH or oracle/build/ref_path_port missing on this host'}
     env = dict(os.environ)
     env['LD_LIBRARY_PATH'] = '/opt/conda/lib:' + env.get('LD_LIBRARY_PATH', '')
-    res = {'kind': 'port', 'ranks': P, 'cores': P,
-           'what': 'oracle/ref_path_port.c: reference token ring + fusion + MPI_Allreduce (MPICH 3.3.2 loopback)'}
-    for tag, n, reps in (('C1_fp32_1024', 1024, 200), ('C3shape_fp32_256MiB', 64 << 20, 3)):
+    res = {'kind': 'port', 'what': 'oracle/ref_path_port.c: reference token ring + fusion + MPI_Allreduce '
+                                   '(MPICH 3.3.2 loopback), one rank per host core'}
+    legs = (('C1_fp32_1024_P2', 2, 1024, 1, 200), ('C1_fp32_1024_P8', 8, 1024, 1, 100),
+            ('C3shape_fp32_256MiB_P2', 2, 64 << 20, 1, 3), ('C3shape_fp32_256MiB_P8', 8, 64 << 20, 1, 2),
+            ('C5like_fp32_512x256KiB_P8', 8, 64 << 10, 512, 2))
+    for tag, P, n, ntens, reps in legs:
         try:
-            p = subprocess.run([mpiexec, '-n', str(P), exe, str(n), '1', str(reps)], capture_output=True,
+            p = subprocess.run([mpiexec, '-n', str(P), exe, str(n), str(ntens), str(reps)], capture_output=True,
                                text=True, timeout=120, env=env)
-            res[tag] = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {'error': p.stderr[-300:]}
+            r = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {'error': p.stderr[-300:]}
+            r['cores'] = P
+            res[tag] = r
         except Exception as e:  # never let the baseline leg break the bench line
             res[tag] = {'error': repr(e)}
     return res
@@ -183,7 +189,7 @@ def single_gpu(args):
             reps = int(min(3000, max(6, (256 << 20) // size)))
             for _ in range(3):
                 step(m=m, bufs=bufs)
-            t = timed_kernel_ms(reps, m=m, bufs=bufs) / 1e3
+            t = min(timed_kernel_ms(reps, m=m, bufs=bufs) for _ in range(3)) / 1e3  # best of 3 rounds
             sweep.append({'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
                           'hbm_GBs': round(3 * size / t / 1e9, 1)})
             del bufs
@@ -228,7 +234,7 @@ def single_gpu(args):
         out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
-        out['cpu_reference_path'] = cpu_reference_path(P=2)
+        out['cpu_reference_path'] = cpu_reference_path()
     emit(out)
 
 

@@ -120,7 +120,7 @@ enum ReduceVariant : int {
     kLdsStageB = 8, // operand b staged through LDS by global_load_lds_dwordx4
     kVariantMask = 15,
 };
-int default_variant();  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2)
+int default_variant(size_t bytes);  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2), by bucket size
 int ring_variant();     // reduce-scatter step of the ring
 
 // out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.

@@ -397,16 +397,20 @@ void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) {
     DDL_HIP(hipGetLastError());
 }
 
-// Standalone reduce (acc += in over whole buckets): every operand streams through once, so all
-// accesses are non-temporal (measured 6.47 TB/s vs 5.75 plain, 256 MiB fp32, rotating buffers).
-int default_variant() {
+// Standalone reduce (acc += in over whole buckets) of `bytes` per operand. Large buckets stream
+// through once, so all accesses are non-temporal (measured 6.47 TB/s vs 5.75 plain, 256 MiB
+// fp32, rotating buffers; 6.41 vs 5.92 at 64 MiB). Below kNtMinBytes plain accesses win (16 MiB:
+// 5.83 vs 5.62 TB/s; 1-4 MiB: 0.2-0.4 us less per launch; tools/small_sweep.py) — the operands
+// of a small bucket are likely still in the Infinity Cache from whoever produced them.
+constexpr size_t kNtMinBytes = 32u << 20;
+int default_variant(size_t bytes) {
     static int v = [] {
         const char *e = std::getenv("DDL_REDUCE_VARIANT");
-        const int dflt = kNtLoadA | kNtLoadB | kNtStore;
-        int x = e ? std::atoi(e) : dflt;
-        return (x >= 0 && x <= kVariantMask) ? x : dflt;
+        const int x = e ? std::atoi(e) : -1;
+        return (x >= 0 && x <= kVariantMask) ? x : -1;
     }();
-    return v;
+    if (v >= 0) return v;
+    return bytes >= kNtMinBytes ? (kNtLoadA | kNtLoadB | kNtStore) : 0;
 }
 
 // Ring reduce-scatter step: a = the rank's own gradient (read once: non-temporal), b = the slice
@@ -427,17 +431,18 @@ void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) 
                 "segment count " << t.count << " outside [1, " << kMaxSegments << "]");
     const size_t es = dtype_size(dtype);
     DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
-    if (variant < 0) variant = default_variant();
-    DDL_REQUIRE(variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant " << variant);
-    uint64_t max_n = 0;
+    uint64_t max_n = 0, total_n = 0;
     bool aligned = true;
     for (int s = 0; s < t.count; ++s) {
         if (t.n[s] == 0) continue;
         DDL_REQUIRE(t.a[s] && t.b[s] && t.out[s], DDL_STATUS_INVALID_ARGUMENT, "null buffer in segment " << s);
         max_n = t.n[s] > max_n ? t.n[s] : max_n;
+        total_n += t.n[s];
         aligned = aligned && aligned16(t.a[s]) && aligned16(t.b[s]) && aligned16(t.out[s]);
     }
     if (max_n == 0) return;
+    if (variant < 0) variant = default_variant((size_t)total_n * es);
+    DDL_REQUIRE(variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant " << variant);
     switch (dtype) {
         case DDL_FLOAT: launch_dt<DDL_FLOAT>(t, stream, variant, aligned, max_n); break;
         case DDL_DOUBLE: launch_dt<DDL_DOUBLE>(t, stream, variant, aligned, max_n); break;
