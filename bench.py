@@ -44,6 +44,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe) measurement')
     ap.add_argument('--no-fusion', action='store_true', help='skip the C5 many-bucket fusion measurement')
+    ap.add_argument('--no-forced-data-plane', action='store_true',
+                    help='N=1: skip the C5 legs that force the keyed data plane (profiling: keeps one pack '
+                         'shape per kernel)')
     ap.add_argument('--no-c4', action='store_true', help='N>1: skip the C4 fp16 64 x 16 MiB measurement')
     ap.add_argument('--no-collectives', action='store_true', help='N>1: skip broadcast/allgather timing')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
@@ -231,7 +234,7 @@ def single_gpu(args):
         out['host_resident'] = host_resident_rate(lib, Communicator.world(), S, reps=8)
     if not args.no_fusion:
         del sets
-        out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5)
+        out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5, forced=not args.no_forced_data_plane)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
         out['cpu_reference_path'] = cpu_reference_path()
@@ -297,7 +300,7 @@ def half_dtypes(lib, dev, sh, S):
     return res
 
 
-def fusion_c5(lib, comm, dev, steps, k=4096):
+def fusion_c5(lib, comm, dev, steps, k=4096, forced=True):
     """C5: k buckets, byte sizes log-uniform in [4 KiB, 4 MiB] rounded to 256 B,
     dtype fp32/fp16 with p = 0.5, keys grad_%05d submitted in random order, one batch per step
     through the keyed path (negotiation, dtype grouping, plans, pack -> ring -> unpack)."""
@@ -346,11 +349,15 @@ def fusion_c5(lib, comm, dev, steps, k=4096):
     try:
         if comm.size == 1:
             res['note'] = 'one-rank world: the engine skips pack/ring/unpack (out = in), so `ms` is host overhead'
-            check(lib.ddl_set_config(b'one_rank_shortcut', 0), 'ddl_set_config')
-            res['data_plane_forced_ms'] = round(timed() * 1e3, 3)
-        check(lib.ddl_set_config(b'fusion_pipeline_bytes', 0), 'ddl_set_config')
-        key = 'data_plane_forced_unpipelined_ms' if comm.size == 1 else 'unpipelined_ms'
-        res[key] = round(timed() * 1e3, 3)
+        if comm.size == 1 and not forced:
+            pass
+        else:
+            if comm.size == 1:
+                check(lib.ddl_set_config(b'one_rank_shortcut', 0), 'ddl_set_config')
+                res['data_plane_forced_ms'] = round(timed() * 1e3, 3)
+            check(lib.ddl_set_config(b'fusion_pipeline_bytes', 0), 'ddl_set_config')
+            key = 'data_plane_forced_unpipelined_ms' if comm.size == 1 else 'unpipelined_ms'
+            res[key] = round(timed() * 1e3, 3)
     finally:
         for kk, v in old.items():
             lib.ddl_set_config(kk, v)

@@ -144,6 +144,8 @@ private:
     struct Slot {
         void *host = nullptr, *dev = nullptr;
         size_t cap = 0;
+        void *idx = nullptr;  // first segment per span (k_span_index)
+        size_t idx_cap = 0;
         hipEvent_t ready = nullptr;
     };
     Slot &free_slot_();  // a slot whose last table copy has been consumed (grows the pool)

@@ -7,8 +7,9 @@
 // Fused layout: segment i occupies [off_i, off_i + len_i) of the flat buffer, off_i = running
 // sum of the 256-byte-rounded lengths before it (every segment starts 256-byte aligned, so a
 // fused bucket keeps the ring's 16-byte vector alignment). The segment table lives in device
-// memory (uploaded with one async copy from a pinned staging table); each 256-lane workgroup
-// copies a 64 KiB span of the flat space (see k_segments).
+// memory (uploaded with one async copy from a pinned staging table). Default mapping: every
+// segment is cut into 1 KiB tiles that restart at the segment start, one 64-lane workgroup per
+// tile, the tile's segment from a per-tile index built on the device (k_tile_index, k_seg_tiles).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -23,17 +24,14 @@ namespace ddl {
 namespace {
 
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-constexpr int kThreads = 256;
-constexpr uint64_t kTileBytes = kThreads * 16;
 
 struct SegDesc {
     uint64_t ptr;   // segment address (tensor side)
     uint64_t off;   // offset in the flat buffer (256-byte aligned)
     uint64_t len;   // bytes
-    uint64_t vec;   // 1 if ptr is 16-byte aligned (16-byte units), else byte copies
+    uint32_t vec;   // 1 if ptr is 16-byte aligned (16-byte units), else byte copies
+    uint32_t tile0; // segment-aligned tiling: index of the segment's first tile
 };
-
-constexpr int kLdsSegs = 64;  // descriptors staged in LDS per workgroup
 
 // Misaligned or partial chunk: byte copy (rare; kept out of line so the unrolled main loop
 // stays small).
@@ -58,33 +56,94 @@ __device__ int find_segment(const SegDesc *__restrict__ d, int count, uint64_t x
     return lo;
 }
 
-// dir 0: gather segments -> flat; dir 1: scatter flat -> segments. One workgroup per 64 KiB
-// span of the flat buffer: wave 0 finds the span's first segment and stages the next 64
-// descriptors in LDS; every lane then resolves its 16 chunks from LDS, issues all 16 loads,
-// then all 16 stores (no dependent descriptor loads between data accesses). Spans holding more
-// than 64 segments (segments under 1 KiB) resolve the rest from global memory.
-template <int DIR, int kIters, bool NT_STORE>
-__global__ void __launch_bounds__(kThreads) k_segments(char *flat, const SegDesc *__restrict__ d, int count,
-                                                       uint64_t total) {
+// dir 0: gather segments -> flat; dir 1: scatter flat -> segments. One workgroup of THREADS
+// lanes per span of THREADS * 16 * kIters bytes of the flat buffer: wave 0 finds the span's first
+// segment and stages the next kSegs descriptors in LDS; every lane then resolves its kIters
+// chunks from LDS, issues all kIters loads, then all kIters stores (no dependent descriptor
+// loads between data accesses). Spans holding more than kSegs segments resolve the rest from
+// global memory. Small spans (2 chunks per lane, 4 KiB per 128-lane workgroup) keep the chunks
+// in flight a compact, interleaved window of each stream, as the reduce kernel's one-tile-per-
+// workgroup mapping does; tools/copy_tune.hip: 1R+1W copies reach 6.5 TB/s with 2-4 KiB tiles
+// per workgroup vs 5.3 TB/s with 64 KiB.
+// Segment-aligned tiling: every segment is cut into tiles of THREADS * 16 * kIters bytes that
+// restart at the segment start, so a tile never crosses a segment and its workgroup needs no
+// per-chunk search: tile_seg[t] (k_tile_index: one thread per tile, binary search of the
+// tile0 column) names the segment, one scalar descriptor load gives ptr / off / len, and lane l
+// moves bytes [16 l + it * THREADS * 16, ...) of the tile.
+__global__ void __launch_bounds__(256) k_tile_index(const SegDesc *__restrict__ d, int count, uint64_t tiles,
+                                                    int *__restrict__ tile_seg) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= tiles) return;
+    int lo = 0, hi = count;  // last segment with tile0 <= t (segments without tiles share tile0)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (d[mid].tile0 <= t) lo = mid;
+        else hi = mid;
+    }
+    tile_seg[t] = lo;
+}
+
+template <int DIR, int kIters, int THREADS>
+__global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc *__restrict__ d,
+                                                       const int *__restrict__ tile_seg) {
+    constexpr uint64_t kTile = (uint64_t)THREADS * 16 * kIters;
+    const SegDesc sd = d[tile_seg[blockIdx.x]];
+    const uint64_t base = (uint64_t)(blockIdx.x - sd.tile0) * kTile;  // tile start inside the segment
+    char *fl = flat + sd.off;
+    char *tp = reinterpret_cast<char *>(sd.ptr);
+    if (!sd.vec) {  // misaligned tensor: bytes
+        for (uint64_t b = base + threadIdx.x; b < sd.len && b < base + kTile; b += THREADS) {
+            if (DIR == 0) fl[b] = tp[b];
+            else tp[b] = fl[b];
+        }
+        return;
+    }
+    u32x4 v[kIters];
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+        const uint64_t b = base + (uint64_t)it * THREADS * 16 + threadIdx.x * 16;
+        if (b + 16 <= sd.len)
+            v[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>((DIR == 0 ? tp : fl) + b));
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+        const uint64_t b = base + (uint64_t)it * THREADS * 16 + threadIdx.x * 16;
+        if (b + 16 <= sd.len) {
+            __builtin_nontemporal_store(v[it], reinterpret_cast<u32x4 *>((DIR == 0 ? fl : tp) + b));
+        } else if (b < sd.len) {  // the segment's last partial 16 bytes
+            const uint32_t m = (uint32_t)(sd.len - b);
+            if (DIR == 0) copy_bytes(fl + b, tp + b, m);
+            else copy_bytes(tp + b, fl + b, m);
+        }
+    }
+}
+
+template <int DIR, int kIters, bool NT_STORE, int THREADS, int kSegs>
+__global__ void __launch_bounds__(THREADS) k_segments(char *flat, const SegDesc *__restrict__ d, int count,
+                                                      uint64_t total) {
+    constexpr uint64_t kTileBytes = (uint64_t)THREADS * 16;
     constexpr uint64_t kSpanBytes = kTileBytes * kIters;
-    __shared__ uint64_t s_off[kLdsSegs + 1], s_len[kLdsSegs], s_ptr[kLdsSegs];
-    __shared__ int s_vec[kLdsSegs];
+    static_assert(kSegs <= 64 && (kSegs & (kSegs - 1)) == 0, "LDS descriptor table: power of two <= 64");
+    __shared__ uint64_t s_off[kSegs + 1], s_len[kSegs], s_ptr[kSegs];
+    __shared__ int s_vec[kSegs];
     __shared__ int s_seg0;
     const uint64_t span0 = (uint64_t)blockIdx.x * kSpanBytes;
     if (threadIdx.x < 64) {
         const int seg0 = find_segment(d, count, span0);
         const int i = seg0 + (int)threadIdx.x;
-        if (i < count) {
-            s_off[threadIdx.x] = d[i].off;
-            s_len[threadIdx.x] = d[i].len;
-            s_ptr[threadIdx.x] = d[i].ptr;
-            s_vec[threadIdx.x] = (int)d[i].vec;
-        } else {
-            s_off[threadIdx.x] = ~0ull;
-            s_len[threadIdx.x] = 0;
+        if (threadIdx.x < kSegs) {
+            if (i < count) {
+                s_off[threadIdx.x] = d[i].off;
+                s_len[threadIdx.x] = d[i].len;
+                s_ptr[threadIdx.x] = d[i].ptr;
+                s_vec[threadIdx.x] = (int)d[i].vec;
+            } else {
+                s_off[threadIdx.x] = ~0ull;
+                s_len[threadIdx.x] = 0;
+            }
         }
         if (threadIdx.x == 0) {
-            s_off[kLdsSegs] = seg0 + kLdsSegs < count ? d[seg0 + kLdsSegs].off : ~0ull;
+            s_off[kSegs] = seg0 + kSegs < count ? d[seg0 + kSegs].off : ~0ull;
             s_seg0 = seg0;
         }
     }
@@ -101,17 +160,17 @@ __global__ void __launch_bounds__(kThreads) k_segments(char *flat, const SegDesc
         // the table are ~0): s = last staged segment starting at or before o, 64 = beyond
         int s = 0;
 #pragma unroll
-        for (int step = kLdsSegs / 2; step > 0; step >>= 1) s = s_off[s + step] <= o ? s + step : s;
-        if (s == kLdsSegs - 1 && s_off[kLdsSegs] <= o) s = kLdsSegs;
+        for (int step = kSegs / 2; step > 0; step >>= 1) s = s_off[s + step] <= o ? s + step : s;
+        if (s == kSegs - 1 && s_off[kSegs] <= o) s = kSegs;
         uint64_t off, len, ptr;
         int vec;
-        if (s < kLdsSegs) {
+        if (s < kSegs) {
             off = s_off[s];
             len = s_len[s];
             ptr = s_ptr[s];
             vec = s_vec[s];
         } else {  // dense span: keep walking in global memory
-            int g = s_seg0 + kLdsSegs;
+            int g = s_seg0 + kSegs;
             while (g + 1 < count && d[g + 1].off <= o) ++g;
             off = d[g].off;
             len = d[g].len;
@@ -156,6 +215,7 @@ SegmentCopier::~SegmentCopier() {
         if (sl.ready) (void)hipEventDestroy(sl.ready);
         if (sl.host) (void)hipHostFree(sl.host);
         if (sl.dev) (void)hipFree(sl.dev);
+        if (sl.idx) (void)hipFree(sl.idx);
     }
 }
 
@@ -197,6 +257,19 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     DDL_REQUIRE(flat && segs && bytes, DDL_STATUS_INVALID_ARGUMENT, "null pack arguments");
     const size_t need = (size_t)count * sizeof(SegDesc);
     Slot &sl = free_slot_();
+    // DDL_PACK_VARIANT (measurement only; tools/pack_tune.py, C5 bucket set, pack / unpack):
+    //   0: span kernel, 256 lanes x 16 chunks per 64 KiB span, in-kernel segment search  5.56 / 5.61 TB/s
+    //   1: segment tiles of 1 KiB, 64 lanes (default)                                     6.10 / 6.37
+    //   2: segment tiles of 2 KiB, 128 lanes                                              6.09 / 6.29
+    //   3: segment tiles of 4 KiB, 128 lanes x 2 chunks                                   5.74 / 6.30
+    // (spans of 2-8 KiB with the in-kernel search, with or without a precomputed first segment
+    // per span, measured 4.5-6.0: the per-chunk search and the LDS round trip cost more than
+    // the smaller window saves.)
+    static const int variant = [] {
+        const char *e = std::getenv("DDL_PACK_VARIANT");
+        const int v = e ? std::atoi(e) : 1;
+        return v >= 0 && v <= 3 ? v : 1;
+    }();
     if (need > sl.cap) {
         if (sl.host) DDL_HIP(hipHostFree(sl.host));
         if (sl.dev) DDL_HIP(hipFree(sl.dev));
@@ -205,41 +278,52 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
         DDL_HIP(hipHostMalloc(&sl.host, sl.cap, hipHostMallocDefault));
         DDL_HIP(hipMalloc(&sl.dev, sl.cap));
     }
+    // segment-aligned tiles (variants 1..3): tile bytes per workgroup; tile0 = running tile count
+    const uint64_t seg_tile = variant == 2 ? 2048 : variant == 3 ? 4096 : 1024;
     SegDesc *t = static_cast<SegDesc *>(sl.host);
-    uint64_t off = 0;
+    uint64_t off = 0, tiles = 0;
     for (int i = 0; i < count; ++i) {
         DDL_REQUIRE(bytes[i] == 0 || segs[i], DDL_STATUS_INVALID_ARGUMENT, "null segment " << i);
         t[i].ptr = reinterpret_cast<uint64_t>(segs[i]);
         t[i].off = off;
         t[i].len = bytes[i];
         t[i].vec = (reinterpret_cast<uintptr_t>(segs[i]) & 15u) == 0;
+        t[i].tile0 = (uint32_t)tiles;
         off += (bytes[i] + 255) & ~uint64_t(255);
+        tiles += (bytes[i] + seg_tile - 1) / seg_tile;
     }
+    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
     if (off == 0) return;
     DDL_HIP(hipMemcpyAsync(sl.dev, sl.host, need, hipMemcpyHostToDevice, stream));
-    // DDL_PACK_VARIANT (measurement only): bit 0 non-temporal stores, bit 1 32 chunks per lane
-    // instead of 16. Default 1: 16 chunks, NT stores — 5.5 / 5.6 TB/s pack / unpack on the C5
-    // bucket set vs 5.3 / 5.6 (cacheable stores) and 5.3 / 5.1 (32 chunks); tools/pack_tune.py.
-    static const int variant = [] {
-        const char *e = std::getenv("DDL_PACK_VARIANT");
-        return e ? std::atoi(e) : 1;
-    }();
-    const int iters = (variant & 2) ? 32 : 16;
-    const uint64_t spans = (off + kTileBytes * iters - 1) / (kTileBytes * iters);
-    DDL_REQUIRE(spans < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
     char *fl = static_cast<char *>(flat);
     const SegDesc *dd = static_cast<const SegDesc *>(sl.dev);
-#define DDL_PACK_LAUNCH(D, I, N) \
-    hipLaunchKernelGGL((k_segments<D, I, N>), dim3((unsigned)spans), dim3(kThreads), 0, stream, fl, dd, count, (uint64_t)off)
-    const bool nt = variant & 1;
-    if (dir == 0) {
-        if (iters == 16) { if (nt) DDL_PACK_LAUNCH(0, 16, true); else DDL_PACK_LAUNCH(0, 16, false); }
-        else { if (nt) DDL_PACK_LAUNCH(0, 32, true); else DDL_PACK_LAUNCH(0, 32, false); }
-    } else {
-        if (iters == 16) { if (nt) DDL_PACK_LAUNCH(1, 16, true); else DDL_PACK_LAUNCH(1, 16, false); }
-        else { if (nt) DDL_PACK_LAUNCH(1, 32, true); else DDL_PACK_LAUNCH(1, 32, false); }
+    if (variant == 0) {
+        const uint64_t spans = (off + 65535) / 65536;
+        DDL_REQUIRE(spans < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
+        if (dir == 0) hipLaunchKernelGGL((k_segments<0, 16, true, 256, 64>), dim3((unsigned)spans), dim3(256), 0, stream, fl, dd, count, (uint64_t)off);
+        else hipLaunchKernelGGL((k_segments<1, 16, true, 256, 64>), dim3((unsigned)spans), dim3(256), 0, stream, fl, dd, count, (uint64_t)off);
+    } else if (tiles > 0) {
+        const size_t ib = tiles * sizeof(int);
+        if (ib > sl.idx_cap) {
+            if (sl.idx) DDL_HIP(hipFree(sl.idx));
+            sl.idx = nullptr;
+            sl.idx_cap = ib + ib / 2;
+            DDL_HIP(hipMalloc(&sl.idx, sl.idx_cap));
+        }
+        int *ts = static_cast<int *>(sl.idx);
+        hipLaunchKernelGGL(k_tile_index, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, stream, dd, count,
+                           (uint64_t)tiles, ts);
+        const dim3 g((unsigned)tiles);
+        if (dir == 0) {
+            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<0, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts);
+            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<0, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts);
+            else hipLaunchKernelGGL((k_seg_tiles<0, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts);
+        } else {
+            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<1, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts);
+            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<1, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts);
+            else hipLaunchKernelGGL((k_seg_tiles<1, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts);
+        }
     }
-#undef DDL_PACK_LAUNCH
     DDL_HIP(hipGetLastError());
     DDL_HIP(hipEventRecord(sl.ready, stream));
 }

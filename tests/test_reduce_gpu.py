@@ -154,10 +154,13 @@ def test_pack_unpack_layouts(lib, gpu, case):
     torch.cuda.synchronize()
     f, src, dst = fused.cpu().numpy(), pool.cpu().numpy(), outpool.cpu().numpy()
     off = 0
+    covered = np.zeros(dst.size, dtype=bool)
     for s, x in zip(sizes, offs):
         assert np.array_equal(f[off:off + s], src[x:x + s])
         assert np.array_equal(dst[x:x + s], src[x:x + s])
+        covered[x:x + s] = True
         off += (s + 255) // 256 * 256
+    assert not dst[~covered].any()  # unpack writes nothing between or past the segments
 
 
 @pytest.mark.parametrize('dt', [1, 2, 3, 9, 14, 19, 23])

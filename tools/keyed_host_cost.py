@@ -1,0 +1,51 @@
+"""Host cost of the keyed path at one rank (measurement tool): the C5 batch of 4096 keyed
+allreduces split into the submit call (request construction, validation, sorted insertion)
+and the wait (handler wake-up, execution bookkeeping, done callbacks)."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
+
+
+def main():
+    import numpy as np
+    import torch
+    from ddl.torch.communicator import Communicator
+    from ddl.torch.cpp_backend import CPPBackend, DONE_FN, check
+    lib = CPPBackend.c_api()
+    comm = Communicator.world()
+    dev = torch.device('cuda', 0)
+    k = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    rng = np.random.default_rng(5)
+    sizes = (np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=k)).astype(np.int64) // 256) * 256
+    order = rng.permutation(k)
+    tensors, dts, keys = [], [], []
+    for i in order:
+        tensors.append(torch.empty(int(sizes[i]) // 4, device=dev))
+        dts.append(1)
+        keys.append(f'grad_{i:05d}'.encode())
+    K, V = ctypes.c_char_p * k, ctypes.c_void_p * k
+    args = (k, K(*keys), V(*[t.data_ptr() for t in tensors]), V(*[t.data_ptr() for t in tensors]),
+            (ctypes.c_size_t * k)(*[t.numel() for t in tensors]), (ctypes.c_int * k)(*dts), 0,
+            torch.cuda.current_stream(dev).cuda_stream, DONE_FN(), None)
+    sub, wait = [], []
+    for it in range(25):
+        t0 = time.perf_counter()
+        check(lib.ddl_allreduce_submit_batch(comm.id, *args), 'submit')
+        t1 = time.perf_counter()
+        check(lib.ddl_wait_all(comm.id), 'wait')
+        t2 = time.perf_counter()
+        if it >= 5:
+            sub.append(t1 - t0)
+            wait.append(t2 - t1)
+    print(json.dumps({'requests': k, 'submit_ms_median': round(1e3 * float(np.median(sub)), 3),
+                      'wait_ms_median': round(1e3 * float(np.median(wait)), 3),
+                      'total_ms_min': round(1e3 * min(a + b for a, b in zip(sub, wait)), 3)}))
+
+
+if __name__ == '__main__':
+    main()
