@@ -298,40 +298,48 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
         DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
     }
     if (slot_bytes_ < chunk) {
-        for (void *&s : slots_)
-            if (s) {
-                DDL_HIP(hipFree(s));
-                s = nullptr;
+        for (void *&sl : slots_)
+            if (sl) {
+                DDL_HIP(hipFree(sl));
+                sl = nullptr;
             }
-        for (void *&s : slots_) DDL_HIP(hipMalloc(&s, chunk));
+        for (void *&sl : slots_) DDL_HIP(hipMalloc(&sl, chunk));
         slot_bytes_ = chunk;
     }
     HostRegistration rs(send, total);
     HostRegistration rr(recv == send ? nullptr : recv, total);
-    hipEvent_t ev[6];  // h2d done, ring done, d2h done — per slot
-    for (hipEvent_t &e : ev) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // per slot: H2D done, ring done, D2H done. kHostSlots chunks in flight: the H2D of chunk i
+    // waits only for the D2H of chunk i - kHostSlots, so the copy engines never wait on a
+    // cross-stream round trip (2 slots: 14 GiB/s at 4 MiB chunks, 40 at 32 MiB)
+    hipEvent_t ev[3 * kHostSlots];
+    int made = 0;
     try {
+        for (hipEvent_t &e : ev) {
+            DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ++made;
+        }
         const RingConfig cfg = ring_config(chunk / es, dtype, ring_);
         const size_t nchunks = (total + chunk - 1) / chunk;
         for (size_t i = 0; i < nchunks; ++i) {
-            const int s = (int)(i & 1);
+            const int s = (int)(i % kHostSlots);
+            hipEvent_t &h2d_done = ev[3 * s], &ring_done = ev[3 * s + 1], &d2h_done = ev[3 * s + 2];
             const size_t off = i * chunk, bytes = total - off < chunk ? total - off : chunk;
-            if (i >= 2) DDL_HIP(hipStreamWaitEvent(h2d_, ev[4 + s], 0));  // slot's previous D2H done
+            if (i >= (size_t)kHostSlots) DDL_HIP(hipStreamWaitEvent(h2d_, d2h_done, 0));  // slot free again
             DDL_HIP(hipMemcpyAsync(slots_[s], static_cast<const char *>(send) + off, bytes, hipMemcpyHostToDevice, h2d_));
-            DDL_HIP(hipEventRecord(ev[s], h2d_));
-            DDL_HIP(hipStreamWaitEvent(ring_, ev[s], 0));
+            DDL_HIP(hipEventRecord(h2d_done, h2d_));
+            DDL_HIP(hipStreamWaitEvent(ring_, h2d_done, 0));
             exec_->allreduce(slots_[s], slots_[s], bytes / es, dtype, ring_, cfg);
-            DDL_HIP(hipEventRecord(ev[2 + s], ring_));
-            DDL_HIP(hipStreamWaitEvent(d2h_, ev[2 + s], 0));
+            DDL_HIP(hipEventRecord(ring_done, ring_));
+            DDL_HIP(hipStreamWaitEvent(d2h_, ring_done, 0));
             DDL_HIP(hipMemcpyAsync(static_cast<char *>(recv) + off, slots_[s], bytes, hipMemcpyDeviceToHost, d2h_));
-            DDL_HIP(hipEventRecord(ev[4 + s], d2h_));
+            DDL_HIP(hipEventRecord(d2h_done, d2h_));
         }
         DDL_HIP(hipStreamSynchronize(d2h_));
     } catch (...) {
         (void)hipStreamSynchronize(h2d_);
         (void)hipStreamSynchronize(ring_);
         (void)hipStreamSynchronize(d2h_);
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        for (int k = 0; k < made; ++k) (void)hipEventDestroy(ev[k]);
         throw;
     }
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);

@@ -121,7 +121,8 @@ private:
     TuneResult tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base);
     // host pipeline resources (lazily created)
     hipStream_t h2d_ = nullptr, ring_ = nullptr, d2h_ = nullptr;
-    void *slots_[2] = {nullptr, nullptr};
+    static constexpr int kHostSlots = 4;
+    void *slots_[kHostSlots] = {};
     size_t slot_bytes_ = 0;
 };
 

@@ -151,7 +151,7 @@ int ddl_allgather(ddl_communicator_id id, const void *send, size_t send_elements
 
 /* Host-resident buckets (the reference's deployment case: CPU tensors behind the MPI buffers,
  * MPIRingTokenCommunication.cc:548-733): chunked H2D -> ddl_allreduce -> D2H pipeline on three
- * streams ("host_chunk_bytes", default 32 MiB, double-buffered in HBM). Pageable memory is
+ * streams ("host_chunk_bytes", default 32 MiB; 4 chunk slots in HBM in flight). Pageable memory is
  * registered for the call; pinned memory avoids that cost. Synchronous: returns when `recv`
  * holds the result. Collective: every rank calls it with the same element count. */
 int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, size_t elements,
