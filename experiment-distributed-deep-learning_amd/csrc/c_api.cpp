@@ -89,6 +89,22 @@ int ddl_init(int rank, int size, int device, const void *unique_id, size_t len) 
 
 int ddl_init_single(int device) { return ddl_init(0, 1, device, nullptr, 0); }
 
+int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn group, ddl_test_max_fn max,
+                            void *user) {
+    return guarded([&] {
+        DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && group && max, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad test transport arguments");
+        DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
+        DDL_HIP(hipSetDevice(device));
+        auto hooks = std::make_shared<TestHooks>();
+        hooks->group = group;
+        hooks->max = max;
+        hooks->user = user;
+        Registry::get().set_world(std::make_shared<Communicator>(rank, size, device, nullptr, hooks, 0));
+        DDL_LOG(1, "initialized rank " << rank << "/" << size << " on device " << device << " (test transport)");
+    });
+}
+
 int ddl_control_listen(char *endpoint_out, size_t len) {
     return guarded([&] {
         std::string ep = world_control().listen();
@@ -351,6 +367,7 @@ int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, 
             if (send != recv) DDL_HIP(hipMemcpyAsync(recv, send, elements * dtype_size(dtype), hipMemcpyDeviceToDevice, as_stream(hip_stream)));
             return;
         }
+        DDL_REQUIRE(c->nccl() != nullptr, DDL_STATUS_INVALID_ARGUMENT, "no RCCL communicator (test transport)");
         ncclDataType_t t;
         switch (dtype) {
             case DDL_FLOAT: t = ncclFloat32; break;

@@ -56,11 +56,15 @@ DeviceGuard::~DeviceGuard() {
 }
 
 // ---- communicator -----------------------------------------------------------------------------
-Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl)
-    : rank_(rank), size_(size), device_(device), nccl_(nccl) {
+Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks,
+                           long long tag)
+    : rank_(rank), size_(size), device_(device), nccl_(nccl), hooks_(std::move(hooks)), tag_(tag) {
     DeviceGuard g(device_);
     std::unique_ptr<Transport> t;
-    if (size_ > 1) t.reset(new RcclTransport(nccl_));
+    if (size_ > 1) {
+        if (hooks_) t.reset(new CallbackTransport(hooks_, tag_));
+        else t.reset(new RcclTransport(nccl_));
+    }
     exec_.reset(new RingExecutor(rank_, size_, device_, std::move(t)));
 }
 
@@ -195,6 +199,11 @@ TuneResult Communicator::tune_(size_t n, int dtype, hipStream_t stream, const Ri
             size_, bytes, stream, base, [&](const RingConfig &c) { exec_->allreduce(a, b, n, dtype, stream, c); },
             [&](float *ms, int nc) {
                 DDL_REQUIRE(nc <= 64, DDL_STATUS_ERROR_UNKNOWN, "too many tuning candidates");
+                if (hooks_) {
+                    DDL_REQUIRE(hooks_->max(tag_, ms, nc, hooks_->user) == 0, DDL_STATUS_COMM_ERROR,
+                                "test transport: max callback failed");
+                    return;
+                }
                 DDL_HIP(hipMemcpyAsync(dms, ms, sizeof(float) * nc, hipMemcpyHostToDevice, stream));
                 rccl_check(rccl().AllReduce(dms, dms, nc, ncclFloat32, ncclMax, nccl_, stream), "ncclAllReduce(tune)");
                 DDL_HIP(hipMemcpyAsync(ms, dms, sizeof(float) * nc, hipMemcpyDeviceToHost, stream));
@@ -349,6 +358,11 @@ std::shared_ptr<Communicator> Communicator::split(int color, int key) {
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
     if (size_ == 1) return std::make_shared<Communicator>(0, 1, device_, nullptr);
+    if (hooks_) {  // test transport: the handler's private copy of this communicator
+        DDL_REQUIRE(color >= 0 && key == rank_, DDL_STATUS_INVALID_ARGUMENT,
+                    "test transport: split needs one color on every rank and key = rank");
+        return std::make_shared<Communicator>(rank_, size_, device_, nullptr, hooks_, hooks_->next_tag.fetch_add(1));
+    }
     ncclComm_t nc = nullptr;
     rccl_check(rccl().CommSplit(nccl_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr),
                "ncclCommSplit");

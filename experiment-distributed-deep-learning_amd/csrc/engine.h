@@ -75,7 +75,10 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
 
 class Communicator : public std::enable_shared_from_this<Communicator> {
 public:
-    Communicator(int rank, int size, int device, ncclComm_t nccl);
+    // `hooks` (test harness only, ddl_init_test_transport): groups go to host callbacks, `tag`
+    // names this communicator to them; nullptr = RCCL on `nccl`.
+    Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks = nullptr,
+                 long long tag = 0);
     ~Communicator();
 
     long long id() const { return reinterpret_cast<long long>(this); }
@@ -112,6 +115,8 @@ public:
 private:
     int rank_, size_, device_;
     ncclComm_t nccl_;
+    std::shared_ptr<TestHooks> hooks_;
+    long long tag_ = 0;
     std::mutex mu_;  // one collective at a time per communicator (RCCL ordering)
     std::unique_ptr<RingExecutor> exec_;
     std::unique_ptr<RequestHandler> handler_;

@@ -20,6 +20,24 @@ void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     rccl_check(e, "ncclGroupEnd");
 }
 
+void CallbackTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
+    if (ops.empty()) return;
+    DDL_HIP(hipStreamSynchronize(stream));  // the sends' data and the receive buffers are ready
+    std::vector<std::vector<char>> host(ops.size());
+    std::vector<ddl_p2p_op> v(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) {
+        host[i].resize(ops[i].bytes);
+        if (ops[i].send && ops[i].bytes)
+            DDL_HIP(hipMemcpy(host[i].data(), ops[i].ptr, ops[i].bytes, hipMemcpyDeviceToHost));
+        v[i] = ddl_p2p_op{ops[i].send ? 1 : 0, ops[i].peer, ops[i].tag, host[i].data(), ops[i].bytes};
+    }
+    const int rc = hooks_->group(tag_, v.data(), (int)v.size(), hooks_->user);
+    DDL_REQUIRE(rc == 0, DDL_STATUS_COMM_ERROR, "test transport: group callback failed (" << rc << ")");
+    for (size_t i = 0; i < ops.size(); ++i)
+        if (!ops[i].send && ops[i].bytes)
+            DDL_HIP(hipMemcpy(ops[i].ptr, host[i].data(), ops[i].bytes, hipMemcpyHostToDevice));
+}
+
 RankResources::RankResources(int dev) : device(dev) {
     DDL_HIP(hipStreamCreateWithFlags(&comm, hipStreamNonBlocking));
     DDL_HIP(hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));

@@ -8,6 +8,7 @@
 // synchronisation anywhere on the path.
 #pragma once
 
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -31,6 +32,27 @@ public:
 
 private:
     ncclComm_t comm_;
+};
+
+// Test harness only (ddl_init_test_transport): groups and the tuner's max-reduce go through
+// host callbacks, so several processes can run the whole engine on one GPU without RCCL.
+struct TestHooks {
+    ddl_test_group_fn group = nullptr;
+    ddl_test_max_fn max = nullptr;
+    void *user = nullptr;
+    std::atomic<long long> next_tag{1};  // communicator tags: 0 = world, then splits in order
+};
+
+// Synchronises the stream, stages the sends in host memory, runs the callback, copies the
+// received bytes to the device: the group is complete, in stream order, when group() returns.
+class CallbackTransport : public Transport {
+public:
+    CallbackTransport(std::shared_ptr<TestHooks> hooks, long long tag) : hooks_(std::move(hooks)), tag_(tag) {}
+    void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
+
+private:
+    std::shared_ptr<TestHooks> hooks_;
+    long long tag_;
 };
 
 // Streams, events and staging memory of one rank (reused across calls).

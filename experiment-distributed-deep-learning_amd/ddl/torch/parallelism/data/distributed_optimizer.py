@@ -4,13 +4,15 @@ src/py/ddl/tensorflow/keras/parallelism/data/distributed_optimizer.py:9-110).
 Every rank computes gradients on its shard of the batch; before the wrapped optimizer's
 `step()` each gradient is submitted as a keyed allreduce request (the reference builds one
 `Allreduce` op per gradient, :43-68), the engine negotiates and fuses them, and the sum is
-divided by the communicator size (allreduce_gradient, tensor_communicate.py:21-25). At
-size 1 nothing is communicated (the reference's `tf.cond(size > 1)`, :53-60).
+divided by the communicator size (allreduce_gradient, tensor_communicate.py:21-25). A sparse
+gradient (torch sparse COO, TF's IndexedSlices) goes through allreduce_gradient's allgather
+branch (:26-30), as the reference's wrapper does for every grad. At size 1 nothing is
+communicated (the reference's `tf.cond(size > 1)`, :53-60).
 """
 import torch
 
 from ddl.torch.communicator import Communicator
-from ddl.torch.tensor_communicate import allreduce_async_batch
+from ddl.torch.tensor_communicate import allreduce_async_batch, allreduce_gradient
 
 
 class DataParallelismDistributedOptimizer:
@@ -22,13 +24,14 @@ class DataParallelismDistributedOptimizer:
         comm = self.communicator or Communicator.world()
         if comm.size <= 1:
             return
-        params, grads, keys = [], [], []
+        params, grads, keys, sparse = [], [], [], []
         for gi, group in enumerate(self.param_groups):
             for pi, p in enumerate(group['params']):
                 if p.grad is None:
                     continue
                 if p.grad.is_sparse:
-                    raise NotImplementedError('sparse gradients need allgather (not implemented)')
+                    sparse.append(p)
+                    continue
                 params.append(p)
                 grads.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
                 keys.append(f'{self._ddl_name}/{type(self).__name__}/Allreduce/group{gi}/param{pi:05d}')
@@ -40,6 +43,9 @@ class DataParallelismDistributedOptimizer:
             out.div_(comm.size)
             if out.data_ptr() != p.grad.data_ptr():
                 p.grad.copy_(out)
+        # sparse gradients: every rank's rows gathered, values averaged (same order on all ranks)
+        for p in sparse:
+            p.grad = allreduce_gradient(p.grad, comm)
 
     @torch.no_grad()
     def step(self, closure=None):

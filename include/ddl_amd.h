@@ -88,6 +88,27 @@ size_t ddl_dtype_size(int dtype); /* 0 for unsupported */
 int ddl_get_unique_id(void *out, size_t len);
 /* Creates the world communicator for this process (one process per GPU). */
 int ddl_init(int rank, int size, int device, const void *unique_id, size_t len);
+
+/* TEST HARNESS ONLY (not a product path): a world communicator whose point-to-point groups and
+ * the autotuner's max-reduce go through host callbacks instead of RCCL, so the multi-process
+ * engine — control channel, keyed handler, fusion, schedules, streams, kernels — can run as
+ * several processes sharing one GPU (RCCL refuses two ranks on one device). `comm_tag` names
+ * the communicator (0 = world, then one per split in creation order), so the callbacks can keep
+ * concurrent communicators apart. The engine synchronises the group's stream, stages every
+ * send into host memory, calls the group callback — which must complete the whole exchange on
+ * the host buffers before it returns, 0 = success — and copies the received host buffers to
+ * the device. Splits must give every rank the same color and key = rank. */
+typedef struct ddl_p2p_op {
+    int send;     /* 1 send, 0 receive */
+    int peer;     /* rank in the communicator */
+    int tag;      /* matches a send with its receive inside one group (posting order per tag) */
+    void *ptr;    /* host staging buffer of `bytes` */
+    size_t bytes;
+} ddl_p2p_op;
+typedef int (*ddl_test_group_fn)(long long comm_tag, const ddl_p2p_op *ops, int count, void *user);
+typedef int (*ddl_test_max_fn)(long long comm_tag, float *values, int count, void *user);
+int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn group, ddl_test_max_fn max,
+                            void *user);
 /* Same, for a single-process world (size 1); no RCCL involved. */
 int ddl_init_single(int device);
 /* Optional control channel for keyed requests at size > 1 (ring of TCP links, replaces the

@@ -1,0 +1,312 @@
+"""Worker of tests/test_multiproc_gpu.py: P processes share the one GPU and run the whole engine
+as at N > 1 — world communicator, TCP token ring, keyed handler, fusion pipeline, ring / direct /
+one-shot schedules, the autotuner, streams and kernels — with only the point-to-point groups
+carried differently: through gloo on host copies (ddl_init_test_transport), because RCCL
+refuses two ranks on one device. Every check compares with the oracle or an exact sum; every
+rank runs the same checks in the same order (they are collectives) and reports
+(name, ok, detail). Test infrastructure only."""
+import ctypes
+import os
+import sys
+import traceback
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+class P2POp(ctypes.Structure):  # ddl_p2p_op (include/ddl_amd.h)
+    _fields_ = [('send', ctypes.c_int), ('peer', ctypes.c_int), ('tag', ctypes.c_int), ('ptr', ctypes.c_void_p),
+                ('bytes', ctypes.c_size_t)]
+
+
+GROUP_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(P2POp), ctypes.c_int, ctypes.c_void_p)
+MAX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                          ctypes.c_void_p)
+
+
+def _tag(comm_tag, t):
+    return int(comm_tag) * 4096 + int(t)  # communicators (world, handler copy) never share a tag
+
+
+def make_callbacks(dist, torch, rank, world):
+    def group(comm_tag, ops, count, user):
+        try:
+            reqs = []
+            for i in range(count):
+                op = ops[i]
+                if op.bytes == 0:
+                    continue
+                t = torch.frombuffer((ctypes.c_uint8 * op.bytes).from_address(op.ptr), dtype=torch.uint8)
+                tg = _tag(comm_tag, op.tag)
+                reqs.append(dist.isend(t, op.peer, tag=tg) if op.send else dist.irecv(t, op.peer, tag=tg))
+            for r in reqs:
+                r.wait()
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def vmax(comm_tag, vals, count, user):
+        try:
+            t = torch.tensor([vals[i] for i in range(count)], dtype=torch.float32)
+            tg = _tag(comm_tag, 4000)
+            if rank == 0:
+                for q in range(1, world):
+                    o = torch.empty_like(t)
+                    dist.recv(o, q, tag=tg)
+                    t = torch.maximum(t, o)
+                for q in range(1, world):
+                    dist.send(t, q, tag=tg + 1)
+            else:
+                dist.send(t, 0, tag=tg)
+                dist.recv(t, 0, tag=tg + 1)
+            for i in range(count):
+                vals[i] = float(t[i])
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    return GROUP_FN(group), MAX_FN(vmax)
+
+
+# ---- checks ------------------------------------------------------------------------------------
+def _dev(torch, x, dev):
+    return torch.from_numpy(x.view(np.int16) if x.dtype == np.uint16 else x).to(dev)
+
+
+def _host(t, like):
+    return t.cpu().numpy().view(like.dtype)
+
+
+def check_reference_known_answers(ctx):
+    """The reference's own test scripts (src/py/ddl/test/*.py) with their known answers."""
+    torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.tensor_communicate import allgather, allreduce, broadcast
+    x = torch.full((16,), float(r), device='cuda')  # allreduce_test.py:13
+    assert torch.equal(allreduce(x, comm), torch.full((16,), float(P * (P - 1) // 2), device='cuda'))
+    root = 3 if P >= 4 else P - 1  # broadcast_test.py:13-14 (root 3 needs P >= 4)
+    y = torch.full((16,), float(r + 1), device='cuda')
+    assert torch.equal(broadcast(y, root, comm), torch.full((16,), float(root + 1), device='cuda'))
+    v = torch.arange(4 + r, dtype=torch.float32, device='cuda') + r  # allgather_test.py:13-21
+    idx = torch.tensor([[0, 0], [1, 1], [2, 2], [3, 3]], dtype=torch.float32, device='cuda') + r
+    want_v = torch.cat([torch.arange(4 + q, dtype=torch.float32) + q for q in range(P)])
+    want_i = torch.cat([torch.tensor([[0, 0], [1, 1], [2, 2], [3, 3]], dtype=torch.float32) + q for q in range(P)])
+    assert torch.equal(allgather(v, comm).cpu(), want_v)
+    assert torch.equal(allgather(idx, comm).cpu(), want_i)
+
+
+def check_schedules_vs_oracle(ctx):
+    """ddl_allreduce with each schedule fixed (tuner off): every rank equals the oracle's
+    summation in that schedule's order, bit for bit, in and out of place, all dtypes."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    s = torch.cuda.current_stream().cuda_stream
+    with h.config(lib, tune=0, slice_bytes=64 << 10):
+        for algo in (0, 1, 2):
+            with h.config(lib, algo=algo):
+                for dt in (h.DT_FLOAT, h.DT_HALF, h.DT_INT32, h.DT_BFLOAT16, h.DT_DOUBLE):
+                    for n in (1, 4099, 300_001):
+                        xs = [h.random_input(dt, n, 100 * algo + 7 * dt + 13 * q + n) for q in range(P)]
+                        if algo == 0:
+                            R, _ = h.ring_shape(lib, n, dt, P)
+                            want = ora.allreduce_ring(dt, xs, h.ring_perms(lib, P, R))
+                        elif algo == 1:
+                            want = ora.allreduce_direct(dt, xs)
+                        else:
+                            want = ora.fold(dt, xs)
+                        for in_place in (False, True):
+                            a = _dev(torch, xs[r], 'cuda')
+                            b = a if in_place else torch.empty_like(a)
+                            st = lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), n, dt, 0, s)
+                            assert st == 0, lib.ddl_last_error()
+                            got = _host(b, xs[r])
+                            assert got.tobytes() == want.tobytes(), (algo, dt, n, in_place)
+
+
+def check_tuned_exact(ctx):
+    """Autotuner on (collective timing, max over ranks through the transport): every rank picks
+    the same schedule per size class, and exactly summable buckets come out exact."""
+    import _helpers as h
+    torch, lib, comm, P, r, dist = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['dist']
+    s = torch.cuda.current_stream().cuda_stream
+    with h.config(lib, tune=1):
+        picks = []
+        for nbytes in (64 << 10, 4 << 20, 24 << 20):
+            n = nbytes // 4
+            xs = [h.random_input(h.DT_FLOAT, n, 5 + q, kind='exact') for q in range(P)]
+            want = np.sum(np.stack(xs).astype(np.float64), axis=0).astype(np.float32)
+            a = _dev(torch, xs[r], 'cuda')
+            assert lib.ddl_allreduce(comm.id, a.data_ptr(), a.data_ptr(), n, h.DT_FLOAT, 0, s) == 0, lib.ddl_last_error()
+            assert np.array_equal(_host(a, xs[r]), want), nbytes
+            chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
+            cfgs = (ctypes.c_longlong * 64)()
+            tms = (ctypes.c_float * 16)()
+            assert lib.ddl_tune_result(comm.id, nbytes, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16) == 0
+            assert chosen.value >= 0 and count.value >= 2
+            picks.append((chosen.value, [round(tms[i], 6) for i in range(count.value)]))
+        everyone = [None] * P
+        dist.all_gather_object(everyone, picks)
+        assert all(e == picks for e in everyone), everyone  # same choice and same agreed times
+
+
+def check_keyed_fusion(ctx):
+    """Keyed batches registered in a different order on every rank: negotiated, grouped by dtype,
+    fused into plans capped at 1 MiB + 1 and pipelined over 256 KiB sub-plans; two rounds (the
+    second by id-table index). Integer-valued data, so every dtype's sum is exact."""
+    import _helpers as h
+    torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    dts = [torch.float32, torch.float16, torch.int32, torch.bfloat16, torch.float64, torch.int64]
+    rng = np.random.default_rng(11)
+    k = 120
+    sizes = [int(np.exp(rng.uniform(0, np.log(200_000)))) for _ in range(k)]
+    with h.config(lib, fusion_threshold_bytes=(1 << 20) + 1, fusion_pipeline_bytes=256 << 10):
+        for rnd in range(2):
+            gen = [torch.Generator().manual_seed(1000 * rnd + i) for i in range(k)]
+            base = [torch.randint(-8, 9, (sizes[i],), generator=gen[i]) for i in range(k)]
+            ts = [(base[i] + r).to(dts[i % len(dts)]).cuda() for i in range(k)]
+            want = [(base[i] * P + P * (P - 1) // 2).to(dts[i % len(dts)]) for i in range(k)]
+            order = np.random.default_rng(100 * rnd + r).permutation(k)  # per-rank submission order
+            hs = allreduce_async_batch([ts[i] for i in order], [f'g_{i:04d}' for i in order], comm)  # same keys
+            for i, hd in zip(order, hs):
+                got = hd.wait(timeout=120).cpu()
+                assert torch.equal(got, want[i]), (rnd, i, dts[i % len(dts)])
+    sr, cr = ctypes.c_longlong(), ctypes.c_longlong()
+    assert lib.ddl_control_stats(ctypes.byref(sr), ctypes.byref(cr)) == 0
+    assert cr.value >= 1  # the repeated key set went by id-table index
+
+
+def check_keyed_broadcast_allgather(ctx):
+    """Keyed broadcasts with mixed roots and dtypes, keyed allgathers with per-rank first dims."""
+    torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.tensor_communicate import allgather_async, broadcast_async
+    hs, want = [], []
+    for i in range(12):
+        root, dt = i % P, [torch.float32, torch.int64, torch.float16][i % 3]
+        t = (torch.arange(1000 + 37 * i) + 100 * r).to(dt).cuda()
+        hs.append(broadcast_async(t, f'b{i:02d}', root, comm))
+        want.append((torch.arange(1000 + 37 * i) + 100 * root).to(dt))
+    for hd, w in zip(hs, want):
+        assert torch.equal(hd.wait(timeout=120).cpu(), w)
+    hs, want = [], []
+    for i in range(6):
+        dt = [torch.float32, torch.int32][i % 2]
+        t = (torch.arange((r + 1 + i) * 5).reshape(-1, 5) + 1000 * r).to(dt).cuda()
+        hs.append(allgather_async(t, f'ag{i}', comm))
+        want.append(torch.cat([(torch.arange((q + 1 + i) * 5).reshape(-1, 5) + 1000 * q).to(dt) for q in range(P)]))
+    for hd, w in zip(hs, want):
+        assert torch.equal(hd.wait(timeout=120).cpu(), w)
+
+
+def check_host_resident(ctx):
+    """allreduce of a CPU tensor: the chunked H2D -> ring -> D2H pipeline (4 slots), many chunks."""
+    import _helpers as h
+    torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.tensor_communicate import allreduce
+    n = 1_000_003
+    base = torch.randint(-1000, 1000, (n,), generator=torch.Generator().manual_seed(9))
+    with h.config(lib, host_chunk_bytes=256 << 10):
+        got = allreduce((base + r).to(torch.float32), comm)
+    assert not got.is_cuda
+    assert torch.equal(got, (base * P + P * (P - 1) // 2).to(torch.float32))
+
+
+def check_dp_training(ctx):
+    """Scripts-level drop-in: InitialParametersBroadcast, the DP optimizer wrapper (dense grads
+    through keyed fused allreduces, a sparse embedding grad through allgather), MetricAverage.
+    Replicas stay identical and equal one full-batch step on the concatenated data."""
+    torch, comm, P, r, dist = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank'], ctx['dist']
+    from ddl.torch.parallelism.data import (InitialParametersBroadcast, MetricAverage,
+                                            data_parallelism_distributed_optimizer_wrapper)
+
+    def model_fn(seed):
+        torch.manual_seed(seed)
+        return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4)).double().cuda()
+    model = model_fn(1234 + r)  # different initial weights on every rank
+    InitialParametersBroadcast(model, 0, communicator=comm).broadcast()
+    ref = model_fn(1234)  # rank 0's initial weights
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.equal(p, q)
+    opt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(model.parameters(), lr=0.1), comm)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(77)
+    for step in range(3):
+        xb = [torch.randn(8, 16, generator=g, dtype=torch.float64) for _ in range(P)]
+        yb = [torch.randn(8, 4, generator=g, dtype=torch.float64) for _ in range(P)]
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(xb[r].cuda()), yb[r].cuda()).backward()
+        opt.step()
+        ref_opt.zero_grad()  # mean of the per-rank losses = what the averaged gradients descend
+        sum(torch.nn.functional.mse_loss(ref(xb[q].cuda()), yb[q].cuda()) for q in range(P)).div(P).backward()
+        ref_opt.step()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, rtol=1e-12, atol=1e-12)
+    # sparse gradient (IndexedSlices branch, tensor_communicate.py:26-30) through the wrapper
+    emb = torch.nn.Embedding(10, 3, sparse=True).double().cuda()
+    InitialParametersBroadcast(emb, 0, communicator=comm).broadcast()
+    w0 = emb.weight.detach().clone()
+    eopt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(emb.parameters(), lr=1.0), comm)
+    eopt.zero_grad()
+    emb(torch.tensor([r, r + 1], device='cuda')).sum().backward()
+    eopt.step()
+    want = w0.clone()
+    for q in range(P):
+        want[q] -= 1.0 / P
+        want[q + 1] -= 1.0 / P
+    assert torch.allclose(emb.weight.detach(), want)
+    logs = MetricAverage(comm).on_epoch_end(0, {'loss': float(r), 'acc': 2.0 * r})
+    assert logs == {'loss': (P - 1) / 2, 'acc': float(P - 1)}
+
+
+CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
+          check_keyed_broadcast_allgather, check_host_resident, check_dp_training]
+
+
+def worker(rank, world, port, q):
+    results = []
+    try:
+        for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), HERE):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        import datetime
+
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group('gloo', rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+        torch.cuda.set_device(0)
+        import _helpers as h
+        from ddl.torch.communicator import Communicator
+        from ddl.torch.cpp_backend import CPPBackend, check
+        lib = CPPBackend.c_api()
+        lib.ddl_init_test_transport.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, GROUP_FN, MAX_FN,
+                                                ctypes.c_void_p]
+        lib.ddl_init_test_transport.restype = ctypes.c_int
+        cbs = make_callbacks(dist, torch, rank, world)  # keep referenced for the process lifetime
+        check(lib.ddl_init_test_transport(rank, world, 0, cbs[0], cbs[1], None), 'ddl_init_test_transport')
+        ep = ctypes.create_string_buffer(256)
+        check(lib.ddl_control_listen(ep, 256), 'ddl_control_listen')
+        eps = [None] * world
+        dist.all_gather_object(eps, ep.value.decode())
+        check(lib.ddl_control_connect(';'.join(eps).encode()), 'ddl_control_connect')
+        comm = Communicator.world()
+        assert comm.size == world and comm.rank == rank
+        ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
+               'oracle': h.Oracle()}
+        for fn in CHECKS:
+            try:
+                fn(ctx)
+                results.append((fn.__name__, True, ''))
+            except Exception:
+                results.append((fn.__name__, False, traceback.format_exc()[-1500:]))
+                break  # a failed collective leaves the ranks out of step: stop here
+        dist.barrier()
+        from ddl.torch.communicator import finalize
+        finalize()
+    except Exception:
+        results.append(('setup', False, traceback.format_exc()[-2000:]))
+    q.put((rank, results))

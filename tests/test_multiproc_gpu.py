@@ -1,0 +1,51 @@
+"""The N>1 product path on one GPU: P = 2, 3, 4 processes share the card and run the engine
+end to end — world communicator, TCP token ring, keyed handler (negotiation, dtype groups,
+fusion pipeline, cached ids), ring / direct / one-shot schedules, the collective autotuner,
+broadcast / allgather, the host-resident pipeline and the scripts-level DP wrapper and
+callbacks — checked against the oracle and exact sums (tests/_mp_gpu_worker.py). Only the
+point-to-point groups differ from an RCCL run: they go through gloo on host copies
+(ddl_init_test_transport), because RCCL refuses two ranks on one device."""
+import socket
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('world', [2, 3, 4])
+def test_engine_multiprocess_on_one_gpu(gpu, world):
+    import torch.multiprocessing as mp
+
+    import _mp_gpu_worker
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_gpu_worker.worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, results = q.get(timeout=100)
+            res[rank] = results
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+        for p in procs:  # only our own children, by handle
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    assert sorted(res) == list(range(world)), f'ranks reported: {sorted(res)}'
+    names = [n for n, _, _ in res[0]]
+    assert names and names[-1] == 'check_dp_training' or any(not ok for _, ok, _ in res[0]), names
+    for rank, results in sorted(res.items()):
+        for name, ok, detail in results:
+            assert ok, f'rank {rank} {name}:\n{detail}'
