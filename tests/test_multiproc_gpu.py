@@ -1,10 +1,11 @@
-"""The N>1 product path on one GPU: P = 2, 3, 4 processes share the card and run the engine
+"""The N>1 product path on one GPU: P = 2, 3, 4, 8 processes share the card and run the engine
 end to end — world communicator, TCP token ring, keyed handler (negotiation, dtype groups,
 fusion pipeline, cached ids), ring / direct / one-shot schedules, the collective autotuner,
 broadcast / allgather, the host-resident pipeline and the scripts-level DP wrapper and
 callbacks — checked against the oracle and exact sums (tests/_mp_gpu_worker.py). Only the
 point-to-point groups differ from an RCCL run: they go through gloo on host copies
 (ddl_init_test_transport), because RCCL refuses two ranks on one device."""
+import os
 import socket
 
 import pytest
@@ -20,7 +21,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize('world', [2, 3, 4])
+@pytest.mark.parametrize('world', [2, 3, 4, 8])
 def test_engine_multiprocess_on_one_gpu(gpu, world):
     import torch.multiprocessing as mp
 
@@ -34,7 +35,7 @@ def test_engine_multiprocess_on_one_gpu(gpu, world):
     res = {}
     try:
         for _ in range(world):
-            rank, results = q.get(timeout=100)
+            rank, results = q.get(timeout=float(os.environ.get('DDL_MP_TIMEOUT', 100)))
             res[rank] = results
     finally:
         for p in procs:
