@@ -51,6 +51,11 @@ def parse():
     ap.add_argument('--no-collectives', action='store_true', help='N>1: skip broadcast/allgather timing')
     ap.add_argument('--no-config-sweep', action='store_true', help='N>1: skip the ring config sweep')
     ap.add_argument('--no-size-sweep', action='store_true', help='N>1: skip the bucket-size sweep (ours vs RCCL)')
+    ap.add_argument('--size-sweep-max-mib', type=int, default=1024, help='N>1: largest bucket of the size sweep')
+    ap.add_argument('--rehearse', action='store_true',
+                    help='N>1 on ONE GPU: run every leg with the point-to-point groups over gloo host copies '
+                         '(test-harness transport, tools/gloo_transport.py) instead of RCCL; exercises the '
+                         'bench code, its numbers are not measurements')
     ap.add_argument('--watchdog-s', type=float, default=420.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
@@ -410,7 +415,7 @@ def multi_gpu(args):
     from ddl.torch.cpp_backend import CPPBackend, check
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
-    local = int(os.environ.get('LOCAL_RANK', rank))
+    local = 0 if args.rehearse else int(os.environ.get('LOCAL_RANK', rank))
 
     state = {'out': None, 'leg': 'main'}  # rank 0's result so far; the leg in progress
 
@@ -437,8 +442,12 @@ def multi_gpu(args):
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    comm = Communicator.world()
     lib = CPPBackend.c_api()
+    if args.rehearse:  # every rank on cuda:0, groups over gloo (RCCL refuses two ranks on one GPU)
+        sys.path.insert(0, os.path.join(ROOT, 'tools'))
+        import gloo_transport
+        state['callbacks'] = gloo_transport.init_world(lib, dist, torch, rank, world, device=local)
+    comm = Communicator.world()
     dev = torch.device('cuda', local)
     S = args.bucket_mib << 20
     n = S // 4
@@ -538,12 +547,15 @@ def multi_gpu(args):
         'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
                   'sum_of_inputs': ref.item()},
     }
+    if args.rehearse:
+        out['rehearsal'] = 'point-to-point over gloo host copies on one GPU: exercises the N>1 legs, NOT a measurement'
     state['out'] = out  # from here on a hung optional leg still reports the headline result
 
     state['leg'] = 'rccl_comparator'
-    sec_rccl = timed(1, max(5, args.steps // 2), 3)
-    out['rccl_allreduce_comparator'] = {'ms': round(sec_rccl * 1e3, 4),
-                                        'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
+    if not args.rehearse:
+        sec_rccl = timed(1, max(5, args.steps // 2), 3)
+        out['rccl_allreduce_comparator'] = {'ms': round(sec_rccl * 1e3, 4),
+                                            'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
     # fixed schedules, tuner off (every rank sets the same values in the same order: the
     # schedule must be identical on all ranks)
     state['leg'] = 'schedule_sweep'
@@ -609,6 +621,8 @@ def multi_gpu(args):
     if not args.no_size_sweep:
         curve = []
         for sz in (4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+            if sz > args.size_sweep_max_mib << 20:
+                break
             m = sz // 4
             a = torch.randn(m, device=dev, generator=g)
             b = torch.empty_like(a)
@@ -618,7 +632,7 @@ def multi_gpu(args):
                 check(lib.ddl_allreduce_variant(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0,
                                                 stream.cuda_stream, variant), 'ddl_allreduce_variant')
             t_ours = timed_fn(lambda: one(0), reps, 3)
-            t_rccl = timed_fn(lambda: one(1), reps, 3)
+            t_rccl = t_ours if args.rehearse else timed_fn(lambda: one(1), reps, 3)
             chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
             check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
                   'ddl_tune_result')

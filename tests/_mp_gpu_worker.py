@@ -16,62 +16,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-class P2POp(ctypes.Structure):  # ddl_p2p_op (include/ddl_amd.h)
-    _fields_ = [('send', ctypes.c_int), ('peer', ctypes.c_int), ('tag', ctypes.c_int), ('ptr', ctypes.c_void_p),
-                ('bytes', ctypes.c_size_t)]
-
-
-GROUP_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(P2POp), ctypes.c_int, ctypes.c_void_p)
-MAX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
-                          ctypes.c_void_p)
-
-
-def _tag(comm_tag, t):
-    return int(comm_tag) * 4096 + int(t)  # communicators (world, handler copy) never share a tag
-
-
-def make_callbacks(dist, torch, rank, world):
-    def group(comm_tag, ops, count, user):
-        try:
-            reqs = []
-            for i in range(count):
-                op = ops[i]
-                if op.bytes == 0:
-                    continue
-                t = torch.frombuffer((ctypes.c_uint8 * op.bytes).from_address(op.ptr), dtype=torch.uint8)
-                tg = _tag(comm_tag, op.tag)
-                reqs.append(dist.isend(t, op.peer, tag=tg) if op.send else dist.irecv(t, op.peer, tag=tg))
-            for r in reqs:
-                r.wait()
-            return 0
-        except Exception:
-            traceback.print_exc()
-            return 1
-
-    def vmax(comm_tag, vals, count, user):
-        try:
-            t = torch.tensor([vals[i] for i in range(count)], dtype=torch.float32)
-            tg = _tag(comm_tag, 4000)
-            if rank == 0:
-                for q in range(1, world):
-                    o = torch.empty_like(t)
-                    dist.recv(o, q, tag=tg)
-                    t = torch.maximum(t, o)
-                for q in range(1, world):
-                    dist.send(t, q, tag=tg + 1)
-            else:
-                dist.send(t, 0, tag=tg)
-                dist.recv(t, 0, tag=tg + 1)
-            for i in range(count):
-                vals[i] = float(t[i])
-            return 0
-        except Exception:
-            traceback.print_exc()
-            return 1
-
-    return GROUP_FN(group), MAX_FN(vmax)
-
-
 # ---- checks ------------------------------------------------------------------------------------
 def _dev(torch, x, dev):
     return torch.from_numpy(x.view(np.int16) if x.dtype == np.uint16 else x).to(dev)
@@ -268,7 +212,7 @@ CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_
 def worker(rank, world, port, q):
     results = []
     try:
-        for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), HERE):
+        for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), HERE, os.path.join(ROOT, 'tools')):
             if p not in sys.path:
                 sys.path.insert(0, p)
         os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -283,16 +227,8 @@ def worker(rank, world, port, q):
         from ddl.torch.communicator import Communicator
         from ddl.torch.cpp_backend import CPPBackend, check
         lib = CPPBackend.c_api()
-        lib.ddl_init_test_transport.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, GROUP_FN, MAX_FN,
-                                                ctypes.c_void_p]
-        lib.ddl_init_test_transport.restype = ctypes.c_int
-        cbs = make_callbacks(dist, torch, rank, world)  # keep referenced for the process lifetime
-        check(lib.ddl_init_test_transport(rank, world, 0, cbs[0], cbs[1], None), 'ddl_init_test_transport')
-        ep = ctypes.create_string_buffer(256)
-        check(lib.ddl_control_listen(ep, 256), 'ddl_control_listen')
-        eps = [None] * world
-        dist.all_gather_object(eps, ep.value.decode())
-        check(lib.ddl_control_connect(';'.join(eps).encode()), 'ddl_control_connect')
+        import gloo_transport
+        cbs = gloo_transport.init_world(lib, dist, torch, rank, world)  # noqa: F841 (keep alive)
         comm = Communicator.world()
         assert comm.size == world and comm.rank == rank
         # the configured schedule unless a check turns the tuner on (check_tuned_exact): tuning
