@@ -39,6 +39,8 @@ class Oracle:
         L.ddlo_allreduce_direct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.c_void_p, SZ]
         L.ddlo_fold.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, SZ]
+        L.ddlo_fold_ref_order.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                          SZ, SZ]
         PV = ctypes.POINTER(ctypes.c_void_p)
         L.ddlo_broadcast.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, PV, SZ]
         L.ddlo_allgatherv.argtypes = [ctypes.c_int, ctypes.c_int, PV, ctypes.POINTER(SZ), ctypes.POINTER(SZ),
@@ -94,6 +96,16 @@ class Oracle:
         out = np.empty_like(xs[0])
         arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
         assert self.lib.ddlo_fold(dt, ptr(out), arr, len(xs), xs[0].size) == 0
+        return out
+
+    def fold_ref_order(self, dt, xs, total_bytes=None):
+        """Sum of xs (rank order) in MPICH 3.3.2's MPI_Allreduce order for a message of
+        total_bytes (default: the whole of one input)."""
+        xs = [np.ascontiguousarray(x) for x in xs]
+        out = np.empty_like(xs[0])
+        arr = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
+        tb = xs[0].nbytes if total_bytes is None else total_bytes
+        assert self.lib.ddlo_fold_ref_order(dt, ptr(out), arr, len(xs), xs[0].size, tb) == 0
         return out
 
     def broadcast(self, dt, xs, root):

@@ -99,6 +99,20 @@ CASES = [
     ("fp64_randn_P4", "randn", "float64", 4, 515),
     ("int64_rand_P4", "randint", "int64", 4, 515),
     ("uint64_rand_P2", "randint", "uint64", 2, 515),
+    # non-power-of-two P on both sides of MPICH's 2048-byte algorithm switch (the order of the
+    # additions differs there: binomial tree below, pre-fold + pairwise tree above)
+    ("fp32_randn_P3_small", "randn", "float32", 3, 300),
+    ("fp32_randn_P3", "randn", "float32", 3, 1031),
+    ("fp32_randn_P5_small", "randn", "float32", 5, 512),
+    ("fp32_randn_P5_switch", "randn", "float32", 5, 513),
+    ("fp32_randn_P5", "randn", "float32", 5, 4099),
+    ("fp32_randn_P6", "randn", "float32", 6, 4099),
+    ("fp32_randn_P7_small", "randn", "float32", 7, 200),
+    ("fp32_randn_P7", "randn", "float32", 7, 4099),
+    ("fp64_randn_P5_small", "randn", "float64", 5, 256),
+    ("fp64_randn_P5", "randn", "float64", 5, 257),
+    ("fp64_randn_P8", "randn", "float64", 8, 515),
+    ("fp32_randn_P8_large", "randn", "float32", 8, 16387),
 ]
 
 

@@ -5,10 +5,11 @@ reference's data-plane call, src/cpp/communicate/backend/mpi/MPICommunicator.cc:
 with mpiexec -n P; the reference's own known answer (src/py/ddl/test/allreduce_test.py:13);
 and the reference outputs recorded in SURVEY.md §4.
 
-Parity bar: bit-exact for integers, fp32 at P=2 (a single commutative add) and exactly
-summable fp32 at any P; random fp32/fp64 at P>2 within the summation bound
-|y - y_hat| <= (P-1) * u * sum_r |x_r| (u = unit roundoff), since MPICH's reduction order is
-its own (recursive doubling / Rabenseifner) and differs from rank order.
+Parity bar: the oracle's restatement of MPICH's own summation order (ddlo_fold_ref_order:
+binomial tree up to 2048 bytes, pre-fold + pairwise tree above) is bit-exact with every golden
+case, every dtype and P = 2..8; the rank-order fold is bit-exact for integers, fp32 at P=2 and
+exactly summable fp32, and within the summation bound |y - y_hat| <= (P-1) * u * sum_r |x_r|
+(u = unit roundoff) otherwise.
 """
 import json
 import os
@@ -25,9 +26,11 @@ CASES = sorted(MANIFEST['cases'])
 
 
 def _bound(xs, dtype):
+    """Largest difference between two summation orders of the same P terms: each is within
+    (P-1) u sum|x| of the exact sum, so two of them are within twice that of each other."""
     u = np.finfo(dtype).eps / 2
     P = xs.shape[0]
-    return (P - 1) * u * np.abs(xs.astype(np.float64)).sum(axis=0) * 1.0001
+    return 2 * (P - 1) * u * np.abs(xs.astype(np.float64)).sum(axis=0) * 1.0001
 
 
 @pytest.mark.parametrize('case', CASES)
@@ -43,6 +46,27 @@ def test_oracle_matches_mpich(oracle, case):
     else:
         err = np.abs(seq.astype(np.float64) - y.astype(np.float64))
         assert np.all(err <= _bound(xs, xs.dtype)), f'{case}: outside the summation bound'
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_reference_order_is_bit_exact_with_mpich(oracle, case):
+    """MPICH's summation order, restated (ddlo_fold_ref_order), reproduces MPI_Allreduce's output
+    bit for bit — random fp32/fp64 at non-power-of-two P on both sides of the 2048-byte
+    algorithm switch included."""
+    meta = MANIFEST['cases'][case]
+    xs, y = GOLD[case + '__inputs'], GOLD[case + '__output']
+    got = oracle.fold_ref_order(FROM_NP[meta['dtype']], list(xs))
+    assert got.tobytes() == y.tobytes(), f'{case}: {int((got != y).sum())} elements differ'
+
+
+def test_reference_order_switch_is_what_distinguishes_p5(oracle):
+    """At P=5 the two MPICH trees differ: each golden case matches exactly one of them, the one
+    its message size selects (<= 2048 bytes: binomial)."""
+    for case, small in (('fp32_randn_P5_small', True), ('fp32_randn_P5_switch', False)):
+        xs, y = GOLD[case + '__inputs'], GOLD[case + '__output']
+        tiny = oracle.fold_ref_order(1, list(xs), total_bytes=2048)
+        big = oracle.fold_ref_order(1, list(xs), total_bytes=2049)
+        assert (tiny.tobytes() == y.tobytes()) == small and (big.tobytes() == y.tobytes()) == (not small)
 
 
 @pytest.mark.parametrize('P', [2, 4, 8])
