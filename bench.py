@@ -530,10 +530,11 @@ def multi_gpu(args):
         'vs_baseline': None,
         'dtype': 'f32',
         'data': 'synthetic N(0,1) fp32 bucket per rank, resident in HBM',
-        'config': {'workload': f'C3: allreduce (autotuned multi-ring or direct RS+AG over RCCL send/recv, '
-                               f'HIP reduce), fp32 '
+        'config': {'workload': f'C3: allreduce (autotuned RS+AG schedule over RCCL send/recv, HIP reduce; '
+                               f'sums in MPICH MPI_Allreduce order, bit-equal to the reference), fp32 '
                                f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
-                   'bucket_bytes': S, 'parallelism': f'dp{world}'},
+                   'bucket_bytes': S, 'parallelism': f'dp{world}',
+                   'reference_order': lib.ddl_get_config(b'reference_order')},
         'algbw_GiBs': round(algbw, 2),
         'busbw_GBs': round(busbw_gbs, 2),
         'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
@@ -561,9 +562,11 @@ def multi_gpu(args):
     state['leg'] = 'schedule_sweep'
     sweep = []
     if not args.no_config_sweep:
-        keys = ('algo', 'rings', 'slice_bytes', 'tune')
+        keys = ('algo', 'rings', 'slice_bytes', 'tune', 'reference_order')
         defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
         lib.ddl_set_config(b'tune', 0)
+        # each schedule as such (with reference_order a ring at P > 2 would run as direct)
+        lib.ddl_set_config(b'reference_order', 0)
         for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
                                        (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64)):
             if algo == 1 and world < 3:

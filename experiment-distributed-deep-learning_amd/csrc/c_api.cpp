@@ -255,6 +255,7 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
             c.fusion_pipeline_bytes = value;
         } else if (k == "one_rank_shortcut") c.one_rank_shortcut = value ? 1 : 0;
+        else if (k == "reference_order") c.reference_order = value ? 1 : 0;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
     });
@@ -275,6 +276,7 @@ long long ddl_get_config(const char *key) {
     if (k == "tune") return c.tune;
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
+    if (k == "reference_order") return c.reference_order;
     return -1;
 }
 
@@ -728,14 +730,16 @@ void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t
                 decode(tk.reduceN.b[i], &bbuf, &boff);
                 staged = staged && bbuf == 2;
             }
-            if (!staged) {
-                // general fold (one-shot): one row per input in fold order, input 0 = a:
-                // {tick, 5, inputs, i, source buffer, source offset, count, output offset}
+            if (!staged || tk.reduceN.order != kFoldLeft) {
+                // general fold (one-shot, reference order): one row per input in fold order,
+                // input 0 = a: {tick, 5 + order, inputs, i, source buffer, source offset, count,
+                // output offset}; kind 5 left fold, 6 MPICH's pre-fold + pairwise tree, 7 binomial
                 const int ni = tk.reduceN.nb + 1;
+                const long long kind = 5 + tk.reduceN.order;
                 for (int i = 0; i < ni; ++i) {
                     long long sbuf, soff;
                     decode(i == 0 ? tk.reduceN.a : tk.reduceN.b[i - 1], &sbuf, &soff);
-                    long long row[8] = {(long long)t, 5, ni, i, sbuf, soff, (long long)tk.reduceN.n, ooff};
+                    long long row[8] = {(long long)t, kind, ni, i, sbuf, soff, (long long)tk.reduceN.n, ooff};
                     rows.insert(rows.end(), row, row + 8);
                 }
                 continue;

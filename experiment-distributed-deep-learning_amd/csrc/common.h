@@ -97,18 +97,30 @@ struct SegTable {
     int count;
 };
 
-// One N-input problem: out = a + b[0] + b[1] + ... + b[nb-1] (left fold in that order); the
-// direct schedule's reduce of a rank's own chunk with the P-1 received copies.
+// One N-input problem over the inputs x_0 = a, x_1 = b[0], ..., x_nb = b[nb-1]: the direct and
+// one-shot schedules' reduce of a chunk with its P-1 received copies.
 constexpr int kMaxInputs = 15;
+// Addition order of an N-input fold (fp32 / fp64; integers wrap, so any order is the same):
+enum FoldOrder : int {
+    kFoldLeft = 0,      // ((x_0 + x_1) + x_2) + ...: the ring-0 order of the direct schedule
+    kFoldMpichTree = 1, // MPICH 3.3.2 MPI_Allreduce above 2048 bytes (x in rank order): the first
+                        // 2*rem inputs folded in pairs, then a pairwise tree over pof2 leaves
+    kFoldBinomial = 2,  // MPICH 3.3.2 MPI_Allreduce up to 2048 bytes: binomial tree over ranks
+};
+// MPICH's order for an allreduce of `message_bytes` (MPIR_CVAR_ALLREDUCE_SHORT_MSG_SIZE = 2048).
+inline int mpich_fold_order(size_t message_bytes) {
+    return message_bytes <= 2048 ? kFoldBinomial : kFoldMpichTree;
+}
 struct SegTableN {
     const void *a;
     const void *b[kMaxInputs];
     void *out;
     uint64_t n;
     int nb;
+    int order = kFoldLeft;  // FoldOrder
 };
-// fp32/fp64/int: one rounding per add (= the ring order's arithmetic); fp16/bf16: accumulate in
-// fp32 and round once at the end.
+// fp32/fp64/int: one rounding per add in `order`; fp16/bf16 (no reference order: the reference
+// rejects them): accumulate in fp32 and round once at the end, whatever the order.
 void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream);
 
 // Reduce-kernel cache-policy / staging flags (bit set). kVariantDefault is what the engine uses;

@@ -78,13 +78,16 @@ Communicator::~Communicator() {
     if (nccl_) (void)rccl().CommDestroy(nccl_);
 }
 
-void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream) {
+void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream,
+                             size_t order_bytes) {
     DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported (op " << op << ")");
     DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
     DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
-    exec_->allreduce(send, recv, n, dtype, stream, ring_config(n, dtype, stream));
+    RingConfig cfg = ring_config(n, dtype, stream);
+    cfg.order_bytes = order_bytes;
+    exec_->allreduce(send, recv, n, dtype, stream, cfg);
 }
 
 namespace {
@@ -97,14 +100,18 @@ namespace {
 
 // Candidate schedules for a P-rank communicator (the configured one first). Every rank builds
 // the same list: it depends on P, the bucket size and the shared config only.
+// With ref_order every candidate is the schedule that runs (effective_config: rings at P > 2
+// become direct), duplicates dropped, so only reference-exact schedules are timed.
 std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &base) {
-    std::vector<RingConfig> c{base};
+    std::vector<RingConfig> c{effective_config(base, P)};
     auto add = [&](int algo, int rings, size_t slice, int max_slices) {
         RingConfig r;
         r.algo = algo;
         r.rings = rings;
         r.slice_bytes = slice;
         r.max_slices = max_slices;
+        r.ref_order = base.ref_order;
+        r = effective_config(r, P);
         for (const RingConfig &x : c)
             if (x.algo == r.algo && x.rings == r.rings && x.slice_bytes == r.slice_bytes &&
                 x.max_slices == r.max_slices)
@@ -327,7 +334,8 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
             DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             ++made;
         }
-        const RingConfig cfg = ring_config(chunk / es, dtype, ring_);
+        RingConfig cfg = ring_config(chunk / es, dtype, ring_);
+        cfg.order_bytes = total;  // the reference reduces the whole host buffer in one call
         const size_t nchunks = (total + chunk - 1) / chunk;
         for (size_t i = 0; i < nchunks; ++i) {
             const int s = (int)(i % kHostSlots);

@@ -44,6 +44,10 @@ struct Config {
     // a one-rank world skips the keyed data plane (the sum is the input); 0 runs pack ->
     // allreduce -> unpack anyway (tests of the fusion path on one GPU)
     std::atomic<long long> one_rank_shortcut{1};
+    // 1: every sum equals the reference's MPI_Allreduce (MPICH 3.3.2) bit for bit — direct /
+    // one-shot folds in MPICH's order, the ring replaced by the direct schedule at P > 2
+    // (RingConfig::ref_order); 0: ring order / left folds (error-bounded against the reference)
+    std::atomic<long long> reference_order{1};
     // bumped by every ddl_set_config: tuned choices are dropped when the tunables change
     std::atomic<long long> epoch{0};
     RingConfig ring() const {
@@ -52,6 +56,7 @@ struct Config {
         c.rings = (int)rings.load();
         c.slice_bytes = (size_t)slice_bytes.load();
         c.max_slices = (int)max_slices.load();
+        c.ref_order = reference_order.load() ? 1 : 0;
         return c;
     }
 };
@@ -88,7 +93,10 @@ public:
     ncclComm_t nccl() const { return nccl_; }
 
     // Communicator::allreduce (reference Communicator.h:45-48), device buffers, stream-ordered.
-    void allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream);
+    // `order_bytes`: the size of the reference's MPI_Allreduce message this call is part of (a
+    // fused plan's bytes, the whole host buffer), which fixes MPICH's summation order; 0 = n.
+    void allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream,
+                   size_t order_bytes = 0);
     // Host-resident buckets (the reference's deployment case: framework CPU tensors behind the
     // MPI buffers): chunked pinned H2D -> device ring -> D2H pipeline; returns when recv holds
     // the result.

@@ -574,18 +574,23 @@ hipEvent_t RequestHandler::pipe_event_(size_t i) {
 //   stream_:         ar 0,   ar 1,     ar 2, ...               (ar j waits pack j)
 // so the pack of j+1 and the unpack of j-1 run under the allreduce of j. Buffer j%2 is reused
 // by pack j+2, issued on side_ after unpack j. Each sub-plan is an allreduce of its own (its
-// ring chunks follow the sub-plan), so fp sums are in a ring order of the sub-plan.
+// ring chunks follow the sub-plan); with reference_order each sub-plan folds in the order MPICH
+// uses for the whole plan's message, so the cut changes no bit.
 void RequestHandler::fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
                                       const std::vector<size_t> &bytes, int dt) {
     const size_t es = dtype_size(dt);
     const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
+    // the reference's MPI buffer holds the requests back to back (no padding): its byte count
+    // picks MPICH's summation order (reference_order)
+    size_t message = 0;
+    for (size_t b : bytes) message += b;
     size_t cap = (size_t)config().fusion_pipeline_bytes.load();
     cap &= ~size_t(255);
     if (cap == 0 || total <= cap) {
         ensure_(fusion_, fusion_bytes_, total);
         copier_.run(0, fusion_, const_cast<void *const *>(reinterpret_cast<const void *const *>(srcs.data())),
                     bytes.data(), (int)srcs.size(), stream_);
-        data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+        data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
         copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
         return;
     }
@@ -635,7 +640,7 @@ void RequestHandler::fused_allreduce_(const std::vector<const void *> &srcs, con
                     sb.bytes.data(), (int)sb.src.size(), side_);
         DDL_HIP(hipEventRecord(pipe_events_[1 + 2 * j], side_));
         DDL_HIP(hipStreamWaitEvent(stream_, pipe_events_[1 + 2 * j], 0));
-        data_->allreduce(buf[j % 2], buf[j % 2], sb.flat / es, dt, DDL_ALLREDUCE_OP_SUM, stream_);
+        data_->allreduce(buf[j % 2], buf[j % 2], sb.flat / es, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
         DDL_HIP(hipEventRecord(pipe_events_[2 + 2 * j], stream_));
         if (j >= 1) unpack(j - 1);
     }

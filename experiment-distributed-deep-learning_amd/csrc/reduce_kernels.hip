@@ -189,6 +189,36 @@ struct Acc<DDL_BFLOAT16> {
     __device__ static T add(T a, T b) { return a + b; }
 };
 
+// Sum of the K values w[0..K-1] (inputs in order x_0..x_{K-1}) in FoldOrder ORDER; every index
+// is a compile-time constant after unrolling. Half types always fold left in fp32 (one rounding
+// at the end), so ORDER only changes fp32 / fp64 (integers wrap: any order is the same sum).
+template <int DT, int K, int ORDER>
+__device__ __forceinline__ typename Acc<DT>::T fold_values(typename Acc<DT>::T *w) {
+    using A = Acc<DT>;
+    if constexpr (ORDER == kFoldBinomial) {
+#pragma unroll
+        for (int m = 1; m < K; m *= 2)
+#pragma unroll
+            for (int t = 0; t + m < K; t += 2 * m) w[t] = A::add(w[t], w[t + m]);
+        return w[0];
+    } else if constexpr (ORDER == kFoldMpichTree) {
+        constexpr int pof2 = K >= 16 ? 16 : K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
+        constexpr int rem = K - pof2;
+        typename A::T leaf[pof2];
+#pragma unroll
+        for (int t = 0; t < pof2; ++t) leaf[t] = t < rem ? A::add(w[2 * t], w[2 * t + 1]) : w[t + rem];
+#pragma unroll
+        for (int m = 1; m < pof2; m *= 2)
+#pragma unroll
+            for (int t = 0; t < pof2; t += 2 * m) leaf[t] = A::add(leaf[t], leaf[t + m]);
+        return leaf[0];
+    } else {
+#pragma unroll
+        for (int k = 1; k < K; ++k) w[0] = A::add(w[0], w[k]);
+        return w[0];
+    }
+}
+
 // Lanes per workgroup (one tile of THREADS x 16 B) of the two-input reduce (DDL_REDUCE_THREADS:
 // 64, 128 or 256; measurement). Default 128 (2 KiB tiles): 6.72-6.77 TB/s vs 6.37-6.55 with
 // 256 lanes on the N=1 bench (256 MiB fp32, 3 rotating sets, interleaved rounds).
@@ -219,7 +249,7 @@ int fold_variant() {
 // are in flight before the first add (a runtime "load or skip" per input makes hipcc wait
 // vmcnt(0) per input).
 constexpr int kFoldThreads = 128;
-template <int DT, int NB, int FV>
+template <int DT, int NB, int FV, int ORDER>
 __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
     constexpr uint64_t kTileVec = kFoldThreads;
     using A = Acc<DT>;
@@ -236,30 +266,46 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
             if (FV & 1) raw[k + 1] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.b[k]) + i);
             else raw[k + 1] = static_cast<const u32x4 *>(t.b[k])[i];
         }
-        const S *s0 = reinterpret_cast<const S *>(&raw[0]);
-        T acc[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) acc[e] = A::widen(s0[e]);
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            const S *sk = reinterpret_cast<const S *>(&raw[k + 1]);
-#pragma unroll
-            for (int e = 0; e < V; ++e) acc[e] = A::add(acc[e], A::widen(sk[e]));
-        }
         u32x4 res;
         S *rs = reinterpret_cast<S *>(&res);
 #pragma unroll
-        for (int e = 0; e < V; ++e) rs[e] = A::narrow(acc[e]);
+        for (int e = 0; e < V; ++e) {
+            T w[NB + 1];
+#pragma unroll
+            for (int k = 0; k <= NB; ++k) w[k] = A::widen(reinterpret_cast<const S *>(&raw[k])[e]);
+            rs[e] = A::narrow(fold_values<DT, NB + 1, ORDER>(w));
+        }
         if (FV & 2) __builtin_nontemporal_store(res, static_cast<u32x4 *>(t.out) + i);
         else static_cast<u32x4 *>(t.out)[i] = res;
     }
     const uint64_t rem = t.n - nv * V;
     if (rem && blockIdx.x == nv / kTileVec && threadIdx.x < rem) {
         const uint64_t e = nv * V + threadIdx.x;
-        T acc = A::widen(static_cast<const S *>(t.a)[e]);
-        for (int k = 0; k < NB; ++k) acc = A::add(acc, A::widen(static_cast<const S *>(t.b[k])[e]));
-        static_cast<S *>(t.out)[e] = A::narrow(acc);
+        T w[NB + 1];
+        w[0] = A::widen(static_cast<const S *>(t.a)[e]);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) w[k + 1] = A::widen(static_cast<const S *>(t.b[k])[e]);
+        static_cast<S *>(t.out)[e] = A::narrow(fold_values<DT, NB + 1, ORDER>(w));
     }
+}
+
+// Half types fold left in fp32 whatever the order: only kFoldLeft is instantiated for them.
+template <int DT>
+constexpr bool kHalfType = DT == DDL_HALF || DT == DDL_BFLOAT16;
+
+template <int DT, int NB, int FV>
+void launch_sumN_order(const SegTableN &t, hipStream_t stream, unsigned tiles) {
+    if constexpr (!kHalfType<DT>) {
+        if (t.order == kFoldMpichTree) {
+            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldMpichTree>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
+            return;
+        }
+        if (t.order == kFoldBinomial) {
+            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldBinomial>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldLeft>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
 }
 
 template <int DT, int NB>
@@ -268,29 +314,52 @@ void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
     } else {
         if (t.nb == NB) {
-            switch (fold_variant()) {
-                case 1: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 1>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
-                case 2: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 2>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
-                case 3: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 3>), dim3(tiles), dim3(kFoldThreads), 0, stream, t); break;
-                default: hipLaunchKernelGGL((k_sumN_tile<DT, NB, 0>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
-            }
+            // cache policy (fold_variant): 3 = every operand non-temporal, measured fastest;
+            // 0 = plain, kept for comparison
+            if (fold_variant() == 0) launch_sumN_order<DT, NB, 0>(t, stream, tiles);
+            else launch_sumN_order<DT, NB, 3>(t, stream, tiles);
         } else {
             launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
         }
     }
 }
 
-// Misaligned buffers for the N-input fold: element-granular grid-stride.
-template <int DT>
+// Misaligned buffers for the N-input fold: element-granular grid-stride, in the same order.
+template <int DT, int NB, int ORDER>
 __global__ void __launch_bounds__(kThreads) k_sumN_scalar(SegTableN t) {
     using A = Acc<DT>;
     using S = typename Add<DT>::S;
     using T = typename A::T;
     const uint64_t stride = (uint64_t)gridDim.x * kThreads;
     for (uint64_t e = (uint64_t)blockIdx.x * kThreads + threadIdx.x; e < t.n; e += stride) {
-        T acc = A::widen(static_cast<const S *>(t.a)[e]);
-        for (int k = 0; k < t.nb; ++k) acc = A::add(acc, A::widen(static_cast<const S *>(t.b[k])[e]));
-        static_cast<S *>(t.out)[e] = A::narrow(acc);
+        T w[NB + 1];
+        w[0] = A::widen(static_cast<const S *>(t.a)[e]);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) w[k + 1] = A::widen(static_cast<const S *>(t.b[k])[e]);
+        static_cast<S *>(t.out)[e] = A::narrow(fold_values<DT, NB + 1, ORDER>(w));
+    }
+}
+
+template <int DT, int NB>
+void launch_sumN_scalar_nb(const SegTableN &t, hipStream_t stream, unsigned blocks) {
+    if constexpr (NB > kMaxInputs) {
+        fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
+    } else {
+        if (t.nb != NB) {
+            launch_sumN_scalar_nb<DT, NB + 1>(t, stream, blocks);
+            return;
+        }
+        if constexpr (!kHalfType<DT>) {
+            if (t.order == kFoldMpichTree) {
+                hipLaunchKernelGGL((k_sumN_scalar<DT, NB, kFoldMpichTree>), dim3(blocks), dim3(kThreads), 0, stream, t);
+                return;
+            }
+            if (t.order == kFoldBinomial) {
+                hipLaunchKernelGGL((k_sumN_scalar<DT, NB, kFoldBinomial>), dim3(blocks), dim3(kThreads), 0, stream, t);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((k_sumN_scalar<DT, NB, kFoldLeft>), dim3(blocks), dim3(kThreads), 0, stream, t);
     }
 }
 
@@ -370,7 +439,7 @@ void launch_sumN_dt(const SegTableN &t, hipStream_t stream) {
         uint64_t blocks = (t.n + kThreads * 4 - 1) / (kThreads * 4);
         const uint64_t cap = (uint64_t)device_cu_count() * 8;
         blocks = blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
-        hipLaunchKernelGGL(k_sumN_scalar<DT>, dim3((unsigned)blocks), dim3(kThreads), 0, stream, t);
+        launch_sumN_scalar_nb<DT, 1>(t, stream, (unsigned)blocks);
         return;
     }
     const uint64_t tiles = (t.n / V + kFoldThreads) / kFoldThreads;
@@ -381,6 +450,7 @@ void launch_sumN_dt(const SegTableN &t, hipStream_t stream) {
 
 void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) {
     DDL_REQUIRE(t.nb >= 1 && t.nb <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "reduce inputs " << t.nb);
+    DDL_REQUIRE(t.order >= kFoldLeft && t.order <= kFoldBinomial, DDL_STATUS_INVALID_ARGUMENT, "fold order " << t.order);
     if (t.n == 0) return;
     DDL_REQUIRE(t.a && t.out, DDL_STATUS_INVALID_ARGUMENT, "null reduce buffer");
     for (int k = 0; k < t.nb; ++k) DDL_REQUIRE(t.b[k], DDL_STATUS_INVALID_ARGUMENT, "null reduce input " << k);

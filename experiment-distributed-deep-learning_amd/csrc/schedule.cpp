@@ -141,8 +141,9 @@ Range slice_range(const Range &chunk, size_t esize, int K, int k) {
     return r;
 }
 
-void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
+void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg_in, int *R, int *K,
                 size_t *staging_stride) {
+    const RingConfig cfg = effective_config(cfg_in, P);
     if (cfg.algo == kAlgoOneShot) {  // one tick, whole bucket per peer
         *R = 1;
         *K = 1;
@@ -171,7 +172,8 @@ void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, in
     *staging_stride = (max_chunk + 63) & ~size_t(63);
 }
 
-size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cfg) {
+size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cfg_in) {
+    const RingConfig cfg = effective_config(cfg_in, P);
     int R, K;
     size_t stride;
     ring_shape(n, esize, P, cfg, &R, &K, &stride);
@@ -183,11 +185,12 @@ namespace {
 
 // Direct reduce-scatter / allgather on a fully connected mesh. Chunk c (of P) is reduced by rank
 // c. RS tick k: send slice k of chunk q to every peer q, receive slice k of my chunk from every
-// peer into its staging slot; then one N-input fold out = in + x_{me+1} + x_{me+2} + ... (the
-// ring's left-fold order for ring 0). AG tick k (waits the fold of slice k): send my reduced
-// slice to every peer, receive theirs straight into out.
+// peer into its staging slot; then one N-input fold: kFoldLeft out = in + x_{me+1} + x_{me+2}
+// + ... (the ring's left-fold order for ring 0); the reference orders fold x_0, ..., x_{P-1} in
+// rank order (x_me = in) in MPICH's tree. AG tick k (waits the fold of slice k): send my
+// reduced slice to every peer, receive theirs straight into out.
 void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
-                  size_t es) {
+                  size_t es, int order) {
     const int K = prog.K;
     DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "direct schedule supports up to "
                                                                        << kMaxInputs + 1 << " ranks");
@@ -216,8 +219,18 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
             t.reduceN.out = outb + ms.begin * es;
             t.reduceN.n = ms.size();
             t.reduceN.nb = P - 1;
-            for (int s = 0; s < P - 1; ++s)
-                t.reduceN.b[s] = stb + ((size_t)s * prog.staging_stride + (ms.begin - mine.begin)) * es;
+            t.reduceN.order = order;
+            auto slot = [&](int s) -> const void * {
+                return stb + ((size_t)s * prog.staging_stride + (ms.begin - mine.begin)) * es;
+            };
+            if (order == kFoldLeft) {
+                for (int s = 0; s < P - 1; ++s) t.reduceN.b[s] = slot(s);
+            } else {  // rank order: x_q is `in` for q == me, else the slot of sender q
+                const void *own = t.reduceN.a;
+                auto x = [&](int q) { return q == rank ? own : slot((q - rank + P) % P - 1); };
+                t.reduceN.a = x(0);
+                for (int q = 1; q < P; ++q) t.reduceN.b[q - 1] = x(q);
+            }
         }
         prog.ticks.push_back(std::move(t));
     }
@@ -239,12 +252,13 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
 
 // One-shot allreduce for latency-bound buckets: tick 0 sends the whole input to every peer and
 // receives every peer's whole input into staging slot (peer - me - 1) mod P, then folds the P
-// inputs in rank order 0, 1, ..., P-1 (in for me, a slot otherwise), so every rank computes the
-// same sum bit for bit (fp16/bf16 accumulated in fp32, rounded once). Tick 1 only waits for the
+// inputs in rank order 0, 1, ..., P-1 (in for me, a slot otherwise) — left to right, or in
+// MPICH's tree with `order` — so every rank computes the same sum bit for bit (fp16/bf16
+// accumulated in fp32, rounded once). Tick 1 only waits for the
 // fold, so the comm stream's tail covers it (the executor joins the caller on the comm stream).
 // In place is safe: the fold runs after the group, i.e. after every send has read `in`.
 void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
-                   size_t es) {
+                   size_t es, int order) {
     DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "one-shot schedule supports up to "
                                                                        << kMaxInputs + 1 << " ranks");
     auto slot = [&](int q) { return stb + (size_t)((q - rank + P) % P - 1) * prog.staging_stride * es; };
@@ -261,6 +275,7 @@ void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *ou
     t.reduceN.out = outb;
     t.reduceN.n = n;
     t.reduceN.nb = P - 1;
+    t.reduceN.order = order;
     for (int q = 1; q < P; ++q) t.reduceN.b[q - 1] = q == rank ? static_cast<const void *>(inb) : slot(q);
     prog.ticks.push_back(std::move(t));
     Tick join;
@@ -272,7 +287,8 @@ void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *ou
 }  // namespace
 
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
-                   size_t n, int dtype, const RingConfig &cfg) {
+                   size_t n, int dtype, const RingConfig &cfg_in) {
+    const RingConfig cfg = effective_config(cfg_in, P);
     const size_t es = dtype_size(dtype);
     prog.P = P;
     prog.rank = rank;
@@ -283,14 +299,16 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
     prog.staging_slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)prog.R;
     if (P <= 1 || n == 0) return;
+    // fold order of the direct / one-shot N-input reduce (kFoldLeft: ring 0's order)
+    const int order = cfg.ref_order ? mpich_fold_order(cfg.order_bytes ? cfg.order_bytes : n * es) : kFoldLeft;
     if (cfg.algo == kAlgoOneShot) {
         build_oneshot(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
-                      static_cast<char *>(staging), n, es);
+                      static_cast<char *>(staging), n, es, order);
         return;
     }
     if (cfg.algo == kAlgoDirect) {
         build_direct(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
-                     static_cast<char *>(staging), n, es);
+                     static_cast<char *>(staging), n, es, order);
         return;
     }
     const int R = prog.R, K = prog.K;

@@ -75,7 +75,24 @@ struct RingConfig {
     int rings = kMaxRings;            // upper bound; clipped to what the topology allows
     size_t slice_bytes = 2u << 20;    // target bytes per reduce-scatter message
     int max_slices = 8;
+    // Reference order: the sum of every element equals the reference's MPI_Allreduce (MPICH
+    // 3.3.2) bit for bit. Direct and one-shot fold the P inputs in rank order in MPICH's tree
+    // (FoldOrder kFoldMpichTree / kFoldBinomial, picked by the message size); the ring, whose
+    // order cannot follow it at P > 2, runs as the direct schedule there (effective_config).
+    // 0: direct folds left in ring 0's order, the ring runs as configured.
+    int ref_order = 0;
+    size_t order_bytes = 0;  // message size that picks MPICH's algorithm (0 = this bucket's)
 };
+
+// The schedule that actually runs for P ranks: with ref_order, a ring at P > 2 becomes the
+// direct schedule with the same slicing. Every builder and shape query goes through it.
+inline RingConfig effective_config(RingConfig c, int P) {
+    if (c.ref_order && c.algo == kAlgoRing && P > 2) {
+        c.algo = kAlgoDirect;
+        c.rings = 1;
+    }
+    return c;
+}
 
 // Per-rank tick list of one allreduce. `staging` must hold staging_elems(R, stride) elements:
 // two slots per ring (reduce-scatter step parity), ring j / parity q at (2j + q) * stride.

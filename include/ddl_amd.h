@@ -133,7 +133,11 @@ int ddl_is_initialized(void);
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
- * one-rank world skips the keyed data plane; 0: runs it, for tests).
+ * one-rank world skips the keyed data plane; 0: runs it, for tests), "reference_order" (1,
+ * default: every allreduce sum equals the reference's MPI_Allreduce — MPICH 3.3.2 — bit for
+ * bit: the direct and one-shot folds add the P inputs in rank order in MPICH's tree, picked by
+ * the message size, and "algo" 0 runs as the direct schedule at P > 2; 0: ring order and left
+ * folds, within (P-1)·u·Σ|x| of the reference).
  * With "tune" = 1 (default) a communicator of P > 1 ranks picks the schedule (algo, rings,
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.

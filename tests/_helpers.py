@@ -262,7 +262,7 @@ def simulate_ring(oracle, lib, dt, xs):
                 st_size = max(st_size, int(row[5] + row[6]))
             elif row[1] in (2, 3):
                 st_size = max(st_size, int(row[7] + row[6]))
-            elif row[1] == 5 and row[4] == 2:
+            elif row[1] in GENERAL_FOLDS and row[4] == 2:
                 st_size = max(st_size, int(row[5] + row[6]))
     bufs = [[x.copy(), np.zeros_like(x), np.zeros(st_size, dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
@@ -289,18 +289,32 @@ def simulate_ring(oracle, lib, dt, xs):
                     _, _, _, _, b, off, cnt, soff = row
                     bufs[r][1][off:off + cnt] = oracle.sum2(dt, bufs[r][0][off:off + cnt],
                                                             bufs[r][2][soff:soff + cnt])
-            folds = rows[rows[:, 1] == 3]
-            if len(folds):
-                nb = int(folds[0, 2])
-                assert len(folds) == nb and list(folds[:, 3]) == list(range(nb))
-                off, cnt = int(folds[0, 5]), int(folds[0, 6])
-                ins = [bufs[r][0][off:off + cnt]] + [bufs[r][2][s:s + cnt] for s in folds[:, 7]]
-                bufs[r][1][off:off + cnt] = oracle.fold(dt, ins)
-            gen = rows[rows[:, 1] == 5]  # general fold (one-shot): every input named
-            if len(gen):
-                ni = int(gen[0, 2])
-                assert len(gen) == ni and list(gen[:, 3]) == list(range(ni))
-                cnt, off = int(gen[0, 6]), int(gen[0, 7])
-                ins = [bufs[r][int(b)][int(s):int(s) + cnt].copy() for b, s in zip(gen[:, 4], gen[:, 5])]
-                bufs[r][1][off:off + cnt] = oracle.fold(dt, ins)
+            apply_folds(oracle, dt, rows, bufs[r])
     return [b[1] for b in bufs]
+
+
+# General N-input fold rows of a program dump: kind -> oracle total_bytes argument (None: left
+# fold). 5 = left fold, 6 = MPICH's pre-fold + pairwise tree (> 2048-byte messages), 7 = MPICH's
+# binomial tree (<= 2048 bytes).
+GENERAL_FOLDS = {5: None, 6: 4096, 7: 0}
+
+
+def apply_folds(oracle, dt, rows, bufs):
+    """Run one tick's N-input folds of one rank (rows of that tick) on bufs = [in, out, staging]:
+    kind 3 (in + staged inputs, left fold) and the general kinds 5/6/7 (every input named)."""
+    folds = rows[rows[:, 1] == 3]
+    if len(folds):
+        nb = int(folds[0, 2])
+        assert len(folds) == nb and list(folds[:, 3]) == list(range(nb))
+        off, cnt = int(folds[0, 5]), int(folds[0, 6])
+        ins = [bufs[0][off:off + cnt]] + [bufs[2][s:s + cnt] for s in folds[:, 7]]
+        bufs[1][off:off + cnt] = oracle.fold(dt, ins)
+    for kind, tb in GENERAL_FOLDS.items():
+        gen = rows[rows[:, 1] == kind]
+        if not len(gen):
+            continue
+        ni = int(gen[0, 2])
+        assert len(gen) == ni and list(gen[:, 3]) == list(range(ni))
+        cnt, off = int(gen[0, 6]), int(gen[0, 7])
+        ins = [bufs[int(b)][int(s):int(s) + cnt].copy() for b, s in zip(gen[:, 4], gen[:, 5])]
+        bufs[1][off:off + cnt] = oracle.fold(dt, ins) if tb is None else oracle.fold_ref_order(dt, ins, tb)

@@ -44,17 +44,22 @@ def check_reference_known_answers(ctx):
 
 def check_schedules_vs_oracle(ctx):
     """ddl_allreduce with each schedule fixed (tuner off): every rank equals the oracle's
-    summation in that schedule's order, bit for bit, in and out of place, all dtypes."""
+    summation in that schedule's order, bit for bit, in and out of place, all dtypes — with
+    reference_order 1 (default) MPICH's own order whatever the schedule, with 0 the ring /
+    left-fold orders."""
     import _helpers as h
     torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
     s = torch.cuda.current_stream().cuda_stream
+    cases = [(algo, ref) for ref in (1, 0) for algo in (0, 1, 2)]
     with h.config(lib, tune=0, slice_bytes=64 << 10):
-        for algo in (0, 1, 2):
-            with h.config(lib, algo=algo):
+        for algo, ref in cases:
+            with h.config(lib, algo=algo, reference_order=ref):
                 for dt in (h.DT_FLOAT, h.DT_HALF, h.DT_INT32, h.DT_BFLOAT16, h.DT_DOUBLE):
-                    for n in (1, 4099, 300_001):
+                    for n in ((1, 300, 4099, 300_001) if ref else (1, 4099, 300_001)):
                         xs = [h.random_input(dt, n, 100 * algo + 7 * dt + 13 * q + n) for q in range(P)]
-                        if algo == 0:
+                        if ref:
+                            want = ora.fold_ref_order(dt, xs)
+                        elif algo == 0:
                             R, _ = h.ring_shape(lib, n, dt, P)
                             want = ora.allreduce_ring(dt, xs, h.ring_perms(lib, P, R))
                         elif algo == 1:
@@ -67,7 +72,7 @@ def check_schedules_vs_oracle(ctx):
                             st = lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), n, dt, 0, s)
                             assert st == 0, lib.ddl_last_error()
                             got = _host(b, xs[r])
-                            assert got.tobytes() == want.tobytes(), (algo, dt, n, in_place)
+                            assert got.tobytes() == want.tobytes(), (algo, ref, dt, n, in_place)
 
 
 def check_tuned_exact(ctx):
@@ -121,6 +126,27 @@ def check_keyed_fusion(ctx):
     sr, cr = ctypes.c_longlong(), ctypes.c_longlong()
     assert lib.ddl_control_stats(ctypes.byref(sr), ctypes.byref(cr)) == 0
     assert cr.value >= 1  # the repeated key set went by id-table index
+
+
+def check_keyed_reference_order(ctx):
+    """Random fp32 / fp64 gradients (not exactly summable) through the keyed path — negotiated,
+    fused per dtype into one plan, pipelined over 256 KiB sub-plans: every element equals
+    MPICH's order for the plan's message (ddlo_fold_ref_order with the group's bytes), bit for
+    bit, on every rank (reference_order default)."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    sizes = [5, 300, 70_001, 4099, 1, 200_000, 513]
+    dts = [h.DT_FLOAT if i % 2 == 0 else h.DT_DOUBLE for i in range(len(sizes))]
+    xs = [[h.random_input(dts[i], n, 500 + 31 * i + q) for q in range(P)] for i, n in enumerate(sizes)]
+    group_bytes = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
+    with h.config(lib, fusion_pipeline_bytes=256 << 10, reference_order=1):
+        ts = [torch.from_numpy(xs[i][r]).cuda() for i in range(len(sizes))]
+        hs = allreduce_async_batch(ts, [f'ro_{i:02d}' for i in range(len(sizes))], comm)
+        for i, hd in enumerate(hs):
+            got = hd.wait(timeout=120).cpu().numpy()
+            want = ora.fold_ref_order(dts[i], xs[i], group_bytes[dts[i]])
+            assert got.tobytes() == want.tobytes(), (i, sizes[i])
 
 
 def check_keyed_broadcast_allgather(ctx):
@@ -206,7 +232,7 @@ def check_dp_training(ctx):
 
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
-          check_keyed_broadcast_allgather, check_host_resident, check_dp_training]
+          check_keyed_reference_order, check_keyed_broadcast_allgather, check_host_resident, check_dp_training]
 
 
 def worker(rank, world, port, q):

@@ -58,6 +58,8 @@ def test_config_roundtrip(lib):
     assert lib.ddl_set_config(b'slice_bytes', old) == 0
     assert lib.ddl_set_config(b'no_such_key', 1) == 3
     assert lib.ddl_set_config(b'fusion_threshold_bytes', 0) == 3
+    # the product default: sums bit-equal to the reference's MPI_Allreduce
+    assert lib.ddl_get_config(b'reference_order') == 1
 
 
 def test_product_does_not_reference_oracle():

@@ -37,7 +37,7 @@ def _setup_paths():
             sys.path.insert(0, p)
 
 
-def _ring_worker(rank, world, port, dt, n, algo, q):
+def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
     try:
         _setup_paths()
         import _helpers as h
@@ -45,13 +45,14 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
         lib = CPPBackend.c_api()
         ora = h.Oracle()
         assert lib.ddl_set_config(b'algo', algo) == 0
+        assert lib.ddl_set_config(b'reference_order', ref_order) == 0
         dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
         xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
         prog = h.ring_program(lib, rank, world, n, dt)
         R, _ = h.ring_shape(lib, n, dt, world)
         st = 1
         for row in prog:
-            if row[1] <= 1 and row[4] == 2 or row[1] == 5 and row[4] == 2:
+            if row[1] <= 1 and row[4] == 2 or row[1] in h.GENERAL_FOLDS and row[4] == 2:
                 st = max(st, int(row[5] + row[6]))
             elif row[1] in (2, 3):
                 st = max(st, int(row[7] + row[6]))
@@ -71,18 +72,12 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
             for row in rows[rows[:, 1] == 2]:
                 _, _, _, _, b, off, cnt, soff = row
                 bufs[1][off:off + cnt] = ora.sum2(dt, bufs[0][off:off + cnt], bufs[2][soff:soff + cnt])
-            folds = rows[rows[:, 1] == 3]
-            if len(folds):
-                off, cnt = int(folds[0, 5]), int(folds[0, 6])
-                ins = [bufs[0][off:off + cnt]] + [bufs[2][o:o + cnt] for o in folds[:, 7]]
-                bufs[1][off:off + cnt] = ora.fold(dt, ins)
-            gen = rows[rows[:, 1] == 5]  # one-shot fold: every input named (buffer, offset)
-            if len(gen):
-                cnt, off = int(gen[0, 6]), int(gen[0, 7])
-                ins = [bufs[int(b)][int(o):int(o) + cnt].copy() for b, o in zip(gen[:, 4], gen[:, 5])]
-                bufs[1][off:off + cnt] = ora.fold(dt, ins)
-        want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo == 2 else
-                ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
+            h.apply_folds(ora, dt, rows, bufs)
+        if ref_order and (algo != 0 or world > 2):  # MPICH's own order (a P = 2 ring is exact)
+            want = ora.fold_ref_order(dt, xs)
+        else:
+            want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo == 2 else
+                    ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
         ok = bufs[1].tobytes() == want.tobytes()
         dist.destroy_process_group()
         q.put((rank, ok, ''))
@@ -94,10 +89,25 @@ def _ring_worker(rank, world, port, dt, n, algo, q):
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('dt,n', [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)])
 def test_ring_program_over_gloo(world, dt, n, algo):
+    """reference_order 0: the ring / left-fold orders."""
+    _run_ring_workers(world, dt, n, algo, 0)
+
+
+@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('dt,n', [(1, 50_000), (1, 300), (2, 4099)])
+def test_reference_order_program_over_gloo(world, dt, n, algo):
+    """reference_order 1 (the default): every rank ends with MPICH's own order (binomial tree at
+    <= 2048 bytes, the pre-fold + pairwise tree above), whichever schedule is asked for."""
+    _run_ring_workers(world, dt, n, algo, 1)
+
+
+def _run_ring_workers(world, dt, n, algo, ref_order):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, dt, n, algo, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, dt, n, algo, ref_order, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]

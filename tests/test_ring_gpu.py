@@ -2,9 +2,12 @@
 programs with HIP streams/events and the reduce kernel, device-to-device copies standing in for
 RCCL send/recv (ddl_local_ring_allreduce). Checked against the oracle:
   * ring-order restatement: bit-exact for every dtype and P;
-  * MPICH golden vectors: bit-exact where order-free (ints, P=2, exactly summable fp32),
-    within the summation bound otherwise;
+  * MPICH golden vectors: with reference_order (the default) bit-exact on every case; the ring
+    order itself bit-exact where order-free (ints, P=2, exactly summable fp32), within the
+    summation bound otherwise;
   * full-size (256 MiB fp32, C3 shape) through size-independent properties.
+Tests of the ring / left-fold orders run with reference_order 0 (autouse fixture); the
+reference-order tests opt back in.
 """
 import ctypes
 import json
@@ -19,6 +22,12 @@ from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, FROM_NP, NAME, config, rand
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(autouse=True)
+def _schedules_as_configured(lib):
+    with config(lib, reference_order=0):
+        yield
 
 
 def run_local(lib, dev, xs, in_place=False, stream=None):
@@ -75,11 +84,16 @@ def test_local_ring_in_place(lib, oracle, gpu, P):
         assert o.tobytes() == want.tobytes()
 
 
-def test_local_ring_vs_mpich_golden(lib, gpu):
+def _golden():
     gold = np.load(os.path.join(HERE, 'golden', 'golden_mpich.npz'), allow_pickle=False)
     meta = json.load(open(os.path.join(HERE, 'golden', 'golden_manifest.json')))['cases']
-    for case, m in meta.items():
-        xs, y = gold[case + '__inputs'], gold[case + '__output']
+    return [(case, m, gold[case + '__inputs'], gold[case + '__output']) for case, m in meta.items()]
+
+
+def test_local_ring_vs_mpich_golden(lib, gpu):
+    """Ring order (reference_order 0) against MPICH's outputs: exact where order-free, else
+    within the bound between two summation orders, 2 (P-1) u sum|x|."""
+    for case, m, xs, y in _golden():
         outs = run_local(lib, gpu, list(xs))
         exact = np.issubdtype(xs.dtype, np.integer) or m['P'] == 2 or m['kind'] != 'randn'
         for o in outs:
@@ -87,8 +101,70 @@ def test_local_ring_vs_mpich_golden(lib, gpu):
                 assert o.tobytes() == y.tobytes(), case
             else:
                 u = np.finfo(xs.dtype).eps / 2
-                bound = (m['P'] - 1) * u * np.abs(xs.astype(np.float64)).sum(0) * 1.0001
+                bound = 2 * (m['P'] - 1) * u * np.abs(xs.astype(np.float64)).sum(0) * 1.0001
                 assert np.all(np.abs(o.astype(np.float64) - y.astype(np.float64)) <= bound), case
+
+
+@pytest.mark.parametrize('algo', [0, 1, 2])
+def test_reference_order_equals_mpich_golden_bit_for_bit(lib, gpu, algo):
+    """The product default (reference_order 1): every golden case — MPICH 3.3.2's own
+    MPI_Allreduce outputs at P = 2..8, fp32 / fp64 / integers, both sides of its 2048-byte
+    algorithm switch — comes out of the GPU bit for bit on every rank, whichever schedule is
+    asked for (a ring at P > 2 runs as the direct schedule; one-shot beyond its tuning range
+    still works)."""
+    with config(lib, algo=algo, reference_order=1, slice_bytes=64 << 10):
+        for case, m, xs, y in _golden():
+            for o in run_local(lib, gpu, list(xs)):
+                assert o.tobytes() == y.tobytes(), case
+
+
+@pytest.mark.parametrize('algo', [1, 2])
+@pytest.mark.parametrize('P', [3, 5, 6, 7, 8])
+@pytest.mark.parametrize('dt', [1, 2, 3], ids=lambda d: NAME[d])
+@pytest.mark.parametrize('n', [1, 300, 512, 513, 65_537, 1_000_003])
+@pytest.mark.parametrize('in_place', [False, True])
+def test_reference_order_matches_oracle(lib, oracle, gpu, algo, P, dt, n, in_place):
+    """The ordered fold kernels (binomial, pre-fold + pairwise tree) through the direct and
+    one-shot programs vs the oracle's MPICH-order restatement, in and out of place, ragged."""
+    xs = [random_input(dt, n, 61 + 5 * r) for r in range(P)]
+    with config(lib, algo=algo, reference_order=1, slice_bytes=256 << 10):
+        outs = run_local(lib, gpu, xs, in_place=in_place)
+    want = oracle.fold_ref_order(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_reference_order_misaligned_fold(lib, oracle, gpu):
+    """The element-granular ordered fold (inputs not 16-byte aligned) at P = 5, both orders."""
+    P = 5
+    for n in (301, 100_003):
+        xs = [random_input(1, n + 1, 3 + r) for r in range(P)]
+        ins = [torch.from_numpy(x).to(gpu)[1:] for x in xs]
+        outs = [torch.empty(n + 1, dtype=torch.float32, device=gpu)[1:] for _ in range(P)]
+        send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+        recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+        with config(lib, algo=1, reference_order=1):
+            assert lib.ddl_local_ring_allreduce(P, send, recv, n, 1, 0, torch.cuda.current_stream().cuda_stream) == 0
+            torch.cuda.synchronize()
+        want = oracle.fold_ref_order(1, [x[1:] for x in xs])
+        for o in outs:
+            assert o.cpu().numpy().tobytes() == want.tobytes(), n
+
+
+@pytest.mark.parametrize('P', [4, 8])
+def test_reference_order_tuner_times_only_exact_schedules(lib, gpu, P):
+    """With reference_order the autotuner's candidates are direct / one-shot schedules only at
+    P > 2 (the configured ring becomes direct), deduplicated."""
+    chosen, count = ctypes.c_int(), ctypes.c_int()
+    cfgs = (ctypes.c_longlong * 64)()
+    ms = (ctypes.c_float * 16)()
+    with config(lib, reference_order=1, algo=0):
+        st = lib.ddl_local_tune(P, 64 << 10, DT_FLOAT, torch.cuda.current_stream().cuda_stream,
+                                ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
+    assert st == 0, lib.ddl_last_error()
+    c = [tuple(cfgs[4 * i:4 * i + 4]) for i in range(count.value)]
+    assert {x[0] for x in c} == {1, 2} and len(set(c)) == len(c)
+    assert c[0][0] == 1
 
 
 @pytest.mark.parametrize('P', [2, 4, 8])

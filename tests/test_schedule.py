@@ -5,10 +5,18 @@ import itertools
 import numpy as np
 import pytest
 
-from _helpers import (ALL_DTYPES, DT_BFLOAT16, DT_FLOAT, DT_HALF, DT_INT32, config, NP, random_input, ring_perms, ring_program,
-                      ring_shape, simulate_ring)
+from _helpers import (ALL_DTYPES, DT_BFLOAT16, DT_FLOAT, DT_HALF, DT_INT32, GENERAL_FOLDS, config, NP, random_input,
+                      ring_perms, ring_program, ring_shape, simulate_ring)
 
 SZ_OF = {1: 4, 2: 8, 3: 4, 9: 8, 14: 2, 19: 2, 23: 8}
+
+
+@pytest.fixture(autouse=True)
+def _schedules_as_configured(lib):
+    """Most tests here check the ring and the left-fold direct / one-shot schedules as built
+    (reference_order 0); the reference-order tests opt back in."""
+    with config(lib, reference_order=0):
+        yield
 
 
 @pytest.mark.parametrize('P', range(1, 9))
@@ -106,22 +114,22 @@ def _overlap(a0, a1, b0, b1):
     return a0 < b1 and b0 < a1
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo,ref_order', [(0, 0), (1, 0), (2, 0), (1, 1), (2, 1)])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
 @pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
-def test_schedule_has_no_stream_races(lib, algo, P, n, slice_bytes):
+def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
     """Comm tick T runs after the reduce it waits on (W) and every earlier reduce (the compute
     stream is in order), but concurrently with the reduces of ticks W+1..T-1. None of T's
     sends/recvs may touch a buffer range those reduces read or write — with in and out treated
     as one buffer, since in-place allreduce (in == out) is allowed."""
-    with config(lib, slice_bytes=slice_bytes, algo=algo):
+    with config(lib, slice_bytes=slice_bytes, algo=algo, reference_order=ref_order):
         for rank in range(P):
             prog = ring_program(lib, rank, P, n, DT_FLOAT)
             red = {}
             for row in prog[(prog[:, 1] == 2) | (prog[:, 1] == 3)]:
                 red.setdefault(int(row[0]), []).append(row)
-            for row in prog[prog[:, 1] == 5]:  # general fold: reads (buf, off), writes out
+            for row in prog[np.isin(prog[:, 1], list(GENERAL_FOLDS))]:  # general fold: reads (buf, off), writes out
                 t_, _, _, _, sb, so, c_, oo = row
                 red.setdefault(int(t_), []).append(('gen', int(sb), int(so), int(c_), int(oo)))
             w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
@@ -268,5 +276,43 @@ def test_oneshot_program_shape(lib):
             ops = prog[prog[:, 1] <= 1]
             assert set(ops[:, 0]) == {0} and len(ops) == 2 * (P - 1) and set(ops[:, 6]) == {n}
             assert sorted(ops[ops[:, 1] == 0][:, 2]) == sorted(set(range(P)) - {rank})
-            folds = prog[(prog[:, 1] == 3) | (prog[:, 1] == 5)]
+            folds = prog[(prog[:, 1] == 3) | np.isin(prog[:, 1], list(GENERAL_FOLDS))]
             assert set(folds[:, 0]) == {0}
+
+
+# ---- reference order (reference_order = 1, the default) ----------------------------------------
+@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize('n', [1, 100, 512, 513, 4099, 50_000])
+@pytest.mark.parametrize('dt', ALL_DTYPES)
+def test_reference_order_programs_compute_mpich_order(lib, oracle, algo, P, n, dt):
+    """With reference_order every schedule's programs, executed with matched sends/recvs, give
+    MPICH 3.3.2's own MPI_Allreduce order on every rank, bit for bit: the oracle's
+    ddlo_fold_ref_order (pinned to MPICH runs by test_oracle_golden), binomial tree for
+    messages <= 2048 bytes and pre-fold + pairwise tree above. A ring at P > 2 runs as the direct
+    schedule; a P = 2 ring is order-free. fp16 / bf16 (rejected by the reference) fold in rank
+    order in fp32."""
+    xs = [random_input(dt, n, 11 + 29 * r) for r in range(P)]
+    with config(lib, algo=algo, reference_order=1):
+        outs = simulate_ring(oracle, lib, dt, xs)
+    want = oracle.fold_ref_order(dt, xs)
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_reference_order_program_kinds(lib):
+    """The fold rows name MPICH's algorithm by the message size: kind 7 (binomial) up to 2048
+    bytes, kind 6 (pre-fold + pairwise tree) above; a ring asked for at P > 2 is the direct
+    schedule (R = 1, 2K ticks); at P = 2 it stays the ring."""
+    with config(lib, algo=0, reference_order=1):
+        assert ring_shape(lib, 1 << 20, DT_FLOAT, 8)[0] == 1
+        assert ring_shape(lib, 1 << 20, DT_FLOAT, 2)[0] == 1
+        for n, kind in ((512, 7), (513, 6), (1 << 20, 6)):
+            prog = ring_program(lib, 3, 5, n, DT_FLOAT)
+            assert set(prog[prog[:, 1] >= 3][:, 1]) == {kind}, n
+            assert set(prog[prog[:, 1] >= 3][:, 2]) == {5}  # every input named, rank order
+        prog = ring_program(lib, 0, 2, 1 << 20, DT_FLOAT)
+        assert set(prog[:, 1]) <= {0, 1, 2}  # ring: two-input reduces only
+    with config(lib, algo=2, reference_order=1):
+        prog = ring_program(lib, 2, 5, 300, DT_FLOAT)
+        assert set(prog[prog[:, 1] >= 3][:, 1]) == {7}
