@@ -208,6 +208,8 @@ def single_gpu(args):
     # reduce in the C4 dtypes, on the same rotating-buffer discipline
     if not args.no_variants:
         extra['fold_kernel'] = fold_roofline(lib, dev, sh, S)
+        # the fold the reference-order direct schedule runs at P = 8 (MPICH's pre-fold + tree)
+        extra['fold_kernel_reference_order'] = fold_roofline(lib, dev, sh, S, order=1)
         extra['reduce_half_dtypes_achieved_GBs'] = half_dtypes(lib, dev, sh, S)
 
     traffic = pmc_traffic(f'reduce_fp32_{args.bucket_mib}MiB')
@@ -246,9 +248,10 @@ def single_gpu(args):
     emit(out)
 
 
-def fold_roofline(lib, dev, sh, S, nb=7):
+def fold_roofline(lib, dev, sh, S, nb=7, order=0):
     """k_sumN_tile<float, 7>: out = in + 7 received slices over one P=8 chunk (S/8 fp32), the
-    direct schedule's reduce; algorithmic bytes (nb + 2) * chunk."""
+    direct schedule's reduce; algorithmic bytes (nb + 2) * chunk. order 0: left fold; 1: MPICH's
+    pre-fold + pairwise tree (reference_order at P = 8)."""
     import torch
     from ddl.torch.cpp_backend import check
     n = S // 8 // 4
@@ -257,8 +260,8 @@ def fold_roofline(lib, dev, sh, S, nb=7):
 
     def run(k):
         b = sets[k % 2]
-        check(lib.ddl_reduce_fold(b[-1].data_ptr(), b[0].data_ptr(), P(*[t.data_ptr() for t in b[1:-1]]), nb, n,
-                                  DT_FLOAT, sh), 'ddl_reduce_fold')
+        check(lib.ddl_reduce_fold_ordered(b[-1].data_ptr(), b[0].data_ptr(), P(*[t.data_ptr() for t in b[1:-1]]),
+                                          nb, n, DT_FLOAT, order, sh), 'ddl_reduce_fold_ordered')
     for k in range(4):
         run(k)
     best = float('inf')
@@ -271,10 +274,10 @@ def fold_roofline(lib, dev, sh, S, nb=7):
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
     byts = (nb + 2) * n * 4
-    return {'kernel': f'k_sumN_tile<DDL_FLOAT,{nb}>', 'chunk_bytes': n * 4, 'us': round(best * 1e6, 1),
+    return {'kernel': f'k_sumN_tile<DDL_FLOAT,{nb},order {order}>', 'chunk_bytes': n * 4, 'us': round(best * 1e6, 1),
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
             'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
-            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 else None}
+            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 and order == 0 else None}
 
 
 def half_dtypes(lib, dev, sh, S):

@@ -576,8 +576,8 @@ int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b
     });
 }
 
-int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
-                    void *hip_stream) {
+int ddl_reduce_fold_ordered(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
+                            int order, void *hip_stream) {
     return guarded([&] {
         DDL_REQUIRE(nb >= 1 && nb <= kMaxInputs && ins, DDL_STATUS_INVALID_ARGUMENT, "fold inputs " << nb);
         SegTableN t;
@@ -585,9 +585,15 @@ int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, si
         t.out = out;
         t.n = elements;
         t.nb = nb;
+        t.order = order;
         for (int i = 0; i < nb; ++i) t.b[i] = ins[i];
         launch_sumN(t, dtype, as_stream(hip_stream));
     });
+}
+
+int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
+                    void *hip_stream) {
+    return ddl_reduce_fold_ordered(out, a, ins, nb, elements, dtype, kFoldLeft, hip_stream);
 }
 
 int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype, void *hip_stream) {

@@ -113,6 +113,7 @@ class CPPBackend:
         sig('ddl_reduce_sum2', ci, vp, vp, vp, sz, ci, vp)
         sig('ddl_reduce_sum2_variant', ci, ci, vp, vp, vp, sz, ci, vp)
         sig('ddl_reduce_fold', ci, vp, vp, ctypes.POINTER(vp), ci, sz, ci, vp)
+        sig('ddl_reduce_fold_ordered', ci, vp, vp, ctypes.POINTER(vp), ci, sz, ci, ci, vp)
         sig('ddl_pack', ci, vp, ctypes.POINTER(vp), ctypes.POINTER(sz), ci, vp)
         sig('ddl_unpack', ci, ctypes.POINTER(vp), vp, ctypes.POINTER(sz), ci, vp)
         sig('ddl_local_ring_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, ci, vp)

@@ -251,6 +251,12 @@ int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b
  * left to right; fp16/bf16 accumulate in fp32 and round once. out may alias a. */
 int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
                     void *hip_stream);
+/* The same fold in a given order of the inputs x_0 = a, x_1 = ins[0], ...: order 0 left to right,
+ * 1 MPICH 3.3.2's MPI_Allreduce order above 2048 bytes (the first 2*rem inputs folded in pairs,
+ * then a pairwise tree over the pof2 leaves), 2 its order up to 2048 bytes (binomial tree).
+ * fp16/bf16 fold left in fp32 whatever the order. The reference-order schedules launch this. */
+int ddl_reduce_fold_ordered(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
+                            int order, void *hip_stream);
 
 /* Fusion pack/unpack (device): gathers `count` segments into one contiguous buffer and
  * scatters it back (executeCommunicatePlan_'s memcpy in/out, MPIRingTokenCommunication.cc:548-733). */

@@ -183,3 +183,34 @@ def test_reduce_fold_kernel(lib, oracle, gpu, dt, nb, n, misalign):
     want = oracle.fold(dt, [x[misalign:] for x in xs])
     got = out.cpu().numpy().view(xs[0].dtype)[misalign:]
     assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize('dt', [1, 2, 3, 14])
+@pytest.mark.parametrize('nb', [1, 2, 3, 4, 5, 6, 7, 9, 12, 15])
+@pytest.mark.parametrize('order', [1, 2])
+@pytest.mark.parametrize('n,misalign', [(1, 0), (300_001, 0), (10_007, 1)])
+def test_reduce_fold_ordered_kernel(lib, oracle, gpu, dt, nb, order, n, misalign):
+    """The reference-order folds alone (ddl_reduce_fold_ordered): MPICH's pre-fold + pairwise
+    tree (order 1) and binomial tree (order 2) over nb + 1 inputs vs the oracle's restatement,
+    vector and misaligned paths; fp16/bf16 keep the fp32 left fold."""
+    from _helpers import random_input
+    xs = [random_input(dt, n + misalign, 700 + 17 * i + dt) for i in range(nb + 1)]
+    ts = [to_dev(x, gpu) for x in xs]
+    es = xs[0].itemsize
+    ptrs = [t.data_ptr() + misalign * es for t in ts]
+    out = torch.zeros_like(ts[0])
+    P = ctypes.c_void_p * nb
+    st = lib.ddl_reduce_fold_ordered(out.data_ptr() + misalign * es, ptrs[0], P(*ptrs[1:]), nb, n, dt, order,
+                                     torch.cuda.current_stream().cuda_stream)
+    assert st == 0, lib.ddl_last_error()
+    torch.cuda.synchronize()
+    want = oracle.fold_ref_order(dt, [x[misalign:] for x in xs], 4096 if order == 1 else 0)
+    got = out.cpu().numpy().view(xs[0].dtype)[misalign:]
+    assert got.tobytes() == want.tobytes()
+
+
+def test_reduce_fold_ordered_rejects_bad_order(lib, gpu):
+    x = torch.zeros(16, device=gpu)
+    P = ctypes.c_void_p * 1
+    assert lib.ddl_reduce_fold_ordered(x.data_ptr(), x.data_ptr(), P(x.data_ptr()), 1, 16, 1, 3,
+                                       torch.cuda.current_stream().cuda_stream) == 3
