@@ -84,10 +84,11 @@ struct RingConfig {
     size_t order_bytes = 0;  // message size that picks MPICH's algorithm (0 = this bucket's)
 };
 
-// The schedule that actually runs for P ranks: with ref_order, a ring at P > 2 becomes the
-// direct schedule with the same slicing. Every builder and shape query goes through it.
+// The schedule that actually runs for P ranks: with ref_order, a ring at 2 < P <= kMaxInputs + 1
+// becomes the direct schedule with the same slicing (beyond 16 ranks the fold kernel's input
+// limit keeps the ring, in ring order). Every builder and shape query goes through it.
 inline RingConfig effective_config(RingConfig c, int P) {
-    if (c.ref_order && c.algo == kAlgoRing && P > 2) {
+    if (c.ref_order && c.algo == kAlgoRing && P > 2 && P - 1 <= kMaxInputs) {
         c.algo = kAlgoDirect;
         c.rings = 1;
     }

@@ -316,3 +316,15 @@ def test_reference_order_program_kinds(lib):
     with config(lib, algo=2, reference_order=1):
         prog = ring_program(lib, 2, 5, 300, DT_FLOAT)
         assert set(prog[prog[:, 1] >= 3][:, 1]) == {7}
+
+
+def test_reference_order_beyond_sixteen_ranks_keeps_the_ring(lib, oracle):
+    """The fold kernel takes at most 16 inputs: with reference_order a ring at P = 17 stays the
+    ring (ring order) instead of failing."""
+    P, n = 17, 3000
+    xs = [random_input(DT_FLOAT, n, 5 + r) for r in range(P)]
+    with config(lib, algo=0, reference_order=1):
+        R, _ = ring_shape(lib, n, DT_FLOAT, P)
+        outs = simulate_ring(oracle, lib, DT_FLOAT, xs)
+    want = oracle.allreduce_ring(DT_FLOAT, xs, ring_perms(lib, P, R))
+    assert all(o.tobytes() == want.tobytes() for o in outs)
