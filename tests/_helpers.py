@@ -318,3 +318,29 @@ def apply_folds(oracle, dt, rows, bufs):
         cnt, off = int(gen[0, 6]), int(gen[0, 7])
         ins = [bufs[int(b)][int(s):int(s) + cnt].copy() for b, s in zip(gen[:, 4], gen[:, 5])]
         bufs[1][off:off + cnt] = oracle.fold(dt, ins) if tb is None else oracle.fold_ref_order(dt, ins, tb)
+
+
+MPI_HOME = os.environ.get('MPI_HOME', '/opt/conda')
+MPI_DRIVER = os.path.join(ROOT, 'oracle', 'build', 'mpi_allreduce_driver')
+
+
+def live_mpich_available():
+    return os.path.exists(MPI_DRIVER) and os.path.exists(os.path.join(MPI_HOME, 'bin', 'mpiexec'))
+
+
+def live_mpich(xs, dt):
+    """MPICH's own MPI_Allreduce(MPI_SUM) of the rank buffers xs (one process per rank, our
+    oracle/mpi_allreduce_driver.c calling MPI as MPICommunicator.cc:14-28 does): rank 0's
+    output; every rank's output must be identical. Test infrastructure only."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        for r, x in enumerate(xs):
+            np.ascontiguousarray(x).tofile(os.path.join(d, f'in_{r}.bin'))
+        env = dict(os.environ)
+        env['LD_LIBRARY_PATH'] = os.path.join(MPI_HOME, 'lib') + ':' + env.get('LD_LIBRARY_PATH', '')
+        subprocess.run([os.path.join(MPI_HOME, 'bin', 'mpiexec'), '-n', str(len(xs)), MPI_DRIVER, str(dt),
+                        str(xs[0].size), d], check=True, env=env, timeout=120, capture_output=True)
+        outs = [np.fromfile(os.path.join(d, f'out_{r}.bin'), dtype=xs[0].dtype) for r in range(len(xs))]
+    assert all(o.tobytes() == outs[0].tobytes() for o in outs), 'MPICH ranks disagree'
+    return outs[0]
