@@ -360,3 +360,32 @@ def test_bucket_beyond_2pow31_elements(lib, gpu, algo):
         assert torch.equal(t, want)
     del ins, base, want
     torch.cuda.empty_cache()
+
+
+def test_random_configurations_on_gpu(lib, oracle, gpu):
+    """Random (P, n, dtype, algo, reference_order, slicing, rings, in place) through the real
+    streams and kernels on virtual ranks: every rank holds the sum the configuration promises,
+    bit for bit (MPICH's order with reference_order; ring / left-fold / rank-order otherwise)."""
+    rng = np.random.default_rng(77)
+    for trial in range(40):
+        P = int(rng.integers(2, 9))
+        n = int(rng.choice([1, 65, 511, 513, 4099, 100_003, 1_000_003]))
+        dt = int(rng.choice([d for d in ALL_DTYPES if d != 14]))
+        algo, ref = int(rng.integers(0, 3)), int(rng.integers(0, 2))
+        kv = dict(algo=algo, reference_order=ref, slice_bytes=int(rng.choice([4 << 10, 256 << 10, 2 << 20])),
+                  max_slices=int(rng.integers(1, 17)), rings=int(rng.integers(1, 9)))
+        xs = [random_input(dt, n, 5 * trial + r) for r in range(P)]
+        with config(lib, **kv):
+            outs = run_local(lib, gpu, xs, in_place=bool(trial % 2))
+            R, _ = ring_shape(lib, n, dt, P)
+            perms = ring_perms(lib, P, R, max_rings=kv['rings'])
+        if ref and (algo != 0 or P > 2):
+            want = oracle.fold_ref_order(dt, xs)
+        elif algo == 0:
+            want = oracle.allreduce_ring(dt, xs, perms)
+        elif algo == 1:
+            want = oracle.allreduce_direct(dt, xs)
+        else:
+            want = oracle.fold(dt, xs)
+        for r in range(P):
+            assert outs[r].tobytes() == want.tobytes(), (trial, P, n, dt, kv, r)

@@ -328,3 +328,34 @@ def test_reference_order_beyond_sixteen_ranks_keeps_the_ring(lib, oracle):
         outs = simulate_ring(oracle, lib, DT_FLOAT, xs)
     want = oracle.allreduce_ring(DT_FLOAT, xs, ring_perms(lib, P, R))
     assert all(o.tobytes() == want.tobytes() for o in outs)
+
+
+def test_random_schedules_property(lib, oracle):
+    """Property check over random (P, n, dtype, algo, reference_order, slice_bytes, max_slices,
+    rings): every rank's program, executed with matched sends/recvs, ends with the sum the
+    configuration promises — MPICH's order with reference_order, else the ring / left-fold /
+    rank-order fold — bit for bit."""
+    rng = np.random.default_rng(2024)
+    for trial in range(120):
+        P = int(rng.integers(2, 9))
+        n = int(rng.choice([1, 2, 63, 64, 65, 257, 511, 512, 513, 1000, 4099, 33_333, 100_003]))
+        dt = int(rng.choice(ALL_DTYPES))
+        algo = int(rng.integers(0, 3))
+        ref = int(rng.integers(0, 2))
+        kv = dict(algo=algo, reference_order=ref, slice_bytes=int(rng.choice([1 << 10, 64 << 10, 2 << 20])),
+                  max_slices=int(rng.integers(1, 17)), rings=int(rng.integers(1, 9)))
+        xs = [random_input(dt, n, 3 * trial + r) for r in range(P)]
+        with config(lib, **kv):
+            outs = simulate_ring(oracle, lib, dt, xs)
+            R, _ = ring_shape(lib, n, dt, P)
+            perms = ring_perms(lib, P, R, max_rings=kv['rings'])
+        if ref and (algo != 0 or P > 2):
+            want = oracle.fold_ref_order(dt, xs)
+        elif algo == 0:
+            want = oracle.allreduce_ring(dt, xs, perms)
+        elif algo == 1:
+            want = oracle.allreduce_direct(dt, xs)
+        else:
+            want = oracle.fold(dt, xs)
+        for r in range(P):
+            assert outs[r].tobytes() == want.tobytes(), (trial, P, n, dt, kv, r)
