@@ -71,3 +71,17 @@ def test_product_does_not_reference_oracle():
                 assert 'ddl_oracle' not in text and 'ddlo_' not in text, f
     out = subprocess.run(['readelf', '-d', LIB], capture_output=True, text=True, check=True).stdout
     assert 'oracle' not in out
+
+
+def test_python_config_module(lib):
+    """ddl.torch.config: every documented key reads back, override() restores, bad keys raise."""
+    from ddl.torch import config
+    from ddl.torch.cpp_backend import DDLError
+    snap = config.snapshot()
+    assert all(v >= 0 for v in snap.values()), snap
+    assert snap['reference_order'] == 1
+    with config.override(reference_order=0, slice_bytes=1 << 20):
+        assert config.get('reference_order') == 0 and config.get('slice_bytes') == 1 << 20
+    assert config.snapshot() == snap
+    with pytest.raises(DDLError):
+        config.set('no_such_key', 1)
