@@ -201,7 +201,7 @@ def single_gpu(args):
             sweep.append({'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
                           'hbm_GBs': round(3 * size / t / 1e9, 1)})
             del bufs
-            size *= 4
+            size *= 2  # 4 KiB * 2^k up to 1 GiB, 19 points
         extra['sweep_fp32'] = sweep
 
     # the direct schedule's fold at P = 8 (chunk = S/8, 7 received inputs) and the per-hop
