@@ -626,7 +626,7 @@ def multi_gpu(args):
     state['leg'] = 'size_sweep'
     if not args.no_size_sweep:
         curve = []
-        for sz in (4 << 10, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+        for sz in [(4 << 10) << (2 * k) for k in range(10)]:  # 4 KiB, 16 KiB, ..., 1 GiB
             if sz > args.size_sweep_max_mib << 20:
                 break
             m = sz // 4
