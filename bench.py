@@ -621,6 +621,10 @@ def multi_gpu(args):
     state['leg'] = 'fusion_c5'
     if not args.no_fusion:
         out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
+    # parity on this node: every rank's result equals MPI_Allreduce's (MPICH 3.3.2 order) bit
+    # for bit, on both sides of MPICH's 2048-byte switch, through the schedule the engine runs
+    state['leg'] = 'parity'
+    out['parity_vs_mpich_order'] = parity_leg(lib, comm, dist, torch, dev, stream, rank, world)
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
     # size class) next to RCCL's own ncclAllReduce on the same buffers
     state['leg'] = 'size_sweep'
@@ -662,6 +666,59 @@ def multi_gpu(args):
     finalize()
     dist.destroy_process_group()
     dog.cancel()
+
+
+def mpich_order_sum(xs, message_bytes):
+    """MPI_Allreduce(MPI_SUM)'s per-element order in MPICH 3.3.2 (numpy, one rounding per add in
+    the element type): a binomial tree over ranks up to 2048 bytes, else the first 2*rem ranks
+    folded in pairs and a pairwise tree over the pof2 leaves. A check of the N>1 run only; the
+    tests pin the same order against MPICH itself (tests/test_live_mpich.py)."""
+    v = [x.copy() for x in xs]
+    k = len(v)
+    if message_bytes <= 2048:
+        m = 1
+        while m < k:
+            for t in range(0, k - m, 2 * m):
+                v[t] = v[t] + v[t + m]
+            m *= 2
+        return v[0]
+    pof2 = 1
+    while pof2 * 2 <= k:
+        pof2 *= 2
+    rem = k - pof2
+    leaf = [v[2 * t] + v[2 * t + 1] for t in range(rem)] + v[2 * rem:]
+    m = 1
+    while m < pof2:
+        for t in range(0, pof2, 2 * m):
+            leaf[t] = leaf[t] + leaf[t + m]
+        m *= 2
+    return leaf[0]
+
+
+def parity_leg(lib, comm, dist, torch, dev, stream, rank, world):
+    """ddl_allreduce (the engine's default: autotuned, reference order) of seeded buckets; the
+    inputs and every rank's output are gathered on rank 0 over gloo and compared with MPICH's
+    order. Returns {case: bit_exact} and the overall verdict."""
+    import numpy as np
+    from ddl.torch.cpp_backend import check
+    cases = [('fp32_300', DT_FLOAT, np.float32, 300), ('fp32_1Mi+3', DT_FLOAT, np.float32, (1 << 20) + 3),
+             ('fp64_257', 2, np.float64, 257), ('int32_4099', 3, np.int32, 4099)]
+    res = {}
+    for name, dt, npt, n in cases:
+        rng = np.random.default_rng(99 + 7919 * rank + n)
+        x = (rng.integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32) if npt is np.int32
+             else rng.standard_normal(n).astype(npt))
+        t = torch.from_numpy(x.copy()).to(dev)
+        check(lib.ddl_allreduce(comm.id, t.data_ptr(), t.data_ptr(), n, dt, 0, stream.cuda_stream), 'ddl_allreduce')
+        torch.cuda.synchronize()
+        mine = torch.from_numpy(np.stack([x, t.cpu().numpy()]))
+        everyone = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(everyone, mine)
+        if rank == 0:
+            want = mpich_order_sum([e[0].numpy() for e in everyone], n * x.itemsize)
+            res[name] = all(e[1].numpy().tobytes() == want.tobytes() for e in everyone)
+    return {'cases': res, 'bit_exact': all(res.values()) if rank == 0 else None,
+            'reference_order': lib.ddl_get_config(b'reference_order')}
 
 
 _REAL_STDOUT = None

@@ -157,3 +157,17 @@ def test_reference_broadcast_and_allgather_known_answers(oracle):
     assert v.tolist() == [0, 1, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 5, 6, 7]
     assert i.tolist() == [[r + k, r + k] for r in range(P) for k in range(4)]
     assert np.array_equal(oracle.allgatherv(1, values), v)
+
+
+def test_bench_parity_check_matches_mpich_golden(oracle):
+    """bench.py's N>1 parity leg restates MPICH's order in numpy (mpich_order_sum); it must agree
+    with MPICH's golden outputs and the oracle on every golden case (P = 2..8, both sides of the
+    2048-byte switch)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('bench_mod', os.path.join(os.path.dirname(HERE), 'bench.py'))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for case, meta in MANIFEST['cases'].items():
+        xs, y = GOLD[case + '__inputs'], GOLD[case + '__output']
+        got = bench.mpich_order_sum(list(xs), xs[0].nbytes)
+        assert got.tobytes() == y.tobytes(), case
