@@ -726,37 +726,46 @@ void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t
             rows.insert(rows.end(), row, row + 8);
         }
         if (tk.has_reduce && tk.multi) {
-            long long obuf, ooff, abuf, aoff;
-            decode(tk.reduceN.out, &obuf, &ooff);
-            decode(tk.reduceN.a, &abuf, &aoff);
-            DDL_REQUIRE(obuf == 1, DDL_STATUS_ERROR_UNKNOWN, "fold output outside the output buffer");
-            bool staged = abuf == 0 && aoff == ooff;
-            for (int i = 0; i < tk.reduceN.nb; ++i) {
-                long long bbuf, boff;
-                decode(tk.reduceN.b[i], &bbuf, &boff);
-                staged = staged && bbuf == 2;
+            // the classic direct fold (one left-order step, a = in at the output offset, every
+            // other input a staging slot): one row per received input, in fold order
+            //   {tick, 3, inputs - 1, i, 1, output offset, count, staging offset}
+            if (tk.folds.size() == 1 && tk.folds[0].order == kFoldLeft) {
+                const SegTableN &f = tk.folds[0];
+                long long obuf, ooff, abuf, aoff;
+                decode(f.out, &obuf, &ooff);
+                decode(f.a, &abuf, &aoff);
+                bool staged = obuf == 1 && abuf == 0 && aoff == ooff;
+                for (int i = 0; i < f.nb; ++i) {
+                    long long bbuf, boff;
+                    decode(f.b[i], &bbuf, &boff);
+                    staged = staged && bbuf == 2;
+                }
+                if (staged) {
+                    for (int i = 0; i < f.nb; ++i) {
+                        long long bbuf, boff;
+                        decode(f.b[i], &bbuf, &boff);
+                        long long row[8] = {(long long)t, 3, f.nb, i, obuf, ooff, (long long)f.n, boff};
+                        rows.insert(rows.end(), row, row + 8);
+                    }
+                    continue;
+                }
             }
-            if (!staged || tk.reduceN.order != kFoldLeft) {
-                // general fold (one-shot, reference order): one row per input in fold order,
-                // input 0 = a: {tick, 5 + order, inputs, i, source buffer, source offset, count,
-                // output offset}; kind 5 left fold, 6 MPICH's pre-fold + pairwise tree, 7 binomial
-                const int ni = tk.reduceN.nb + 1;
-                const long long kind = 5 + tk.reduceN.order;
+            // general fold steps, in execution order: one row per input, input 0 = a:
+            //   {tick, kind, inputs, i, source buffer, source offset, count, output offset}
+            // kind 5 + order into the output buffer, 8 + order into staging (a partial sum);
+            // order 0 left, 1 MPICH's pre-fold + pairwise tree, 2 binomial
+            for (const SegTableN &f : tk.folds) {
+                long long obuf, ooff;
+                decode(f.out, &obuf, &ooff);
+                DDL_REQUIRE(obuf == 1 || obuf == 2, DDL_STATUS_ERROR_UNKNOWN, "fold output outside out / staging");
+                const int ni = f.nb + 1;
+                const long long kind = (obuf == 1 ? 5 : 8) + f.order;
                 for (int i = 0; i < ni; ++i) {
                     long long sbuf, soff;
-                    decode(i == 0 ? tk.reduceN.a : tk.reduceN.b[i - 1], &sbuf, &soff);
-                    long long row[8] = {(long long)t, kind, ni, i, sbuf, soff, (long long)tk.reduceN.n, ooff};
+                    decode(i == 0 ? f.a : f.b[i - 1], &sbuf, &soff);
+                    long long row[8] = {(long long)t, kind, ni, i, sbuf, soff, (long long)f.n, ooff};
                     rows.insert(rows.end(), row, row + 8);
                 }
-                continue;
-            }
-            // direct fold (a = in at the output offset): one row per received input, in fold order
-            for (int i = 0; i < tk.reduceN.nb; ++i) {
-                long long bbuf, boff;
-                decode(tk.reduceN.b[i], &bbuf, &boff);
-                DDL_REQUIRE(bbuf == 2, DDL_STATUS_ERROR_UNKNOWN, "fold input outside staging");
-                long long row[8] = {(long long)t, 3, tk.reduceN.nb, i, obuf, ooff, (long long)tk.reduceN.n, boff};
-                rows.insert(rows.end(), row, row + 8);
             }
         }
     }

@@ -127,7 +127,7 @@ std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &b
     add(kAlgoRing, kMaxRings, 8u << 20, 8);
     add(kAlgoRing, kMaxRings, 64u << 20, 8);
     if (R > 1) add(kAlgoRing, 1, 2u << 20, 8);
-    if (P > 2 && P - 1 <= kMaxInputs) {
+    if (P > 2) {
         add(kAlgoDirect, 1, 2u << 20, 8);
         add(kAlgoDirect, 1, 512u << 10, 16);
         add(kAlgoDirect, 1, 8u << 20, 8);
@@ -135,7 +135,7 @@ std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &b
     }
     // latency-bound buckets: one group (whole bucket to every peer) instead of two or more;
     // costs (P-1) x the bucket in wire bytes and staging, so only small buckets
-    if (P - 1 <= kMaxInputs && bytes <= kOneShotMaxBytes) add(kAlgoOneShot, 1, 0, 1);
+    if (bytes <= kOneShotMaxBytes) add(kAlgoOneShot, 1, 0, 1);
     return c;
 }
 

@@ -84,9 +84,13 @@ void *RankResources::ensure_staging(size_t bytes) {
 
 double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream) {
     const double es = (double)dtype_size(dtype);
-    if (tk.multi) {
-        launch_sumN(tk.reduceN, dtype, stream);
-        return (tk.reduceN.nb + 2.0) * (double)tk.reduceN.n * es;
+    if (tk.multi) {  // fold steps in order on the compute stream
+        double bytes = 0;
+        for (const SegTableN &f : tk.folds) {
+            launch_sumN(f, dtype, stream);
+            bytes += (f.nb + 2.0) * (double)f.n * es;
+        }
+        return bytes;
     }
     launch_sum2(tk.reduce, dtype, stream, ring_variant());
     double elems = 0;

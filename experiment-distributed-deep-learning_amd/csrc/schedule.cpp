@@ -177,8 +177,72 @@ size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cf
     int R, K;
     size_t stride;
     ring_shape(n, esize, P, cfg, &R, &K, &stride);
-    const size_t slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)R;
+    const size_t slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 + fold_temp_slots(P) : 0) : 2 * (size_t)R;
     return slots * stride;
+}
+
+void plan_fold(std::vector<SegTableN> &steps, const std::vector<const void *> &xs, void *out, size_t n, int order,
+               const std::function<void *(int)> &temp) {
+    const size_t W = kMaxInputs + 1;
+    int used = 0;
+    auto step = [&](const std::vector<const void *> &in, int ord, void *dst) {
+        SegTableN t;
+        t.a = in[0];
+        t.nb = (int)in.size() - 1;
+        for (int i = 0; i < t.nb; ++i) t.b[i] = in[i + 1];
+        t.out = dst;
+        t.n = n;
+        t.order = ord;
+        steps.push_back(t);
+    };
+    DDL_REQUIRE(xs.size() >= 2, DDL_STATUS_ERROR_UNKNOWN, "fold of " << xs.size() << " inputs");
+    if (xs.size() <= W) {
+        step(xs, order, out);
+        return;
+    }
+    if (order == kFoldLeft) {  // ((x_0 + ... + x_15) + x_16 + ... + x_30) + ...: one partial
+        void *acc = temp(used++);
+        step(std::vector<const void *>(xs.begin(), xs.begin() + W), kFoldLeft, acc);
+        for (size_t i = W; i < xs.size();) {
+            const size_t take = std::min(W - 1, xs.size() - i);
+            std::vector<const void *> in{acc};
+            in.insert(in.end(), xs.begin() + i, xs.begin() + i + take);
+            i += take;
+            step(in, kFoldLeft, i == xs.size() ? out : acc);
+        }
+        return;
+    }
+    std::vector<const void *> level = xs;
+    if (order == kFoldMpichTree) {  // leaves: pre-folded pairs, then the rest; pof2 of them
+        size_t pof2 = 1;
+        while (pof2 * 2 <= xs.size()) pof2 *= 2;
+        const size_t rem = xs.size() - pof2;
+        level.clear();
+        for (size_t t = 0; t < rem; ++t) {
+            void *d = temp(used++);
+            step({xs[2 * t], xs[2 * t + 1]}, kFoldLeft, d);
+            level.push_back(d);
+        }
+        for (size_t t = rem; t < pof2; ++t) level.push_back(xs[t + rem]);
+    }
+    // a binomial tree (the pairwise tree over pof2 leaves is one) restricted to aligned blocks
+    // of W is the block's own binomial tree; the block sums then continue the same tree
+    while (level.size() > W) {
+        std::vector<const void *> next;
+        for (size_t b = 0; b < level.size(); b += W) {
+            const size_t e = std::min(level.size(), b + W);
+            if (e - b == 1) {
+                next.push_back(level[b]);
+                continue;
+            }
+            void *d = temp(used++);
+            step(std::vector<const void *>(level.begin() + b, level.begin() + e), kFoldBinomial, d);
+            next.push_back(d);
+        }
+        level.swap(next);
+    }
+    step(level, kFoldBinomial, out);
+    DDL_REQUIRE(used <= fold_temp_slots((int)xs.size()), DDL_STATUS_ERROR_UNKNOWN, "fold temp slots exceeded");
 }
 
 namespace {
@@ -192,8 +256,6 @@ namespace {
 void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
                   size_t es, int order) {
     const int K = prog.K;
-    DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "direct schedule supports up to "
-                                                                       << kMaxInputs + 1 << " ranks");
     const Range mine = chunk_range(n, es, P, 1, 0, rank);
     for (int k = 0; k < K; ++k) {
         Tick t;
@@ -215,22 +277,19 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
         if (ms.size()) {
             t.has_reduce = true;
             t.multi = true;
-            t.reduceN.a = inb + ms.begin * es;
-            t.reduceN.out = outb + ms.begin * es;
-            t.reduceN.n = ms.size();
-            t.reduceN.nb = P - 1;
-            t.reduceN.order = order;
-            auto slot = [&](int s) -> const void * {
-                return stb + ((size_t)s * prog.staging_stride + (ms.begin - mine.begin)) * es;
-            };
-            if (order == kFoldLeft) {
-                for (int s = 0; s < P - 1; ++s) t.reduceN.b[s] = slot(s);
-            } else {  // rank order: x_q is `in` for q == me, else the slot of sender q
-                const void *own = t.reduceN.a;
-                auto x = [&](int q) { return q == rank ? own : slot((q - rank + P) % P - 1); };
-                t.reduceN.a = x(0);
-                for (int q = 1; q < P; ++q) t.reduceN.b[q - 1] = x(q);
+            const size_t off = ms.begin - mine.begin;
+            auto slot = [&](int s) -> const void * { return stb + ((size_t)s * prog.staging_stride + off) * es; };
+            const void *own = inb + ms.begin * es;
+            // kFoldLeft: in, x_{me+1}, x_{me+2}, ... (slot s holds sender me+1+s); the reference
+            // orders: x_0, ..., x_{P-1} in rank order (x_me = in)
+            std::vector<const void *> xs;
+            for (int q = 0; q < P; ++q) {
+                const int who = order == kFoldLeft ? (rank + q) % P : q;
+                xs.push_back(who == rank ? own : slot((who - rank + P) % P - 1));
             }
+            plan_fold(t.folds, xs, outb + ms.begin * es, ms.size(), order, [&](int j) {
+                return static_cast<void *>(stb + ((size_t)(P - 1 + j) * prog.staging_stride + off) * es);
+            });
         }
         prog.ticks.push_back(std::move(t));
     }
@@ -259,8 +318,6 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
 // In place is safe: the fold runs after the group, i.e. after every send has read `in`.
 void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
                    size_t es, int order) {
-    DDL_REQUIRE(P - 1 <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "one-shot schedule supports up to "
-                                                                       << kMaxInputs + 1 << " ranks");
     auto slot = [&](int q) { return stb + (size_t)((q - rank + P) % P - 1) * prog.staging_stride * es; };
     Tick t;
     t.reduce.count = 0;
@@ -271,12 +328,10 @@ void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *ou
     }
     t.has_reduce = true;
     t.multi = true;
-    t.reduceN.a = rank == 0 ? static_cast<const void *>(inb) : slot(0);
-    t.reduceN.out = outb;
-    t.reduceN.n = n;
-    t.reduceN.nb = P - 1;
-    t.reduceN.order = order;
-    for (int q = 1; q < P; ++q) t.reduceN.b[q - 1] = q == rank ? static_cast<const void *>(inb) : slot(q);
+    std::vector<const void *> xs;
+    for (int q = 0; q < P; ++q) xs.push_back(q == rank ? static_cast<const void *>(inb) : slot(q));
+    plan_fold(t.folds, xs, outb, n, order,
+              [&](int j) { return static_cast<void *>(stb + (size_t)(P - 1 + j) * prog.staging_stride * es); });
     prog.ticks.push_back(std::move(t));
     Tick join;
     join.reduce.count = 0;
@@ -297,10 +352,13 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     prog.algo = cfg.algo;
     prog.ticks.clear();
     ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
-    prog.staging_slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 : 0) : 2 * (size_t)prog.R;
+    prog.staging_slots =
+        cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 + fold_temp_slots(P) : 0) : 2 * (size_t)prog.R;
     if (P <= 1 || n == 0) return;
     // fold order of the direct / one-shot N-input reduce (kFoldLeft: ring 0's order)
-    const int order = cfg.ref_order ? mpich_fold_order(cfg.order_bytes ? cfg.order_bytes : n * es) : kFoldLeft;
+    // (fp16 / bf16, which the reference rejects, always fold left in fp32)
+    const bool half = dtype == DDL_HALF || dtype == DDL_BFLOAT16;
+    const int order = cfg.ref_order && !half ? mpich_fold_order(cfg.order_bytes ? cfg.order_bytes : n * es) : kFoldLeft;
     if (cfg.algo == kAlgoOneShot) {
         build_oneshot(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
                       static_cast<char *>(staging), n, es, order);

@@ -13,6 +13,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "common.h"
@@ -54,7 +55,9 @@ struct Tick {
     std::vector<CopyOp> copies;
     std::vector<P2POp> ops;
     SegTable reduce;       // valid when has_reduce && !multi
-    SegTableN reduceN;     // valid when has_reduce && multi (direct schedule)
+    // valid when has_reduce && multi (direct / one-shot): N-input fold steps run in order; one
+    // step up to 16 ranks, a chain or tree of steps through temp slots beyond (plan_fold)
+    std::vector<SegTableN> folds;
     bool has_reduce = false;
     bool multi = false;
     int wait_reduce = -1;  // the comm stream waits for this tick's reduce before posting ops
@@ -84,16 +87,25 @@ struct RingConfig {
     size_t order_bytes = 0;  // message size that picks MPICH's algorithm (0 = this bucket's)
 };
 
-// The schedule that actually runs for P ranks: with ref_order, a ring at 2 < P <= kMaxInputs + 1
-// becomes the direct schedule with the same slicing (beyond 16 ranks the fold kernel's input
-// limit keeps the ring, in ring order). Every builder and shape query goes through it.
+// The schedule that actually runs for P ranks: with ref_order, a ring at P > 2 becomes the
+// direct schedule with the same slicing. Every builder and shape query goes through it.
 inline RingConfig effective_config(RingConfig c, int P) {
-    if (c.ref_order && c.algo == kAlgoRing && P > 2 && P - 1 <= kMaxInputs) {
+    if (c.ref_order && c.algo == kAlgoRing && P > 2) {
         c.algo = kAlgoDirect;
         c.rings = 1;
     }
     return c;
 }
+
+// Fold steps that compute out = x_0 + ... + x_{K-1} (xs in the order the sum takes them) in
+// FoldOrder `order`, each step at most kMaxInputs + 1 inputs over n elements. Up to 16 inputs
+// it is one step. Beyond: kFoldLeft chains 16-input steps through one partial; the MPICH orders
+// fold aligned blocks of 16 (pre-folded pairs first for kFoldMpichTree), then the block sums,
+// which is the same tree. Partial sums go to temp(0), temp(1), ... (n elements each, at most
+// fold_temp_slots(K) of them).
+void plan_fold(std::vector<SegTableN> &steps, const std::vector<const void *> &xs, void *out, size_t n, int order,
+               const std::function<void *(int)> &temp);
+inline int fold_temp_slots(int K) { return K > kMaxInputs + 1 ? K : 0; }
 
 // Per-rank tick list of one allreduce. `staging` must hold staging_elems(R, stride) elements:
 // two slots per ring (reduce-scatter step parity), ring j / parity q at (2j + q) * stride.

@@ -249,12 +249,8 @@ def simulate_moves(progs, bufs):
     return bufs
 
 
-def simulate_ring(oracle, lib, dt, xs):
-    """Execute every rank's ring (or direct) program, taken from the engine's own schedule, on
-    host buffers: sends/recvs matched by (tick, peer, tag), 2-input reduces and N-input folds
-    through the oracle's operators."""
-    P, n = len(xs), xs[0].size
-    progs = [ring_program(lib, r, P, n, dt) for r in range(P)]
+def staging_size(progs):
+    """Elements of staging a set of program dumps touches (recv targets, fold inputs/outputs)."""
     st_size = 1
     for p in progs:
         for row in p:
@@ -262,8 +258,21 @@ def simulate_ring(oracle, lib, dt, xs):
                 st_size = max(st_size, int(row[5] + row[6]))
             elif row[1] in (2, 3):
                 st_size = max(st_size, int(row[7] + row[6]))
-            elif row[1] in GENERAL_FOLDS and row[4] == 2:
-                st_size = max(st_size, int(row[5] + row[6]))
+            elif row[1] in GENERAL_FOLDS:
+                if row[4] == 2:
+                    st_size = max(st_size, int(row[5] + row[6]))
+                if GENERAL_FOLDS[int(row[1])][1] == 2:
+                    st_size = max(st_size, int(row[7] + row[6]))
+    return st_size
+
+
+def simulate_ring(oracle, lib, dt, xs):
+    """Execute every rank's ring (or direct) program, taken from the engine's own schedule, on
+    host buffers: sends/recvs matched by (tick, peer, tag), 2-input reduces and N-input folds
+    through the oracle's operators."""
+    P, n = len(xs), xs[0].size
+    progs = [ring_program(lib, r, P, n, dt) for r in range(P)]
+    st_size = staging_size(progs)
     bufs = [[x.copy(), np.zeros_like(x), np.zeros(st_size, dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
     for t in range(T):
@@ -293,15 +302,17 @@ def simulate_ring(oracle, lib, dt, xs):
     return [b[1] for b in bufs]
 
 
-# General N-input fold rows of a program dump: kind -> oracle total_bytes argument (None: left
-# fold). 5 = left fold, 6 = MPICH's pre-fold + pairwise tree (> 2048-byte messages), 7 = MPICH's
-# binomial tree (<= 2048 bytes).
-GENERAL_FOLDS = {5: None, 6: 4096, 7: 0}
+# General N-input fold rows of a program dump: kind -> (oracle total_bytes argument, output
+# buffer). Order: None = left fold, 4096 = MPICH's pre-fold + pairwise tree (> 2048-byte
+# messages), 0 = MPICH's binomial tree (<= 2048 bytes). Kinds 5-7 write the output buffer,
+# 8-10 a partial sum into staging (fold chains / trees beyond 16 ranks).
+GENERAL_FOLDS = {5: (None, 1), 6: (4096, 1), 7: (0, 1), 8: (None, 2), 9: (4096, 2), 10: (0, 2)}
 
 
 def apply_folds(oracle, dt, rows, bufs):
     """Run one tick's N-input folds of one rank (rows of that tick) on bufs = [in, out, staging]:
-    kind 3 (in + staged inputs, left fold) and the general kinds 5/6/7 (every input named)."""
+    kind 3 (in + staged inputs, left fold) and the general fold steps (every input named), in
+    the order the engine launches them."""
     folds = rows[rows[:, 1] == 3]
     if len(folds):
         nb = int(folds[0, 2])
@@ -309,15 +320,17 @@ def apply_folds(oracle, dt, rows, bufs):
         off, cnt = int(folds[0, 5]), int(folds[0, 6])
         ins = [bufs[0][off:off + cnt]] + [bufs[2][s:s + cnt] for s in folds[:, 7]]
         bufs[1][off:off + cnt] = oracle.fold(dt, ins)
-    for kind, tb in GENERAL_FOLDS.items():
-        gen = rows[rows[:, 1] == kind]
-        if not len(gen):
-            continue
-        ni = int(gen[0, 2])
-        assert len(gen) == ni and list(gen[:, 3]) == list(range(ni))
-        cnt, off = int(gen[0, 6]), int(gen[0, 7])
-        ins = [bufs[int(b)][int(s):int(s) + cnt].copy() for b, s in zip(gen[:, 4], gen[:, 5])]
-        bufs[1][off:off + cnt] = oracle.fold(dt, ins) if tb is None else oracle.fold_ref_order(dt, ins, tb)
+    gen = rows[np.isin(rows[:, 1], list(GENERAL_FOLDS))]
+    i = 0
+    while i < len(gen):
+        ni = int(gen[i, 2])
+        step = gen[i:i + ni]
+        assert len(step) == ni and list(step[:, 3]) == list(range(ni)) and len(set(step[:, 1])) == 1
+        tb, ob = GENERAL_FOLDS[int(step[0, 1])]
+        cnt, off = int(step[0, 6]), int(step[0, 7])
+        ins = [bufs[int(b)][int(s):int(s) + cnt].copy() for b, s in zip(step[:, 4], step[:, 5])]
+        bufs[ob][off:off + cnt] = oracle.fold(dt, ins) if tb is None else oracle.fold_ref_order(dt, ins, tb)
+        i += ni
 
 
 MPI_HOME = os.environ.get('MPI_HOME', '/opt/conda')

@@ -50,12 +50,7 @@ def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
         xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
         prog = h.ring_program(lib, rank, world, n, dt)
         R, _ = h.ring_shape(lib, n, dt, world)
-        st = 1
-        for row in prog:
-            if row[1] <= 1 and row[4] == 2 or row[1] in h.GENERAL_FOLDS and row[4] == 2:
-                st = max(st, int(row[5] + row[6]))
-            elif row[1] in (2, 3):
-                st = max(st, int(row[7] + row[6]))
+        st = h.staging_size([prog])
         bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
         view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
         for t in sorted(set(prog[:, 0].tolist())):

@@ -389,3 +389,22 @@ def test_random_configurations_on_gpu(lib, oracle, gpu):
             want = oracle.fold(dt, xs)
         for r in range(P):
             assert outs[r].tobytes() == want.tobytes(), (trial, P, n, dt, kv, r)
+
+
+@pytest.mark.parametrize('P', [17, 33])
+@pytest.mark.parametrize('algo,ref', [(0, 1), (1, 1), (2, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize('dt', [1, 2, 3], ids=lambda d: NAME[d])
+def test_fold_trees_beyond_sixteen_ranks_on_gpu(lib, oracle, gpu, P, algo, ref, dt):
+    """Beyond 16 virtual ranks the fold runs as several launches through staging partials (a
+    left chain, or MPICH's tree in blocks of 16): bit-exact with the requested order, in place,
+    on both sides of the 2048-byte switch."""
+    for n in (300, 100_003):
+        xs = [random_input(dt, n, 7 * P + 3 * r + n) for r in range(P)]
+        with config(lib, algo=algo, reference_order=ref, slice_bytes=64 << 10):
+            outs = run_local(lib, gpu, xs, in_place=True)
+        if ref:
+            want = oracle.fold_ref_order(dt, xs)
+        else:
+            want = oracle.allreduce_direct(dt, xs) if algo == 1 else oracle.fold(dt, xs)
+        for r in range(P):
+            assert outs[r].tobytes() == want.tobytes(), (n, r)

@@ -115,7 +115,7 @@ def _overlap(a0, a1, b0, b1):
 
 
 @pytest.mark.parametrize('algo,ref_order', [(0, 0), (1, 0), (2, 0), (1, 1), (2, 1)])
-@pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8, 17, 33])
 @pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
 @pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
 def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
@@ -130,8 +130,9 @@ def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
             for row in prog[(prog[:, 1] == 2) | (prog[:, 1] == 3)]:
                 red.setdefault(int(row[0]), []).append(row)
             for row in prog[np.isin(prog[:, 1], list(GENERAL_FOLDS))]:  # general fold: reads (buf, off), writes out
-                t_, _, _, _, sb, so, c_, oo = row
-                red.setdefault(int(t_), []).append(('gen', int(sb), int(so), int(c_), int(oo)))
+                t_, kind_, _, _, sb, so, c_, oo = row
+                ob = GENERAL_FOLDS[int(kind_)][1]  # 1: the output buffer, 2: a staging partial
+                red.setdefault(int(t_), []).append(('gen', int(sb), int(so), int(c_), int(oo), ob))
             w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
             for t in sorted(set(prog[:, 0].tolist())):
                 ops = prog[(prog[:, 0] == t) & (prog[:, 1] <= 1)]
@@ -144,13 +145,16 @@ def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
                 for op in ops:
                     _, kind, _, _, buf, off, cnt, _ = op
                     for r in running:
-                        if isinstance(r, tuple):  # general fold input: (tag, buffer, offset, count, out offset)
-                            _, sb, so, c_, oo = r
+                        if isinstance(r, tuple):  # general fold step: (tag, buffer, offset, count, out offset, out buffer)
+                            _, sb, so, c_, oo, ob = r
                             rng_ = (so, so + c_) if sb == 2 else None
                             if buf == 2 and rng_:
                                 assert not _overlap(off, off + cnt, *rng_), (rank, t, 'staging')
+                            if buf == 2 and ob == 2:
+                                assert not _overlap(off, off + cnt, oo, oo + c_), (rank, t, 'staging partial')
                             if buf != 2:
-                                assert not _overlap(off, off + cnt, oo, oo + c_), (rank, t, 'in/out')
+                                if ob == 1:
+                                    assert not _overlap(off, off + cnt, oo, oo + c_), (rank, t, 'in/out')
                                 if sb != 2:
                                     assert not _overlap(off, off + cnt, so, so + c_), (rank, t, 'in/out')
                             continue
@@ -318,16 +322,51 @@ def test_reference_order_program_kinds(lib):
         assert set(prog[prog[:, 1] >= 3][:, 1]) == {7}
 
 
-def test_reference_order_beyond_sixteen_ranks_keeps_the_ring(lib, oracle):
-    """The fold kernel takes at most 16 inputs: with reference_order a ring at P = 17 stays the
-    ring (ring order) instead of failing."""
-    P, n = 17, 3000
-    xs = [random_input(DT_FLOAT, n, 5 + r) for r in range(P)]
-    with config(lib, algo=0, reference_order=1):
-        R, _ = ring_shape(lib, n, DT_FLOAT, P)
-        outs = simulate_ring(oracle, lib, DT_FLOAT, xs)
-    want = oracle.allreduce_ring(DT_FLOAT, xs, ring_perms(lib, P, R))
-    assert all(o.tobytes() == want.tobytes() for o in outs)
+@pytest.mark.parametrize('algo,ref_order', [(0, 1), (1, 1), (2, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize('P', [17, 20, 31, 32, 33])
+@pytest.mark.parametrize('n', [1, 300, 513, 5000])
+@pytest.mark.parametrize('dt', [1, 2, 3, 19])
+def test_fold_trees_beyond_sixteen_ranks(lib, oracle, algo, ref_order, P, n, dt):
+    """Beyond 16 ranks one fold launch cannot take every input: the fold runs as a chain (left)
+    or a tree of 16-input steps through staging partials (MPICH's orders), and must still give
+    the exact sum of the requested order — MPICH's with reference_order (a ring runs as direct),
+    else the left fold. fp16 (not in the reference) rounds once per 16-input step."""
+    xs = [random_input(dt, n, 3 + 17 * r) for r in range(P)]
+    with config(lib, algo=algo, reference_order=ref_order):
+        outs = simulate_ring(oracle, lib, dt, xs)
+    if dt == 19:
+        want = None
+    elif ref_order:
+        want = oracle.fold_ref_order(dt, xs)
+    elif algo == 1:
+        want = oracle.allreduce_direct(dt, xs)
+    else:
+        want = oracle.fold(dt, xs)
+    if want is None:  # fp16: identical on every rank and within the fp16 summation bound
+        exact = np.sum([x.astype(np.float64) for x in xs], axis=0)
+        bound = P * 2.0 ** -11 * np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0) + 2.0 ** -14
+        for r in range(P):
+            assert outs[r].tobytes() == outs[0].tobytes()
+        assert np.all(np.abs(outs[0].astype(np.float64) - exact) <= bound)
+        return
+    for r in range(P):
+        assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+def test_fold_tree_shape_beyond_sixteen_ranks(lib):
+    """P = 33, reference order, > 2048 bytes: one pre-fold step (rem = 1), then binomial blocks
+    of 16 leaves into staging partials, then the top; every step has at most 16 inputs."""
+    with config(lib, algo=1, reference_order=1):
+        prog = ring_program(lib, 5, 33, 100_000, DT_FLOAT)
+    gen = prog[np.isin(prog[:, 1], list(GENERAL_FOLDS))]
+    assert gen[:, 2].max() <= 16
+    t0 = gen[gen[:, 0] == gen[0, 0]]
+    sizes, kinds, i = [], [], 0
+    while i < len(t0):
+        sizes.append(int(t0[i, 2]))
+        kinds.append(int(t0[i, 1]))
+        i += sizes[-1]
+    assert sizes == [2, 16, 16, 2] and kinds == [8, 10, 10, 7], (sizes, kinds)
 
 
 def test_random_schedules_property(lib, oracle):
