@@ -2,6 +2,8 @@
 // errors into a status code; no C++ exception crosses the ABI.
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -48,6 +50,99 @@ int current_device() {
     return d;
 }
 
+std::vector<std::string> split_endpoints(const char *endpoints) {
+    std::vector<std::string> eps;
+    std::string s(endpoints);
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        size_t sc = s.find(';', pos);
+        if (sc == std::string::npos) sc = s.size();
+        if (sc > pos) eps.push_back(s.substr(pos, sc - pos));
+        pos = sc + 1;
+    }
+    return eps;
+}
+
+std::mutex &channels_mu() {
+    static std::mutex mu;
+    return mu;
+}
+std::map<long long, std::shared_ptr<ControlChannel>> &channels() {
+    static auto *m = new std::map<long long, std::shared_ptr<ControlChannel>>();
+    return *m;
+}
+std::shared_ptr<ControlChannel> channel(long long h) {
+    std::lock_guard<std::mutex> g(channels_mu());
+    auto it = channels().find(h);
+    DDL_REQUIRE(it != channels().end(), DDL_STATUS_INVALID_ARGUMENT, "unknown control channel " << h);
+    return it->second;
+}
+
+// One negotiation round with a fixed key set ('\n'-separated) over `ch`: the agreed keys,
+// '\n'-separated and lexicographic, into out (the handler's protocol without the data plane).
+void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len) {
+    DDL_REQUIRE(keys && out && len > 0, DDL_STATUS_INVALID_ARGUMENT, "bad negotiate args");
+    DDL_REQUIRE(ch.connected(), DDL_STATUS_NOT_INITIALIZED, "control channel not connected");
+    std::vector<std::string> mine;
+    std::string s(keys);
+    size_t pos = 0;
+    while (pos < s.size()) {
+        size_t nl = s.find('\n', pos);
+        if (nl == std::string::npos) nl = s.size();
+        if (nl > pos) mine.push_back(std::string(request_type_name(kReqAllreduce)) + "::" + s.substr(pos, nl - pos));
+        pos = nl + 1;
+    }
+    std::sort(mine.begin(), mine.end());
+    mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+    // this rank's ids by table index, as the handler keeps them
+    std::vector<uint8_t> held(ch.cache.size(), 0);
+    std::vector<uint32_t> idx;
+    bool cached = !mine.empty();
+    for (const auto &k : mine) {
+        uint32_t i;
+        if (ch.cache.lookup(k, &i)) {
+            held[i] = 1;
+            idx.push_back(i);
+        } else {
+            cached = false;
+        }
+    }
+    Agreed a;
+    if (ch.rank() == 0) {
+        a = negotiate_root(ch, cached, idx, mine);
+        negotiate_root_finish(ch);
+    } else {
+        Token t;
+        ch.recv(t, -1);
+        a = negotiate_member(
+            ch, t,
+            [&](const std::vector<std::string> &proposed) {
+                std::vector<std::string> both;
+                for (const auto &k : proposed)
+                    if (std::binary_search(mine.begin(), mine.end(), k)) both.push_back(k);
+                return both;
+            },
+            [&](const std::vector<uint32_t> &proposed) {
+                std::vector<uint32_t> both;
+                for (uint32_t i : proposed)
+                    if (i < held.size() && held[i]) both.push_back(i);
+                return both;
+            });
+    }
+    std::vector<std::string> agreed;
+    if (a.cached) {
+        for (uint32_t i : a.idx) agreed.push_back(ch.cache.at(i));
+        std::sort(agreed.begin(), agreed.end());
+    } else {
+        agreed = a.wire;
+        ch.cache.learn(agreed);
+    }
+    std::string res;
+    for (const auto &k : agreed) res.append(k.substr(k.find("::") + 2)).append("\n");
+    DDL_REQUIRE(res.size() < len, DDL_STATUS_INVALID_ARGUMENT, "output buffer too small");
+    std::memcpy(out, res.c_str(), res.size() + 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -73,14 +168,7 @@ int ddl_init(int rank, int size, int device, const void *unique_id, size_t len) 
                     "bad rank/size " << rank << "/" << size);
         DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
         DDL_HIP(hipSetDevice(device));
-        ncclComm_t nc = nullptr;
-        if (size > 1) {
-            DDL_REQUIRE(unique_id && len >= sizeof(ncclUniqueId), DDL_STATUS_INVALID_ARGUMENT,
-                        "unique id of " << sizeof(ncclUniqueId) << " bytes required");
-            ncclUniqueId id;
-            std::memcpy(&id, unique_id, sizeof id);
-            rccl_check(rccl().CommInitRank(&nc, size, id, rank), "ncclCommInitRank");
-        }
+        ncclComm_t nc = size > 1 ? rccl_init_rank(rank, size, unique_id, len) : nullptr;
         Registry::get().set_world(std::make_shared<Communicator>(rank, size, device, nc));
         DDL_LOG(1, "initialized rank " << rank << "/" << size << " on device " << device
                                        << (size > 1 ? std::string(" rccl=") + rccl().path : ""));
@@ -92,7 +180,7 @@ int ddl_init_single(int device) { return ddl_init(0, 1, device, nullptr, 0); }
 int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn group, ddl_test_max_fn max,
                             void *user) {
     return guarded([&] {
-        DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && group && max, DDL_STATUS_INVALID_ARGUMENT,
+        DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && group, DDL_STATUS_INVALID_ARGUMENT,
                     "bad test transport arguments");
         DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
         DDL_HIP(hipSetDevice(device));
@@ -107,7 +195,7 @@ int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn gr
 
 int ddl_control_listen(char *endpoint_out, size_t len) {
     return guarded([&] {
-        std::string ep = world_control().listen();
+        std::string ep = standalone_control()->listen();
         DDL_REQUIRE(endpoint_out && len > ep.size(), DDL_STATUS_INVALID_ARGUMENT, "endpoint buffer too small");
         std::memcpy(endpoint_out, ep.c_str(), ep.size() + 1);
     });
@@ -117,114 +205,75 @@ int ddl_control_connect(const char *endpoints) {
     return guarded([&] {
         DDL_REQUIRE(endpoints, DDL_STATUS_INVALID_ARGUMENT, "null endpoints");
         auto world = Registry::get().world();
-        std::vector<std::string> eps;
-        std::string s(endpoints);
-        size_t pos = 0;
-        while (pos <= s.size()) {
-            size_t sc = s.find(';', pos);
-            if (sc == std::string::npos) sc = s.size();
-            if (sc > pos) eps.push_back(s.substr(pos, sc - pos));
-            pos = sc + 1;
-        }
-        world_control().connect(world->rank(), world->size(), eps, 120000);
-        world->handler();  // collective: creates the handler's private RCCL communicator now
+        auto ch = standalone_control();
+        ch->connect(world->rank(), world->size(), split_endpoints(endpoints), 120000);
+        standalone_control() = std::make_shared<ControlChannel>();
+        // collective: the world's token ring and its keyed data-plane communicator
+        world->enable_keyed(ch);
     });
 }
 
 int ddl_control_connect_ranked(int rank, int size, const char *endpoints) {
     return guarded([&] {
         DDL_REQUIRE(endpoints, DDL_STATUS_INVALID_ARGUMENT, "null endpoints");
-        std::vector<std::string> eps;
-        std::string s(endpoints);
-        size_t pos = 0;
-        while (pos <= s.size()) {
-            size_t sc = s.find(';', pos);
-            if (sc == std::string::npos) sc = s.size();
-            if (sc > pos) eps.push_back(s.substr(pos, sc - pos));
-            pos = sc + 1;
-        }
-        world_control().connect(rank, size, eps, 120000);
+        standalone_control()->connect(rank, size, split_endpoints(endpoints), 120000);
     });
 }
 
 int ddl_control_stats(long long *string_rounds, long long *cached_rounds) {
     return guarded([&] {
         DDL_REQUIRE(string_rounds && cached_rounds, DDL_STATUS_INVALID_ARGUMENT, "null output");
-        *string_rounds = world_control().string_rounds;
-        *cached_rounds = world_control().cached_rounds;
+        ControlChannel *ch = standalone_control().get();
+        if (Registry::get().initialized() && Registry::get().world()->control())
+            ch = Registry::get().world()->control();
+        *string_rounds = ch->string_rounds;
+        *cached_rounds = ch->cached_rounds;
     });
 }
 
 int ddl_control_negotiate(const char *keys, char *out, size_t len) {
+    return guarded([&] { negotiate_keys(*standalone_control(), keys, out, len); });
+}
+
+// ---- handle-based control channels (several token rings in one process: tools, CPU tests) ----
+long long ddl_control_channel_open(char *endpoint_out, size_t len) {
+    long long h = 0;
+    int st = guarded([&] {
+        auto ch = std::make_shared<ControlChannel>();
+        std::string ep = ch->listen();
+        DDL_REQUIRE(endpoint_out && len > ep.size(), DDL_STATUS_INVALID_ARGUMENT, "endpoint buffer too small");
+        std::memcpy(endpoint_out, ep.c_str(), ep.size() + 1);
+        std::lock_guard<std::mutex> g(channels_mu());
+        h = reinterpret_cast<long long>(ch.get());
+        channels()[h] = ch;
+    });
+    return st == DDL_STATUS_OK ? h : 0;
+}
+
+int ddl_control_channel_connect(long long h, int rank, int size, const char *endpoints) {
     return guarded([&] {
-        DDL_REQUIRE(keys && out && len > 0, DDL_STATUS_INVALID_ARGUMENT, "bad negotiate args");
-        ControlChannel &ch = world_control();
-        DDL_REQUIRE(ch.connected(), DDL_STATUS_NOT_INITIALIZED, "control channel not connected");
-        std::vector<std::string> mine;
-        std::string s(keys);
-        size_t pos = 0;
-        while (pos < s.size()) {
-            size_t nl = s.find('\n', pos);
-            if (nl == std::string::npos) nl = s.size();
-            if (nl > pos) mine.push_back(std::string(request_type_name(kReqAllreduce)) + "::" + s.substr(pos, nl - pos));
-            pos = nl + 1;
-        }
-        std::sort(mine.begin(), mine.end());
-        mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
-        // this rank's ids by table index, as the handler keeps them
-        std::vector<uint8_t> held(ch.cache.size(), 0);
-        std::vector<uint32_t> idx;
-        bool cached = !mine.empty();
-        for (const auto &k : mine) {
-            uint32_t i;
-            if (ch.cache.lookup(k, &i)) {
-                held[i] = 1;
-                idx.push_back(i);
-            } else {
-                cached = false;
-            }
-        }
-        Agreed a;
-        if (ch.rank() == 0) {
-            a = negotiate_root(ch, cached, idx, mine);
-            negotiate_root_finish(ch);
-        } else {
-            Token t;
-            ch.recv(t, -1);
-            a = negotiate_member(
-                ch, t,
-                [&](const std::vector<std::string> &proposed) {
-                    std::vector<std::string> both;
-                    for (const auto &k : proposed)
-                        if (std::binary_search(mine.begin(), mine.end(), k)) both.push_back(k);
-                    return both;
-                },
-                [&](const std::vector<uint32_t> &proposed) {
-                    std::vector<uint32_t> both;
-                    for (uint32_t i : proposed)
-                        if (i < held.size() && held[i]) both.push_back(i);
-                    return both;
-                });
-        }
-        std::vector<std::string> agreed;
-        if (a.cached) {
-            for (uint32_t i : a.idx) agreed.push_back(ch.cache.at(i));
-            std::sort(agreed.begin(), agreed.end());
-        } else {
-            agreed = a.wire;
-            ch.cache.learn(agreed);
-        }
-        std::string res;
-        for (const auto &k : agreed) res.append(k.substr(k.find("::") + 2)).append("\n");
-        DDL_REQUIRE(res.size() < len, DDL_STATUS_INVALID_ARGUMENT, "output buffer too small");
-        std::memcpy(out, res.c_str(), res.size() + 1);
+        DDL_REQUIRE(endpoints, DDL_STATUS_INVALID_ARGUMENT, "null endpoints");
+        channel(h)->connect(rank, size, split_endpoints(endpoints), 120000);
+    });
+}
+
+int ddl_control_channel_negotiate(long long h, const char *keys, char *out, size_t len) {
+    return guarded([&] { negotiate_keys(*channel(h), keys, out, len); });
+}
+
+int ddl_control_channel_close(long long h) {
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(channels_mu());
+        DDL_REQUIRE(channels().erase(h) == 1, DDL_STATUS_INVALID_ARGUMENT, "unknown control channel " << h);
     });
 }
 
 int ddl_finalize(void) {
     return guarded([&] {
         Registry::get().clear();
-        world_control().close_all();
+        standalone_control() = std::make_shared<ControlChannel>();
+        std::lock_guard<std::mutex> g(channels_mu());
+        channels().clear();
     });
 }
 
@@ -250,6 +299,9 @@ int ddl_set_config(const char *key, long long value) {
         else if (k == "host_chunk_bytes") {
             DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
             c.host_chunk_bytes = value;
+        } else if (k == "host_copy_threads") {
+            DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
+            c.host_copy_threads = value;
         } else if (k == "tune") c.tune = value ? 1 : 0;
         else if (k == "fusion_pipeline_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
@@ -274,6 +326,7 @@ long long ddl_get_config(const char *key) {
     if (k == "cycle_time_us") return c.cycle_time_us;
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
     if (k == "tune") return c.tune;
+    if (k == "host_copy_threads") return c.host_copy_threads;
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "reference_order") return c.reference_order;
@@ -445,9 +498,18 @@ int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int
     });
 }
 
-int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
-                         size_t elements, int dtype, int op, void *hip_stream, ddl_done_fn done,
-                         void *user) {
+namespace {
+// The submitter's input-ready event: device requests are ordered after hip_stream's current
+// position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
+std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
+    DDL_REQUIRE(memory == DDL_MEMORY_DEVICE || memory == DDL_MEMORY_HOST, DDL_STATUS_INVALID_ARGUMENT,
+                "memory must be DDL_MEMORY_DEVICE (0) or DDL_MEMORY_HOST (1), not " << memory);
+    return memory == DDL_MEMORY_HOST ? nullptr : std::make_shared<ReadyEvent>(as_stream(hip_stream));
+}
+}  // namespace
+
+int ddl_allreduce_submit_mem(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                             int dtype, int op, int memory, void *hip_stream, ddl_done_fn done, void *user) {
     return guarded([&] {
         DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
         auto c = Registry::get().find(id);
@@ -461,13 +523,19 @@ int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in
         r.op = op;
         r.done = done;
         r.user = user;
-        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        r.host = memory == DDL_MEMORY_HOST;
+        r.ready = ready_event(memory, hip_stream);
         c->handler().submit(r);
     });
 }
 
-int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
-                         int dtype, int root, void *hip_stream, ddl_done_fn done, void *user) {
+int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                         int dtype, int op, void *hip_stream, ddl_done_fn done, void *user) {
+    return ddl_allreduce_submit_mem(id, key, in, out, elements, dtype, op, DDL_MEMORY_DEVICE, hip_stream, done, user);
+}
+
+int ddl_broadcast_submit_mem(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                             int dtype, int root, int memory, void *hip_stream, ddl_done_fn done, void *user) {
     return guarded([&] {
         DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
         auto c = Registry::get().find(id);
@@ -482,13 +550,21 @@ int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in
         r.root = root;
         r.done = done;
         r.user = user;
-        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        r.host = memory == DDL_MEMORY_HOST;
+        r.ready = ready_event(memory, hip_stream);
         c->handler().submit(r);
     });
 }
 
-int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in, size_t first_dim, size_t row_elements,
-                         int dtype, void *hip_stream, ddl_alloc_fn alloc, ddl_done_fn done, void *user) {
+int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                         int dtype, int root, void *hip_stream, ddl_done_fn done, void *user) {
+    return ddl_broadcast_submit_mem(id, key, in, out, elements, dtype, root, DDL_MEMORY_DEVICE, hip_stream, done,
+                                    user);
+}
+
+int ddl_allgather_submit_mem(ddl_communicator_id id, const char *key, const void *in, size_t first_dim,
+                             size_t row_elements, int dtype, int memory, void *hip_stream, ddl_alloc_fn alloc,
+                             ddl_done_fn done, void *user) {
     return guarded([&] {
         DDL_REQUIRE(key, DDL_STATUS_INVALID_ARGUMENT, "null key");
         auto c = Registry::get().find(id);
@@ -504,21 +580,28 @@ int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in
         r.alloc = alloc;
         r.done = done;
         r.user = user;
-        r.ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        r.host = memory == DDL_MEMORY_HOST;
+        r.ready = ready_event(memory, hip_stream);
         c->handler().submit(r);
     });
 }
 
-int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys, const void *const *ins,
-                               void *const *outs, const size_t *elements, const int *dtypes, int op,
-                               void *hip_stream, ddl_done_fn done, void *const *users) {
+int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in, size_t first_dim, size_t row_elements,
+                         int dtype, void *hip_stream, ddl_alloc_fn alloc, ddl_done_fn done, void *user) {
+    return ddl_allgather_submit_mem(id, key, in, first_dim, row_elements, dtype, DDL_MEMORY_DEVICE, hip_stream, alloc,
+                                    done, user);
+}
+
+int ddl_allreduce_submit_batch_mem(ddl_communicator_id id, int count, const char *const *keys, const void *const *ins,
+                                   void *const *outs, const size_t *elements, const int *dtypes, int op, int memory,
+                                   void *hip_stream, ddl_done_fn done, void *const *users) {
     return guarded([&] {
         DDL_REQUIRE(count >= 0 && (count == 0 || (keys && ins && outs && elements && dtypes)),
                     DDL_STATUS_INVALID_ARGUMENT, "bad batch arguments");
         if (count == 0) return;
         auto c = Registry::get().find(id);
         DeviceGuard g(c->device());
-        auto ready = std::make_shared<ReadyEvent>(as_stream(hip_stream));
+        auto ready = ready_event(memory, hip_stream);
         std::vector<Request> rs(count);
         for (int i = 0; i < count; ++i) {
             DDL_REQUIRE(keys[i], DDL_STATUS_INVALID_ARGUMENT, "null key " << i);
@@ -530,10 +613,18 @@ int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *co
             rs[i].op = op;
             rs[i].done = done;
             rs[i].user = users ? users[i] : nullptr;
+            rs[i].host = memory == DDL_MEMORY_HOST;
             rs[i].ready = ready;
         }
         c->handler().submit_batch(rs);
     });
+}
+
+int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys, const void *const *ins,
+                               void *const *outs, const size_t *elements, const int *dtypes, int op,
+                               void *hip_stream, ddl_done_fn done, void *const *users) {
+    return ddl_allreduce_submit_batch_mem(id, count, keys, ins, outs, elements, dtypes, op, DDL_MEMORY_DEVICE,
+                                          hip_stream, done, users);
 }
 
 int ddl_kernel_timing(ddl_communicator_id id, int on) {
@@ -648,6 +739,136 @@ int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recv
         DDL_REQUIRE(sends && recvs && counts && displs, DDL_STATUS_INVALID_ARGUMENT, "null argument");
         (void)current_device();
         local_world(nranks).allgatherv(sends, recvs, counts, displs, dtype, as_stream(hip_stream));
+    });
+}
+
+// ---- RCCL loopback (one GPU, real RCCL transport) --------------------------------------------
+int ddl_rccl_loopback_init(int device) {
+    return guarded([&] {
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        DDL_REQUIRE(l.comm == nullptr, DDL_STATUS_INVALID_ARGUMENT, "RCCL loopback already initialized");
+        DDL_HIP(hipSetDevice(device));
+        char uid[sizeof(ncclUniqueId)];
+        DDL_REQUIRE(ddl_get_unique_id(uid, sizeof uid) == DDL_STATUS_OK, DDL_STATUS_COMM_ERROR, last_error());
+        l.comm = rccl_init_rank(0, 1, uid, sizeof uid);
+        l.owned.push_back(l.comm);
+    });
+}
+
+int ddl_rccl_loopback_split(int color, int key, int *rank, int *size) {
+    return guarded([&] {
+        DDL_REQUIRE(rank && size, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        DDL_REQUIRE(l.comm != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_rccl_loopback_init has not been called");
+        *rank = -1;
+        *size = 0;
+        ncclComm_t nc = rccl_split(l.comm, color, key, rank, size);
+        if (!nc) return;  // color < 0: in no communicator; the current one stays
+        l.owned.push_back(nc);
+        l.comm = nc;
+    });
+}
+
+int ddl_rccl_loopback_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements, int dtype,
+                                void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        DDL_REQUIRE(sends && recvs, DDL_STATUS_INVALID_ARGUMENT, "null buffer arrays");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        l.world(nranks).allreduce(sends, recvs, elements, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_rccl_loopback_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
+                                void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && root >= 0 && root < nranks && bufs, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad loopback broadcast");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        l.world(nranks).broadcast(bufs, elements, dtype, root, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                                 const size_t *displs, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && sends && recvs && counts && displs, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad loopback allgatherv");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        l.world(nranks).allgatherv(sends, recvs, counts, displs, dtype, as_stream(hip_stream));
+    });
+}
+
+int ddl_rccl_loopback_max(float *values, int count, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(values, DDL_STATUS_INVALID_ARGUMENT, "null values");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        DDL_REQUIRE(l.comm != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_rccl_loopback_init has not been called");
+        rccl_max_floats(l.comm, values, count, as_stream(hip_stream));
+    });
+}
+
+int ddl_rccl_loopback_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
+                           long long *configs, float *ms, int max_candidates) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 2 && nranks <= 16, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
+        const size_t es = dtype_size(dtype), bytes = elements * es;
+        DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+        DDL_REQUIRE(elements > 0, DDL_STATUS_INVALID_ARGUMENT, "empty bucket");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        hipStream_t stream = as_stream(hip_stream);
+        std::vector<void *> bufs(2 * nranks, nullptr);
+        auto release = [&] {
+            (void)hipStreamSynchronize(stream);
+            for (void *p : bufs)
+                if (p) (void)hipFree(p);
+        };
+        TuneResult r;
+        try {
+            for (void *&p : bufs) {
+                DDL_HIP(hipMalloc(&p, bytes));
+                DDL_HIP(hipMemsetAsync(p, 0, bytes, stream));
+            }
+            LocalWorld &w = l.world(nranks);
+            // the candidates run through RCCL; the agreement is the product's ncclAllReduce(MAX)
+            r = run_tuning(
+                nranks, bytes, stream, config().ring(),
+                [&](const RingConfig &c) { w.allreduce(bufs.data(), bufs.data() + nranks, elements, dtype, stream, c); },
+                [&](float *v, int nc) { rccl_max_floats(l.comm, v, nc, stream); });
+        } catch (...) {
+            release();
+            throw;
+        }
+        release();
+        export_tune(r, chosen, count, configs, ms, max_candidates);
+    });
+}
+
+int ddl_rccl_loopback_stats(int nranks, long long *pairs) {
+    return guarded([&] {
+        DDL_REQUIRE(pairs, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        *pairs = l.world(nranks).loopback_pairs();
+    });
+}
+
+int ddl_rccl_loopback_finalize(void) {
+    return guarded([&] {
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        (void)hipDeviceSynchronize();
+        l.worlds.clear();
+        for (auto it = l.owned.rbegin(); it != l.owned.rend(); ++it) (void)rccl().CommDestroy(*it);
+        l.owned.clear();
+        l.comm = nullptr;
     });
 }
 

@@ -1,6 +1,7 @@
 // engine.cpp — communicators, registry, config, logging, errors.
 #include "engine.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -57,19 +58,26 @@ DeviceGuard::~DeviceGuard() {
 
 // ---- communicator -----------------------------------------------------------------------------
 Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks,
-                           long long tag)
-    : rank_(rank), size_(size), device_(device), nccl_(nccl), hooks_(std::move(hooks)), tag_(tag) {
+                           long long tag, std::vector<int> world_ranks)
+    : rank_(rank), size_(size), device_(device), nccl_(nccl), hooks_(std::move(hooks)), tag_(tag),
+      world_ranks_(std::move(world_ranks)) {
     DeviceGuard g(device_);
     std::unique_ptr<Transport> t;
     if (size_ > 1) {
-        if (hooks_) t.reset(new CallbackTransport(hooks_, tag_));
-        else t.reset(new RcclTransport(nccl_));
+        if (hooks_) {
+            cb_ = new CallbackTransport(hooks_, tag_, world_ranks_);
+            t.reset(cb_);
+        } else {
+            t.reset(new RcclTransport(nccl_));
+        }
     }
     exec_.reset(new RingExecutor(rank_, size_, device_, std::move(t)));
 }
 
 Communicator::~Communicator() {
-    handler_.reset();
+    handler_.reset();  // stops the handler thread (its SHUT_DOWN lap uses control_)
+    keyed_data_.reset();
+    control_.reset();
     exec_.reset();
     for (void *s : slots_)
         if (s) (void)hipFree(s);
@@ -189,32 +197,21 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
 TuneResult Communicator::tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base) {
     const size_t bytes = n * dtype_size(dtype);
     void *a = nullptr, *b = nullptr;
-    float *dms = nullptr;
     auto cleanup = [&] {
         (void)hipStreamSynchronize(stream);
         if (a) (void)hipFree(a);
         if (b) (void)hipFree(b);
-        if (dms) (void)hipFree(dms);
     };
     TuneResult res;
     try {
         DDL_HIP(hipMalloc(&a, bytes));
         DDL_HIP(hipMalloc(&b, bytes));
-        DDL_HIP(hipMalloc(&dms, sizeof(float) * 64));
         DDL_HIP(hipMemsetAsync(a, 0, bytes, stream));
         res = run_tuning(
             size_, bytes, stream, base, [&](const RingConfig &c) { exec_->allreduce(a, b, n, dtype, stream, c); },
             [&](float *ms, int nc) {
                 DDL_REQUIRE(nc <= 64, DDL_STATUS_ERROR_UNKNOWN, "too many tuning candidates");
-                if (hooks_) {
-                    DDL_REQUIRE(hooks_->max(tag_, ms, nc, hooks_->user) == 0, DDL_STATUS_COMM_ERROR,
-                                "test transport: max callback failed");
-                    return;
-                }
-                DDL_HIP(hipMemcpyAsync(dms, ms, sizeof(float) * nc, hipMemcpyHostToDevice, stream));
-                rccl_check(rccl().AllReduce(dms, dms, nc, ncclFloat32, ncclMax, nccl_, stream), "ncclAllReduce(tune)");
-                DDL_HIP(hipMemcpyAsync(ms, dms, sizeof(float) * nc, hipMemcpyDeviceToHost, stream));
-                DDL_HIP(hipStreamSynchronize(stream));
+                agree_max_(ms, nc, stream);
             });
     } catch (...) {
         cleanup();
@@ -362,23 +359,179 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 }
 
-std::shared_ptr<Communicator> Communicator::split(int color, int key) {
+void Communicator::agree_max_(float *values, int count, hipStream_t stream) {
+    if (size_ <= 1) return;
+    if (!hooks_) {
+        rccl_max_floats(nccl_, values, count, stream);
+        return;
+    }
+    // test transport: every member sends its values to every other member (one group), then
+    // each takes the elementwise max — the same numbers on every rank
+    std::vector<std::vector<float>> got(size_, std::vector<float>(values, values + count));
+    std::vector<ddl_p2p_op> ops;
+    for (int d = 1; d < size_; ++d) {
+        const int to = (rank_ + d) % size_, from = (rank_ + size_ - d) % size_;
+        ops.push_back(ddl_p2p_op{1, to, 4001, values, sizeof(float) * count});
+        ops.push_back(ddl_p2p_op{0, from, 4001, got[from].data(), sizeof(float) * count});
+    }
+    cb_->host_group(ops);
+    for (int q = 0; q < size_; ++q)
+        for (int i = 0; i < count; ++i) values[i] = std::max(values[i], got[q][i]);
+}
+
+namespace {
+// One rank's contribution to a split: MPI_Comm_split's (color, key) plus what the new
+// communicator needs agreed (the test transport's next tag, the token ring endpoint).
+struct SplitRecord {
+    int64_t color, key, tag;
+    char endpoint[40];
+};
+static_assert(sizeof(SplitRecord) == 64, "split record is 8 int64 on the wire");
+}  // namespace
+
+std::shared_ptr<Communicator> Communicator::split(int color, int key, bool keyed) {
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
-    if (size_ == 1) return std::make_shared<Communicator>(0, 1, device_, nullptr);
-    if (hooks_) {  // test transport: the handler's private copy of this communicator
-        DDL_REQUIRE(color >= 0 && key == rank_, DDL_STATUS_INVALID_ARGUMENT,
-                    "test transport: split needs one color on every rank and key = rank");
-        return std::make_shared<Communicator>(rank_, size_, device_, nullptr, hooks_, hooks_->next_tag.fetch_add(1));
+    // 1) every rank's record, in rank order, over this communicator's data plane (an allgather,
+    //    as MPI_Comm_split does inside MPI)
+    std::shared_ptr<ControlChannel> ring;
+    SplitRecord mine{};
+    mine.color = color < 0 ? -1 : color;
+    mine.key = key;
+    mine.tag = hooks_ ? hooks_->next_tag.load() : 0;
+    if (keyed && color >= 0 && size_ > 1) {
+        ring = std::make_shared<ControlChannel>();
+        const std::string ep = ring->listen();
+        DDL_REQUIRE(ep.size() < sizeof mine.endpoint, DDL_STATUS_ERROR_UNKNOWN, "endpoint too long: " << ep);
+        std::memcpy(mine.endpoint, ep.c_str(), ep.size() + 1);
     }
+    std::vector<SplitRecord> all(size_);
+    all[rank_] = mine;
+    if (size_ > 1) {
+        void *d = nullptr;
+        hipStream_t s = nullptr;
+        auto release = [&] {
+            if (s) (void)hipStreamSynchronize(s);
+            if (d) (void)hipFree(d);
+            if (s) (void)hipStreamDestroy(s);
+        };
+        try {
+            DDL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            DDL_HIP(hipMalloc(&d, sizeof(SplitRecord) * size_));
+            char *base = static_cast<char *>(d);
+            DDL_HIP(hipMemcpyAsync(base + sizeof(SplitRecord) * rank_, &mine, sizeof mine, hipMemcpyHostToDevice, s));
+            std::vector<size_t> cnt(size_, sizeof(SplitRecord) / 8), dsp(size_);
+            for (int q = 0; q < size_; ++q) dsp[q] = q * (sizeof(SplitRecord) / 8);
+            exec_->allgatherv(base + sizeof(SplitRecord) * rank_, base, cnt.data(), dsp.data(), DDL_INT64, s);
+            DDL_HIP(hipMemcpyAsync(all.data(), d, sizeof(SplitRecord) * size_, hipMemcpyDeviceToHost, s));
+            DDL_HIP(hipStreamSynchronize(s));
+        } catch (...) {
+            release();
+            throw;
+        }
+        release();
+    }
+    // 2) the members of my color, ordered by (key, rank here)
+    std::vector<int> members;
+    int64_t tag = 0;
+    for (int q = 0; q < size_; ++q) {
+        tag = std::max(tag, all[q].tag);
+        if (color >= 0 && all[q].color == color) members.push_back(q);
+    }
+    std::stable_sort(members.begin(), members.end(), [&](int a, int b) { return all[a].key < all[b].key; });
+    const int me = (int)(std::find(members.begin(), members.end(), rank_) - members.begin());
+    const int s = (int)members.size();
+    // 3) the data plane of the new communicator
+    std::shared_ptr<Communicator> c;
+    if (hooks_) {
+        // tags only need to differ between communicators that share a pair of ranks: the max
+        // over this communicator's ranks is above every tag any member has used
+        long long want = tag + 1, cur = hooks_->next_tag.load();
+        while (cur < want && !hooks_->next_tag.compare_exchange_weak(cur, want)) {
+        }
+        DDL_REQUIRE(color >= 0, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
+        std::vector<int> wr;
+        for (int q : members) wr.push_back(world_ranks_.empty() ? q : world_ranks_[q]);
+        c = std::make_shared<Communicator>(me, s, device_, nullptr, s > 1 ? hooks_ : nullptr, tag, wr);
+    } else if (nccl_) {
+        int r = 0, n = 0;
+        ncclComm_t nc = rccl_split(nccl_, color, key, &r, &n);
+        DDL_REQUIRE(nc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
+        DDL_REQUIRE(r == me && n == s, DDL_STATUS_COMM_ERROR,
+                    "ncclCommSplit gave rank " << r << " of " << n << ", the split exchange " << me << " of " << s);
+        c = std::make_shared<Communicator>(r, n, device_, nc);
+    } else {
+        DDL_REQUIRE(color >= 0, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
+        c = std::make_shared<Communicator>(0, 1, device_, nullptr);
+    }
+    // 4) its token ring and keyed data plane (collective over the new communicator)
+    if (keyed && s > 1) {
+        std::vector<std::string> eps;
+        for (int q : members) eps.push_back(std::string(all[q].endpoint));
+        ring->connect(me, s, eps, 120000);
+        c->enable_keyed(ring);
+    }
+    return c;
+}
+
+void Communicator::enable_keyed(std::shared_ptr<ControlChannel> ch) {
+    DDL_REQUIRE(size_ == 1 || (ch && ch->connected() && ch->size() == size_ && ch->rank() == rank_),
+                DDL_STATUS_INVALID_ARGUMENT, "token ring does not match the communicator");
+    control_ = std::move(ch);
+    // private data-plane communicator: the handler thread's collectives never interleave with
+    // the user's calls on this one
+    if (size_ > 1 && !keyed_data_) keyed_data_ = split(0, rank_, false);
+}
+
+ncclComm_t rccl_init_rank(int rank, int size, const void *unique_id, size_t len) {
+    DDL_REQUIRE(unique_id && len >= sizeof(ncclUniqueId), DDL_STATUS_INVALID_ARGUMENT,
+                "unique id of " << sizeof(ncclUniqueId) << " bytes required");
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof id);
     ncclComm_t nc = nullptr;
-    rccl_check(rccl().CommSplit(nccl_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr),
-               "ncclCommSplit");
-    DDL_REQUIRE(nc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
-    int r = 0, s = 0;
-    rccl_check(rccl().CommCount(nc, &s), "ncclCommCount");
-    rccl_check(rccl().CommUserRank(nc, &r), "ncclCommUserRank");
-    return std::make_shared<Communicator>(r, s, device_, nc);
+    rccl_check(rccl().CommInitRank(&nc, size, id, rank), "ncclCommInitRank");
+    return nc;
+}
+
+ncclComm_t rccl_split(ncclComm_t parent, int color, int key, int *rank, int *size) {
+    ncclComm_t nc = nullptr;
+    rccl_check(rccl().CommSplit(parent, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr), "ncclCommSplit");
+    if (!nc) return nullptr;
+    rccl_check(rccl().CommCount(nc, size), "ncclCommCount");
+    rccl_check(rccl().CommUserRank(nc, rank), "ncclCommUserRank");
+    return nc;
+}
+
+void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stream) {
+    DDL_REQUIRE(count > 0 && count <= 1024, DDL_STATUS_INVALID_ARGUMENT, "max of " << count << " floats");
+    float *d = nullptr;
+    DDL_HIP(hipMalloc(&d, sizeof(float) * count));
+    try {
+        DDL_HIP(hipMemcpyAsync(d, values, sizeof(float) * count, hipMemcpyHostToDevice, stream));
+        rccl_check(rccl().AllReduce(d, d, count, ncclFloat32, ncclMax, comm, stream), "ncclAllReduce(max)");
+        DDL_HIP(hipMemcpyAsync(values, d, sizeof(float) * count, hipMemcpyDeviceToHost, stream));
+        DDL_HIP(hipStreamSynchronize(stream));
+    } catch (...) {
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(d);
+        throw;
+    }
+    DDL_HIP(hipFree(d));
+}
+
+RcclLoopback &rccl_loopback() {
+    static RcclLoopback *l = new RcclLoopback();  // leaked: no static-destruction order issues
+    return *l;
+}
+
+LocalWorld &RcclLoopback::world(int nranks) {
+    DDL_REQUIRE(comm != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_rccl_loopback_init has not been called");
+    int dev = 0;
+    DDL_HIP(hipGetDevice(&dev));
+    auto key = std::make_pair(nranks, comm);
+    auto it = worlds.find(key);
+    if (it == worlds.end()) it = worlds.emplace(key, std::unique_ptr<LocalWorld>(new LocalWorld(nranks, dev, comm))).first;
+    return *it->second;
 }
 
 RequestHandler &Communicator::handler() {

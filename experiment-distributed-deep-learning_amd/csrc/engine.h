@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "control.h"
 #include "executor.h"
 
 namespace ddl {
@@ -32,8 +33,11 @@ struct Config {
     // keyed requests: rank 0 waits this long after the first registration before proposing
     // a round (0 = propose at once, as the reference's READY token does)
     std::atomic<long long> cycle_time_us{0};
-    // host-resident pipeline chunk (ddl_allreduce_host)
+    // host-resident pipeline chunk (ddl_allreduce_host, keyed host requests)
     std::atomic<long long> host_chunk_bytes{32ll << 20};
+    // memcpy workers of the keyed host-staging pipeline (pageable <-> pinned), besides the
+    // engine thread itself
+    std::atomic<long long> host_copy_threads{7};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};
@@ -81,9 +85,10 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
 class Communicator : public std::enable_shared_from_this<Communicator> {
 public:
     // `hooks` (test harness only, ddl_init_test_transport): groups go to host callbacks, `tag`
-    // names this communicator to them; nullptr = RCCL on `nccl`.
+    // names this communicator to them, `world_ranks[i]` is the world rank of rank i (empty: the
+    // world itself); nullptr = RCCL on `nccl`.
     Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks = nullptr,
-                 long long tag = 0);
+                 long long tag = 0, std::vector<int> world_ranks = {});
     ~Communicator();
 
     long long id() const { return reinterpret_cast<long long>(this); }
@@ -108,7 +113,14 @@ public:
     // elements land at recv + displs[q] on every rank; `send` holds counts[rank()] elements.
     void allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
                     hipStream_t stream);
-    std::shared_ptr<Communicator> split(int color, int key);
+    // MPI_Comm_split (MPICommunicator.cc:92-101), collective over this communicator: ranks of one
+    // color form a communicator ordered by (key, rank here); color < 0 joins none (fails after
+    // taking part). The members exchange (color, key, control endpoint) over this
+    // communicator's data plane; with `keyed` a new communicator of more than one rank also gets
+    // its own token ring over TCP and its private data-plane communicator for keyed requests, as
+    // the reference gives every communicator its own handler and token ring
+    // (RingTokenCommunicateController.cc:53-79, MPIRingTokenCommunication.cc:50-57).
+    std::shared_ptr<Communicator> split(int color, int key, bool keyed = true);
 
     // The schedule for an n-element bucket: the tuned choice for its size class (tuning it now,
     // collectively, if this is the class's first bucket), or the configured one.
@@ -116,17 +128,31 @@ public:
     // Tuning result for the size class of `bytes` (chosen = -1 if not tuned yet).
     TuneResult tune_result(size_t bytes);
 
+    // Keyed requests: the handler (created on first use; not collective), this communicator's
+    // token ring and the private data-plane communicator its handler reduces on.
     RequestHandler &handler();
+    ControlChannel *control() const { return control_.get(); }
+    // Collective over this communicator: adopts `ch` (already connected over these ranks) as the
+    // token ring and creates the keyed data-plane communicator (world: ddl_control_connect).
+    void enable_keyed(std::shared_ptr<ControlChannel> ch);
+    std::shared_ptr<Communicator> keyed_data() const { return keyed_data_; }
     RingExecutor &executor() { return *exec_; }
     std::mutex &mutex() { return mu_; }
 
 private:
+    // elementwise max of host floats over the ranks (the autotuner's agreement)
+    void agree_max_(float *values, int count, hipStream_t stream);
+
     int rank_, size_, device_;
     ncclComm_t nccl_;
     std::shared_ptr<TestHooks> hooks_;
     long long tag_ = 0;
+    std::vector<int> world_ranks_;
+    CallbackTransport *cb_ = nullptr;  // the executor's transport when hooks_ (owned by exec_)
     std::mutex mu_;  // one collective at a time per communicator (RCCL ordering)
     std::unique_ptr<RingExecutor> exec_;
+    std::shared_ptr<ControlChannel> control_;
+    std::shared_ptr<Communicator> keyed_data_;
     std::unique_ptr<RequestHandler> handler_;
     std::mutex handler_mu_;
     std::map<int, TuneResult> tuned_;  // by floor(log2(bucket bytes)); guarded by mu_
@@ -167,5 +193,26 @@ private:
 };
 
 LocalWorld &local_world(int nranks);
+
+// ---- RCCL pieces shared by the product path and the one-GPU loopback tests ---------------------
+// ncclCommInitRank of `rank` in a `size`-rank communicator from a 128-byte ncclUniqueId.
+ncclComm_t rccl_init_rank(int rank, int size, const void *unique_id, size_t len);
+// ncclCommSplit (MPI_Comm_split, MPICommunicator.cc:92-101): nullptr when color < 0 (the rank is
+// in no communicator); *rank / *size of the new communicator from ncclCommUserRank / Count.
+ncclComm_t rccl_split(ncclComm_t parent, int color, int key, int *rank, int *size);
+// Elementwise max over the communicator's ranks of `count` host floats (the autotuner's
+// agreement step: one ncclAllReduce(MAX) on `stream`, host-synchronising).
+void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stream);
+
+// One-rank RCCL communicator driving P virtual ranks' programs through RcclTransport (self
+// send/recv pairs) — test / diagnostic path (ddl_rccl_loopback_*), never used by ddl_init.
+struct RcclLoopback {
+    std::mutex mu;
+    ncclComm_t comm = nullptr;                  // current (the last split, or the initial comm)
+    std::vector<ncclComm_t> owned;              // every communicator created, destroyed at finalize
+    std::map<std::pair<int, ncclComm_t>, std::unique_ptr<LocalWorld>> worlds;  // (P, comm)
+    LocalWorld &world(int nranks);
+};
+RcclLoopback &rccl_loopback();
 
 }  // namespace ddl

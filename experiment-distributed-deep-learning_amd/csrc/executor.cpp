@@ -31,11 +31,21 @@ void CallbackTransport::group(const std::vector<P2POp> &ops, hipStream_t stream)
             DDL_HIP(hipMemcpy(host[i].data(), ops[i].ptr, ops[i].bytes, hipMemcpyDeviceToHost));
         v[i] = ddl_p2p_op{ops[i].send ? 1 : 0, ops[i].peer, ops[i].tag, host[i].data(), ops[i].bytes};
     }
-    const int rc = hooks_->group(tag_, v.data(), (int)v.size(), hooks_->user);
-    DDL_REQUIRE(rc == 0, DDL_STATUS_COMM_ERROR, "test transport: group callback failed (" << rc << ")");
+    host_group(v);
     for (size_t i = 0; i < ops.size(); ++i)
         if (!ops[i].send && ops[i].bytes)
             DDL_HIP(hipMemcpy(ops[i].ptr, host[i].data(), ops[i].bytes, hipMemcpyHostToDevice));
+}
+
+void CallbackTransport::host_group(std::vector<ddl_p2p_op> &ops) {
+    if (ops.empty()) return;
+    for (ddl_p2p_op &o : ops) {
+        if (world_ranks_.empty()) continue;
+        DDL_REQUIRE(o.peer >= 0 && o.peer < (int)world_ranks_.size(), DDL_STATUS_ERROR_UNKNOWN, "bad peer " << o.peer);
+        o.peer = world_ranks_[o.peer];
+    }
+    const int rc = hooks_->group(tag_, ops.data(), (int)ops.size(), hooks_->user);
+    DDL_REQUIRE(rc == 0, DDL_STATUS_COMM_ERROR, "test transport: group callback failed (" << rc << ")");
 }
 
 RankResources::RankResources(int dev) : device(dev) {
@@ -207,9 +217,30 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
 }
 
-LocalWorld::LocalWorld(int nranks, int device) : P_(nranks) {
+LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks) {
     for (int r = 0; r < nranks; ++r) res_.emplace_back(new RankResources(device));
     progs_.resize(nranks);
+    if (loopback) {
+        loop_.reset(new RcclTransport(loopback));
+        DDL_HIP(hipStreamCreateWithFlags(&loop_stream_, hipStreamNonBlocking));
+    }
+}
+
+LocalWorld::~LocalWorld() {
+    for (hipEvent_t e : loop_ev_) (void)hipEventDestroy(e);
+    if (loop_stream_) (void)hipStreamDestroy(loop_stream_);
+}
+
+const P2POp &LocalWorld::match_(int r, size_t t, const P2POp &op, std::map<std::pair<int, int>, int> &seen) const {
+    int skip = seen[std::make_pair(op.peer, op.tag)]++;
+    for (const P2POp &o : progs_[op.peer].ticks[t].ops)
+        if (o.send && o.peer == r && o.tag == op.tag && skip-- == 0) {
+            DDL_REQUIRE(o.bytes == op.bytes, DDL_STATUS_ERROR_UNKNOWN,
+                        "local world: recv of " << op.bytes << " B matches a send of " << o.bytes << " B");
+            return o;
+        }
+    fail(DDL_STATUS_ERROR_UNKNOWN, "local world: unmatched recv rank " + std::to_string(r) + " tick " +
+                                       std::to_string(t) + " tag " + std::to_string(op.tag));
 }
 
 void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, int dtype,
@@ -249,6 +280,11 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         DDL_REQUIRE(progs_[r].ticks.size() == T, DDL_STATUS_ERROR_UNKNOWN, "local world: tick counts differ");
         res_[r]->ensure_events(T);
     }
+    while (loop_ && loop_ev_.size() < T) {
+        hipEvent_t e;
+        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        loop_ev_.push_back(e);
+    }
     hipEvent_t fork = res_[0]->fork_ev;
     DDL_HIP(hipEventRecord(fork, user));
     for (int r = 0; r < P_; ++r) {
@@ -268,33 +304,48 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, rr.comm));
             DDL_HIP(hipEventRecord(rr.pre_ev[t], rr.comm));
         }
-        // 2) receives: copy from the matching send of the peer, once the peer reached the tick
-        //    (the k-th recv from a peer with a tag matches the k-th send to us with that tag,
-        //    as RCCL matches p2p operations between a pair in posting order)
-        for (int r = 0; r < P_; ++r) {
-            RankResources &rr = *res_[r];
-            std::map<std::pair<int, int>, int> seen;
-            for (const P2POp &op : progs_[r].ticks[t].ops) {
-                if (op.send) continue;
-                int skip = seen[std::make_pair(op.peer, op.tag)]++;
-                const P2POp *match = nullptr;
-                for (const P2POp &o : progs_[op.peer].ticks[t].ops)
-                    if (o.send && o.peer == r && o.tag == op.tag && skip-- == 0) {
-                        match = &o;
-                        break;
-                    }
-                DDL_REQUIRE(match && match->bytes == op.bytes, DDL_STATUS_ERROR_UNKNOWN,
-                            "local world: unmatched recv rank " << r << " tick " << t << " tag " << op.tag);
-                DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->pre_ev[t], 0));
-                DDL_HIP(hipMemcpyAsync(op.ptr, match->ptr, op.bytes, hipMemcpyDeviceToDevice, rr.comm));
+        if (loop_) {
+            // 2') every matched pair of the tick through RCCL as a self send / self recv, posted
+            //     in matching order in one group on the transport stream, which waits for every
+            //     rank to reach the tick; every rank's comm stream then waits for the group
+            std::vector<P2POp> pairs;
+            for (int r = 0; r < P_; ++r) {
+                std::map<std::pair<int, int>, int> seen;
+                for (const P2POp &op : progs_[r].ticks[t].ops) {
+                    if (op.send) continue;
+                    const P2POp &s = match_(r, t, op, seen);
+                    pairs.push_back(P2POp{true, 0, op.tag, s.ptr, s.bytes});
+                    pairs.push_back(P2POp{false, 0, op.tag, op.ptr, op.bytes});
+                }
             }
-            DDL_HIP(hipEventRecord(rr.post_ev[t], rr.comm));
-        }
-        // 3) a group completes for the sender only once its receivers have the data
-        for (int r = 0; r < P_; ++r) {
-            RankResources &rr = *res_[r];
-            for (const P2POp &op : progs_[r].ticks[t].ops)
-                if (op.send) DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->post_ev[t], 0));
+            if (!pairs.empty()) {
+                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(loop_stream_, res_[r]->pre_ev[t], 0));
+                loop_->group(pairs, loop_stream_);
+                DDL_HIP(hipEventRecord(loop_ev_[t], loop_stream_));
+                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, loop_ev_[t], 0));
+                loop_pairs_ += (long long)pairs.size() / 2;
+            }
+        } else {
+            // 2) receives: copy from the matching send of the peer, once the peer reached the tick
+            //    (the k-th recv from a peer with a tag matches the k-th send to us with that tag,
+            //    as RCCL matches p2p operations between a pair in posting order)
+            for (int r = 0; r < P_; ++r) {
+                RankResources &rr = *res_[r];
+                std::map<std::pair<int, int>, int> seen;
+                for (const P2POp &op : progs_[r].ticks[t].ops) {
+                    if (op.send) continue;
+                    const P2POp &match = match_(r, t, op, seen);
+                    DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->pre_ev[t], 0));
+                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, rr.comm));
+                }
+                DDL_HIP(hipEventRecord(rr.post_ev[t], rr.comm));
+            }
+            // 3) a group completes for the sender only once its receivers have the data
+            for (int r = 0; r < P_; ++r) {
+                RankResources &rr = *res_[r];
+                for (const P2POp &op : progs_[r].ticks[t].ops)
+                    if (op.send) DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->post_ev[t], 0));
+            }
         }
         // 4) reduce of the received slices
         for (int r = 0; r < P_; ++r) {

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <atomic>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -45,14 +46,20 @@ struct TestHooks {
 
 // Synchronises the stream, stages the sends in host memory, runs the callback, copies the
 // received bytes to the device: the group is complete, in stream order, when group() returns.
+// Peers are ranks of the communicator; the callback sees world ranks (world_ranks[peer], or the
+// peer itself when world_ranks is empty).
 class CallbackTransport : public Transport {
 public:
-    CallbackTransport(std::shared_ptr<TestHooks> hooks, long long tag) : hooks_(std::move(hooks)), tag_(tag) {}
+    CallbackTransport(std::shared_ptr<TestHooks> hooks, long long tag, std::vector<int> world_ranks)
+        : hooks_(std::move(hooks)), tag_(tag), world_ranks_(std::move(world_ranks)) {}
     void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
+    // One group of host-buffer operations straight to the callback (no device staging).
+    void host_group(std::vector<ddl_p2p_op> &ops);
 
 private:
     std::shared_ptr<TestHooks> hooks_;
     long long tag_;
+    std::vector<int> world_ranks_;
 };
 
 // Streams, events and staging memory of one rank (reused across calls).
@@ -114,21 +121,37 @@ private:
 
 // P virtual ranks in one process on one GPU: the same per-rank programs, with
 // device-to-device copies standing in for RCCL send/recv (matched by peer and ring tag).
+//
+// With `loopback` (a one-rank RCCL communicator) the bytes move through RCCL instead: each
+// tick's matched send/recv pairs of all P virtual ranks are posted through RcclTransport::group
+// as self-send / self-recv pairs in matching order (RCCL pairs the k-th send to a peer with the
+// k-th receive from it), on a transport stream that waits for every rank to reach the tick.
+// That runs the production transport code on one GPU (test / diagnostic path).
 class LocalWorld {
 public:
-    LocalWorld(int nranks, int device);
+    LocalWorld(int nranks, int device, ncclComm_t loopback = nullptr);
+    ~LocalWorld();
     void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
     void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
     void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
                     int dtype, hipStream_t user);
+    // self pairs posted through RCCL since construction (loopback only)
+    long long loopback_pairs() const { return loop_pairs_; }
 
 private:
     void run_(int dtype, hipStream_t user);
+    // the matching send of rank r's recv `op` at tick t (k-th recv from a (peer, tag) pairs with
+    // the peer's k-th send to r with that tag)
+    const P2POp &match_(int r, size_t t, const P2POp &op, std::map<std::pair<int, int>, int> &seen) const;
 
     int P_;
     std::vector<std::unique_ptr<RankResources>> res_;
     std::vector<RingProgram> progs_;
+    std::unique_ptr<RcclTransport> loop_;
+    hipStream_t loop_stream_ = nullptr;
+    std::vector<hipEvent_t> loop_ev_;
+    long long loop_pairs_ = 0;
 };
 
 // Most recent tick <= w that launched a reduce (-1 if none).

@@ -3,7 +3,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <set>
+#include <tuple>
 
 namespace ddl {
 
@@ -99,21 +101,92 @@ ReadyEvent::~ReadyEvent() {
     if (e) (void)hipEventDestroy(e);
 }
 
-ControlChannel &world_control() {
-    static ControlChannel *ch = new ControlChannel();
+CopyPool::CopyPool(int threads) {
+    for (int i = 0; i < threads; ++i) threads_.emplace_back(&CopyPool::worker_, this);
+}
+
+CopyPool::~CopyPool() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread &t : threads_) t.join();
+}
+
+void CopyPool::worker_() {
+    for (;;) {
+        std::vector<Piece> work;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
+            if (stop_ && queue_.empty()) return;
+            work.swap(queue_.back());
+            queue_.pop_back();
+        }
+        for (const Piece &p : work) std::memcpy(p.dst, p.src, p.bytes);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            --outstanding_;
+        }
+        done_cv_.notify_all();
+    }
+}
+
+void CopyPool::run(const std::vector<Piece> &pieces) {
+    size_t total = 0;
+    for (const Piece &p : pieces) total += p.bytes;
+    const size_t T = threads_.size() + 1;
+    if (threads_.empty() || total < (2u << 20)) {
+        for (const Piece &p : pieces) std::memcpy(p.dst, p.src, p.bytes);
+        return;
+    }
+    // T shares of about total / T bytes each, pieces cut where a share ends
+    const size_t share = (total + T - 1) / T;
+    std::vector<std::vector<Piece>> shares(1);
+    size_t room = share;
+    for (Piece p : pieces) {
+        while (p.bytes) {
+            if (room == 0) {
+                shares.emplace_back();
+                room = share;
+            }
+            const size_t n = p.bytes < room ? p.bytes : room;
+            shares.back().push_back(Piece{p.dst, p.src, n});
+            p.dst = static_cast<char *>(p.dst) + n;
+            p.src = static_cast<const char *>(p.src) + n;
+            p.bytes -= n;
+            room -= n;
+        }
+    }
+    std::vector<Piece> mine = std::move(shares[0]);
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (size_t i = 1; i < shares.size(); ++i) queue_.push_back(std::move(shares[i]));
+        outstanding_ += shares.size() - 1;
+    }
+    cv_.notify_all();
+    for (const Piece &p : mine) std::memcpy(p.dst, p.src, p.bytes);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return outstanding_ == 0; });
+}
+
+std::shared_ptr<ControlChannel> &standalone_control() {
+    static auto *ch = new std::shared_ptr<ControlChannel>(std::make_shared<ControlChannel>());
     return *ch;
 }
 
 RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
     DeviceGuard g(owner_->device());
     if (owner_->size() > 1) {
-        DDL_REQUIRE(world_control().connected() && world_control().size() == owner_->size() &&
-                        world_control().rank() == owner_->rank(),
+        ch_ = owner_->control();
+        DDL_REQUIRE(ch_ && ch_->connected() && ch_->size() == owner_->size() && ch_->rank() == owner_->rank() &&
+                        owner_->keyed_data(),
                     DDL_STATUS_NOT_INITIALIZED,
-                    "keyed requests at size > 1 need the control channel (ddl_control_connect)");
-        // private RCCL communicator for the data plane (collective: created on every rank
-        // inside ddl_control_connect)
-        data_ = owner_->split(0, owner_->rank());
+                    "keyed requests at size > 1 need the communicator's token ring (ddl_control_connect for the "
+                    "world; split_communicator builds one for every split)");
+        // the private data-plane communicator made with the ring (Communicator::enable_keyed)
+        data_ = owner_->keyed_data();
     } else {
         data_ = owner_->shared_from_this();
     }
@@ -136,6 +209,17 @@ RequestHandler::~RequestHandler() {
     if (side_) (void)hipStreamDestroy(side_);
     if (gather_) (void)hipFree(gather_);
     if (dims_) (void)hipFree(dims_);
+    if (pin_gather_) (void)hipHostFree(pin_gather_);
+    for (hipStream_t st : {h2d_, d2h_})
+        if (st) (void)hipStreamSynchronize(st);
+    for (int k = 0; k < kHostSlots; ++k) {
+        if (pin_[k]) (void)hipHostFree(pin_[k]);
+        if (dslot_[k]) (void)hipFree(dslot_[k]);
+    }
+    for (hipEvent_t e : hev_)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {h2d_, d2h_})
+        if (st) (void)hipStreamDestroy(st);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -239,7 +323,7 @@ void RequestHandler::fail_all_(int status) {
 void RequestHandler::main_() {
     try {
         DDL_HIP(hipSetDevice(owner_->device()));
-        ControlChannel &ch = world_control();
+        ControlChannel *ch = ch_;  // null at size 1
         const int P = owner_->size(), rank = owner_->rank();
         for (;;) {
             if (P == 1 || rank == 0) {
@@ -260,19 +344,19 @@ void RequestHandler::main_() {
                 else root_round_();
             } else {
                 Token t;
-                bool got = ch.recv(t, 50);
+                bool got = ch->recv(t, 50);
                 if (!got) {
                     std::lock_guard<std::mutex> g(mu_);
                     if (stop_ && pending_.empty()) {
                         // rank 0 shuts the ring down; keep listening a little for it
                         Token s;
-                        if (ch.recv(s, 5000) && s.type == TOKEN_SHUT_DOWN) ch.send(s);
+                        if (ch->recv(s, 5000) && s.type == TOKEN_SHUT_DOWN) ch->send(s);
                         break;
                     }
                     continue;
                 }
                 if (t.type == TOKEN_SHUT_DOWN) {
-                    ch.send(t);
+                    ch->send(t);
                     break;
                 }
                 member_round_(t);
@@ -283,9 +367,9 @@ void RequestHandler::main_() {
             s.type = TOKEN_SHUT_DOWN;
             s.request = TOKEN_REQUEST_SHUTDOWN;
             s.msg = "shut down";
-            ch.send(s);
+            ch->send(s);
             Token back;
-            while (ch.recv(back, 5000) && back.type != TOKEN_SHUT_DOWN) {
+            while (ch->recv(back, 5000) && back.type != TOKEN_SHUT_DOWN) {
             }
         }
     } catch (const Error &e) {
@@ -385,7 +469,7 @@ std::vector<ReqId> RequestHandler::agreed_ids_(const Agreed &a) {
         std::sort(ids.begin(), ids.end());
         return ids;
     }
-    ControlChannel &ch = world_control();
+    ControlChannel &ch = *ch_;
     if (ch.cache.learn(a.wire)) forget_ids_();
     for (size_t j = cache_req_.size(); j < ch.cache.size(); ++j) {  // mirror every new table entry
         ReqId rid = parse_wire_id(ch.cache.at((uint32_t)j));
@@ -406,7 +490,7 @@ std::vector<ReqId> RequestHandler::agreed_ids_(const Agreed &a) {
 // Rank 0: propose every registered id of one type (lap 1, SYNC — each rank intersects), then
 // announce the agreed set (lap 2, COMMUNICATE) and run it.
 void RequestHandler::root_round_() {
-    ControlChannel &ch = world_control();
+    ControlChannel &ch = *ch_;
     // one request type per round (the token carries one RequestType): the type of the first
     // registered id, as the reference proposes registeredRequest_.begin() (:184-190)
     std::vector<std::string> strs;
@@ -436,7 +520,7 @@ void RequestHandler::root_round_() {
 // intersection, then forward COMMUNICATE and run the agreed set (:302-310).
 void RequestHandler::member_round_(Token &t) {
     const Agreed a = negotiate_member(
-        world_control(), t,
+        *ch_, t,
         [this](const std::vector<std::string> &keys) {
             std::vector<ReqId> proposed;
             for (const auto &w : keys) proposed.push_back(parse_wire_id(w));
@@ -498,17 +582,99 @@ void plan_slice(const Plan &p, size_t q, size_t n, size_t *b, size_t *e) {
 }
 }  // namespace
 
+void RequestHandler::host_pieces_(const std::vector<HostSeg> &segs, const std::vector<size_t> &starts, size_t off,
+                                  size_t len, char *pinned, bool pack, std::vector<CopyPool::Piece> &out) {
+    size_t i = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+    size_t pos = off;
+    const size_t end = off + len;
+    for (; pos < end && i < segs.size(); ++i) {
+        const size_t so = pos - starts[i];
+        if (so >= segs[i].bytes) continue;  // empty segment
+        const size_t n = std::min(segs[i].bytes - so, end - pos);
+        if (pack) out.push_back(CopyPool::Piece{pinned + (pos - off), segs[i].src + so, n});
+        else out.push_back(CopyPool::Piece{segs[i].dst + so, pinned + (pos - off), n});
+        pos += n;
+    }
+}
+
+void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
+                                  const std::function<void(void *, size_t)> &coll) {
+    std::vector<size_t> starts(segs.size());
+    size_t total = 0;
+    for (size_t i = 0; i < segs.size(); ++i) {
+        starts[i] = total;
+        total += segs[i].bytes;
+    }
+    if (total == 0) return;
+    size_t chunk = (size_t)config().host_chunk_bytes.load() & ~size_t(255);  // a multiple of es
+    if (chunk < 4096) chunk = 4096;
+    if (chunk > total) chunk = (total + 255) & ~size_t(255);
+    if (host_slot_bytes_ < chunk) {
+        for (hipStream_t st : {h2d_, d2h_, stream_})
+            if (st) DDL_HIP(hipStreamSynchronize(st));
+        for (int k = 0; k < kHostSlots; ++k) {
+            if (pin_[k]) DDL_HIP(hipHostFree(pin_[k]));
+            if (dslot_[k]) DDL_HIP(hipFree(dslot_[k]));
+            pin_[k] = dslot_[k] = nullptr;
+        }
+        host_slot_bytes_ = 0;
+        for (int k = 0; k < kHostSlots; ++k) {
+            DDL_HIP(hipHostMalloc(&pin_[k], chunk, hipHostMallocDefault));
+            DDL_HIP(hipMalloc(&dslot_[k], chunk));
+        }
+        host_slot_bytes_ = chunk;
+    }
+    if (!h2d_) {
+        DDL_HIP(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
+        DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+        for (hipEvent_t &e : hev_) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
+    const size_t nchunks = (total + chunk - 1) / chunk;
+    std::vector<CopyPool::Piece> pieces;
+    auto unpack = [&](size_t j) {
+        const int k = (int)(j % kHostSlots);
+        DDL_HIP(hipEventSynchronize(hev_[3 * k + 2]));  // D2H of chunk j landed
+        const size_t off = j * chunk;
+        pieces.clear();
+        host_pieces_(segs, starts, off, std::min(chunk, total - off), static_cast<char *>(pin_[k]), false, pieces);
+        pool_->run(pieces);
+    };
+    for (size_t i = 0; i < nchunks; ++i) {
+        const int k = (int)(i % kHostSlots);
+        if (i >= (size_t)kHostSlots) unpack(i - kHostSlots);  // frees slot k (pinned and device)
+        const size_t off = i * chunk, len = std::min(chunk, total - off);
+        if (upload) {
+            pieces.clear();
+            host_pieces_(segs, starts, off, len, static_cast<char *>(pin_[k]), true, pieces);
+            pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
+            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], len, hipMemcpyHostToDevice, h2d_));
+        }
+        DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
+        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
+        coll(dslot_[k], len / es);
+        DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
+        DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
+        DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], len, hipMemcpyDeviceToHost, d2h_));
+        DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
+    }
+    for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) unpack(j);
+}
+
 // allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
 // ids lexicographic inside, plans capped at the fusion threshold.
 void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
-    std::map<int, std::vector<size_t>> groups;
+    // (dtype, host): dtype groups in ascending enum order; host-resident requests — all of them
+    // in the reference, which only has CPU tensors — form their own groups after the device ones
+    std::map<std::pair<int, int>, std::vector<size_t>> groups;
     for (size_t i = 0; i < reqs.size(); ++i) {
         if (reqs[i].n == 0) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});  // nothing to reduce
-        else groups[reqs[i].dtype].push_back(i);
+        else groups[std::make_pair(reqs[i].dtype, reqs[i].host ? 1 : 0)].push_back(i);
     }
     std::vector<hipEvent_t> waited;
     for (auto &g : groups) {
-        const int dt = g.first;
+        const int dt = g.first.first;
+        const bool host = g.first.second != 0;
         const size_t es = dtype_size(dt);
         std::vector<size_t> elems, esz;
         for (size_t i : g.second) {
@@ -517,7 +683,31 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
-            if (data_->size() == 1 && config().one_rank_shortcut.load()) {
+            if (host) {
+                // memcpy in -> MPI_Allreduce -> memcpy out (MPIRingTokenCommunication.cc:548-733),
+                // the allreduce on the device through pinned chunks
+                std::vector<HostSeg> segs;
+                size_t message = 0;
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    size_t b, e;
+                    plan_slice(p, q, r.n, &b, &e);
+                    segs.push_back(HostSeg{static_cast<const char *>(r.in) + b * es, static_cast<char *>(r.out) + b * es,
+                                           (e - b) * es});
+                    message += (e - b) * es;
+                }
+                if (data_->size() == 1 && config().one_rank_shortcut.load()) {
+                    std::vector<CopyPool::Piece> pieces;
+                    for (const HostSeg &sg : segs)
+                        if (sg.src != sg.dst) pieces.push_back(CopyPool::Piece{sg.dst, sg.src, sg.bytes});
+                    if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
+                    pool_->run(pieces);
+                } else {
+                    host_staged_(segs, es, true, [&](void *d, size_t elems) {
+                        data_->allreduce(d, d, elems, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
+                    });
+                }
+            } else if (data_->size() == 1 && config().one_rank_shortcut.load()) {
                 // a one-rank world: the sum is the input; move bytes only where out != in
                 for (size_t q = p.req_begin; q <= p.req_end; ++q) {
                     const Request &r = reqs[g.second[q]];
@@ -653,15 +843,16 @@ void RequestHandler::fused_allreduce_(const std::vector<const void *> &srcs, con
 // the packed plan from the root. The reference broadcasts every group from the first request's
 // root; requests are grouped by (dtype, root) here so mixed roots stay correct.
 void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
-    std::map<std::pair<int, int>, std::vector<size_t>> groups;
+    std::map<std::tuple<int, int, int>, std::vector<size_t>> groups;  // (dtype, root, host)
     for (size_t i = 0; i < reqs.size(); ++i) {
         if (reqs[i].n == 0) dones.push_back(Done{kNoPlan, i, DDL_STATUS_OK});
-        else groups[std::make_pair(reqs[i].dtype, reqs[i].root)].push_back(i);
+        else groups[std::make_tuple(reqs[i].dtype, reqs[i].root, reqs[i].host ? 1 : 0)].push_back(i);
     }
     const int me = data_->rank();
     std::vector<hipEvent_t> waited;
     for (auto &g : groups) {
-        const int dt = g.first.first, root = g.first.second;
+        const int dt = std::get<0>(g.first), root = std::get<1>(g.first);
+        const bool host = std::get<2>(g.first) != 0;
         const size_t es = dtype_size(dt);
         std::vector<size_t> elems, esz;
         for (size_t i : g.second) {
@@ -670,7 +861,19 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
-            if (p.req_begin == p.req_end) {
+            if (host) {
+                // root: pack in -> H2D -> broadcast -> D2H -> unpack to out; others only receive
+                std::vector<HostSeg> segs;
+                for (size_t q = p.req_begin; q <= p.req_end; ++q) {
+                    const Request &r = reqs[g.second[q]];
+                    size_t b, e;
+                    plan_slice(p, q, r.n, &b, &e);
+                    segs.push_back(HostSeg{static_cast<const char *>(r.in) + b * es, static_cast<char *>(r.out) + b * es,
+                                           (e - b) * es});
+                }
+                host_staged_(segs, es, me == root,
+                             [&](void *d, size_t elems) { data_->broadcast(d, elems, dt, root, stream_); });
+            } else if (p.req_begin == p.req_end) {
                 const Request &r = reqs[g.second[p.req_begin]];
                 const size_t cnt = p.elem_end - p.elem_begin;
                 char *out = static_cast<char *>(r.out) + p.elem_begin * es;
@@ -713,12 +916,13 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
 // allgatherv of the packed requests and an unpack into the outputs in rank order. A single
 // request gathers straight into its output (rank-major blocks are the concatenation).
 void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans) {
-    std::map<int, std::vector<size_t>> groups;
-    for (size_t i = 0; i < reqs.size(); ++i) groups[reqs[i].dtype].push_back(i);
+    std::map<std::pair<int, int>, std::vector<size_t>> groups;  // (dtype, host)
+    for (size_t i = 0; i < reqs.size(); ++i) groups[std::make_pair(reqs[i].dtype, reqs[i].host ? 1 : 0)].push_back(i);
     const int P = data_->size(), me = data_->rank();
     std::vector<hipEvent_t> waited;
     for (auto &g : groups) {
-        const int dt = g.first;
+        const int dt = g.first.first;
+        const bool host = g.first.second != 0;
         const size_t es = dtype_size(dt), m = g.second.size();
         // 1) first dims of every rank: fd[q * m + j]
         std::vector<uint64_t> fd(P * m);
@@ -745,7 +949,53 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         for (size_t j = 0; j < m; ++j) wait_inputs_(reqs[g.second[j]], waited);
         // 3) data
-        if (m == 1) {
+        if (host) {
+            // host tensors: this rank's rows packed back to back through a pinned buffer, one
+            // allgatherv on the device, then every rank's rows unpacked into the host outputs
+            std::vector<size_t> blk(P, 0);
+            for (int q = 0; q < P; ++q)
+                for (size_t j = 0; j < m; ++j) blk[q] += fd[q * m + j] * reqs[g.second[j]].row_elems * es;
+            size_t all = 0;
+            std::vector<size_t> cnt(P), dsp(P);
+            for (int q = 0; q < P; ++q) {
+                cnt[q] = blk[q] / es;
+                dsp[q] = all / es;
+                all += blk[q];
+            }
+            if (all) {
+                ensure_(fusion_, fusion_bytes_, std::max<size_t>(blk[me], 256));
+                ensure_(gather_, gather_bytes_, all);
+                if (pin_gather_bytes_ < all) {
+                    if (pin_gather_) DDL_HIP(hipHostFree(pin_gather_));
+                    pin_gather_ = nullptr;
+                    pin_gather_bytes_ = 0;
+                    DDL_HIP(hipHostMalloc(&pin_gather_, all + all / 2, hipHostMallocDefault));
+                    pin_gather_bytes_ = all + all / 2;
+                }
+                char *pin = static_cast<char *>(pin_gather_);
+                size_t off = 0;
+                for (size_t j = 0; j < m; ++j) {
+                    const Request &r = reqs[g.second[j]];
+                    const size_t b = fd[me * m + j] * r.row_elems * es;
+                    std::memcpy(pin + off, r.in, b);
+                    off += b;
+                }
+                DDL_HIP(hipMemcpyAsync(fusion_, pin, blk[me], hipMemcpyHostToDevice, stream_));
+                data_->allgatherv(fusion_, gather_, cnt.data(), dsp.data(), dt, stream_);
+                DDL_HIP(hipMemcpyAsync(pin, gather_, all, hipMemcpyDeviceToHost, stream_));
+                DDL_HIP(hipStreamSynchronize(stream_));
+                std::vector<size_t> row_off(m, 0);
+                off = 0;
+                for (int q = 0; q < P; ++q)
+                    for (size_t j = 0; j < m; ++j) {
+                        const Request &r = reqs[g.second[j]];
+                        const size_t b = fd[q * m + j] * r.row_elems * es;
+                        std::memcpy(static_cast<char *>(r.out) + row_off[j] * r.row_elems * es, pin + off, b);
+                        row_off[j] += fd[q * m + j];
+                        off += b;
+                    }
+            }
+        } else if (m == 1) {
             const Request &r = reqs[g.second[0]];
             std::vector<size_t> cnt(P), dsp(P);
             size_t acc = 0;

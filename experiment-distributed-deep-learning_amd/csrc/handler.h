@@ -59,10 +59,37 @@ struct Request {
     size_t first_dim = 0;             // allgather: rows of `in` (n = first_dim * row_elems)
     size_t row_elems = 1;             //   elements per row (the shape without its first dim)
     ddl_alloc_fn alloc = nullptr;     //   output allocation once the gathered first dim is known
+    bool host = false;                // in / out are host memory (the reference's CPU tensors)
     int64_t cidx = -1;                // index in the control channel's id table, once agreed before
     std::shared_ptr<ReadyEvent> ready;
     ddl_done_fn done = nullptr;
     void *user = nullptr;
+};
+
+// Parallel host memcpy for the host-staging pipeline (pageable <-> pinned): one memcpy thread
+// moves ~10 GB/s, less than the PCIe link, so large chunks are split over a few workers.
+class CopyPool {
+public:
+    struct Piece {
+        void *dst;
+        const void *src;
+        size_t bytes;
+    };
+    explicit CopyPool(int threads);
+    ~CopyPool();
+    CopyPool(const CopyPool &) = delete;
+    CopyPool &operator=(const CopyPool &) = delete;
+    // Copies every piece; returns when all are done (the caller's thread takes a share).
+    void run(const std::vector<Piece> &pieces);
+
+private:
+    void worker_();
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::vector<Piece>> queue_;
+    size_t outstanding_ = 0;
+    bool stop_ = false;
 };
 
 // Request identity: (type, key), ordered as the reference's (typeName, key) pairs —
@@ -90,8 +117,10 @@ struct Plan {  // makeCollectiveCommunicatePlan's (requestBegin, elementBegin, r
 std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vector<size_t> &esize,
                              size_t limit);
 
-// Global control channel of the world communicator (ddl_control_listen/connect).
-ControlChannel &world_control();
+// The process's listening / standalone control channel: ddl_control_listen opens it,
+// ddl_control_connect hands it to the world communicator (replacing it with a fresh one),
+// ddl_control_connect_ranked keeps it for ddl_control_negotiate (tools, CPU tests).
+std::shared_ptr<ControlChannel> &standalone_control();
 
 // One negotiation round of the 2-lap token protocol.
 //   root:   SYNC(proposal) -> ... -> SYNC(intersection) back; COMMUNICATE(agreed) sent.
@@ -145,11 +174,26 @@ private:
     void fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
                           const std::vector<size_t> &bytes, int dtype);
     hipEvent_t pipe_event_(size_t i);
+    // Host-resident requests (the reference's deployment case, MPIRingTokenCommunication.cc:
+    // 548-733 copies CPU tensors into its MPI buffer): the plan's segments are staged through
+    // pinned slots in chunks — host pack (CopyPool) -> H2D -> `coll` on the device slot
+    // (stream_) -> D2H -> host unpack — with kHostSlots chunks in flight so the copies overlap
+    // the collective. `upload` false: nothing is packed (a broadcast's non-root ranks).
+    struct HostSeg {
+        const char *src;
+        char *dst;
+        size_t bytes;
+    };
+    void host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
+                      const std::function<void(void *dev, size_t elems)> &coll);
+    void host_pieces_(const std::vector<HostSeg> &segs, const std::vector<size_t> &starts, size_t off, size_t len,
+                      char *pinned, bool pack, std::vector<CopyPool::Piece> &out);
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);
 
     Communicator *owner_;
+    ControlChannel *ch_ = nullptr;        // the owner's token ring (size > 1)
     std::shared_ptr<Communicator> data_;  // private data-plane communicator
     hipStream_t stream_ = nullptr;
     void *fusion_ = nullptr;  // packed requests (allreduce / broadcast / allgather send side)
@@ -164,12 +208,21 @@ private:
     size_t dims_bytes_ = 0;
     SegmentCopier copier_;
     std::vector<hipEvent_t> plan_events_;
+    static constexpr int kHostSlots = 4;
+    void *pin_[kHostSlots] = {};    // pinned host staging slots
+    void *dslot_[kHostSlots] = {};  // device slots
+    size_t host_slot_bytes_ = 0;
+    hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+    hipEvent_t hev_[3 * kHostSlots] = {};
+    std::unique_ptr<CopyPool> pool_;
+    void *pin_gather_ = nullptr;  // host allgather staging
+    size_t pin_gather_bytes_ = 0;
 
     std::mutex mu_;
     std::condition_variable cv_;       // new registrations / stop
     std::condition_variable idle_cv_;  // completions
     std::map<ReqId, Request> pending_;  // (type name, key) order
-    // id table mirror (indices of world_control().cache): parsed ids, key -> index per type,
+    // id table mirror (indices of the ring's cache): parsed ids, key -> index per type,
     // and which indices are pending here — a cached round is intersected by index
     std::vector<ReqId> cache_req_;
     std::unordered_map<std::string, uint32_t> cache_by_key_[3];

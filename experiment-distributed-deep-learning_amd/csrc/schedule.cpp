@@ -254,7 +254,7 @@ namespace {
 // rank order (x_me = in) in MPICH's tree. AG tick k (waits the fold of slice k): send my
 // reduced slice to every peer, receive theirs straight into out.
 void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
-                  size_t es, int order) {
+                  size_t es, int order, bool rank_order) {
     const int K = prog.K;
     const Range mine = chunk_range(n, es, P, 1, 0, rank);
     for (int k = 0; k < K; ++k) {
@@ -280,11 +280,12 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
             const size_t off = ms.begin - mine.begin;
             auto slot = [&](int s) -> const void * { return stb + ((size_t)s * prog.staging_stride + off) * es; };
             const void *own = inb + ms.begin * es;
-            // kFoldLeft: in, x_{me+1}, x_{me+2}, ... (slot s holds sender me+1+s); the reference
-            // orders: x_0, ..., x_{P-1} in rank order (x_me = in)
+            // ring order: in, x_{me+1}, x_{me+2}, ... (slot s holds sender me+1+s); reference
+            // order: x_0, ..., x_{P-1} in rank order (x_me = in) — in MPICH's tree, or left to
+            // right in fp32 for fp16 / bf16, which the reference rejects (the oracle's rank-order fold)
             std::vector<const void *> xs;
             for (int q = 0; q < P; ++q) {
-                const int who = order == kFoldLeft ? (rank + q) % P : q;
+                const int who = rank_order ? q : (rank + q) % P;
                 xs.push_back(who == rank ? own : slot((who - rank + P) % P - 1));
             }
             plan_fold(t.folds, xs, outb + ms.begin * es, ms.size(), order, [&](int j) {
@@ -313,7 +314,7 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
 // receives every peer's whole input into staging slot (peer - me - 1) mod P, then folds the P
 // inputs in rank order 0, 1, ..., P-1 (in for me, a slot otherwise) — left to right, or in
 // MPICH's tree with `order` — so every rank computes the same sum bit for bit (fp16/bf16
-// accumulated in fp32, rounded once). Tick 1 only waits for the
+// accumulated in fp32, rounded once per fold step: once up to 16 ranks). Tick 1 only waits for the
 // fold, so the comm stream's tail covers it (the executor joins the caller on the comm stream).
 // In place is safe: the fold runs after the group, i.e. after every send has read `in`.
 void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
@@ -366,7 +367,7 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     }
     if (cfg.algo == kAlgoDirect) {
         build_direct(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
-                     static_cast<char *>(staging), n, es, order);
+                     static_cast<char *>(staging), n, es, order, cfg.ref_order != 0);
         return;
     }
     const int R = prog.R, K = prog.K;

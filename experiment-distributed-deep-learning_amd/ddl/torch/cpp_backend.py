@@ -19,6 +19,7 @@ STATUS_OK = 0
 STATUS_NAMES = {0: 'OK', 1: 'COMM_ERROR', 2: 'ERROR_UNKNOWN', 3: 'INVALID_ARGUMENT',
                 4: 'UNSUPPORTED_DTYPE', 5: 'HIP_ERROR', 6: 'NOT_INITIALIZED', 7: 'DUPLICATE_KEY'}
 OP_SUM = 0
+MEMORY_DEVICE, MEMORY_HOST = 0, 1  # enum ddl_memory
 
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_void_p)
 # ddl_alloc_fn: output allocation of a keyed allgather (first_dim, bytes, user) -> device pointer
@@ -89,6 +90,15 @@ class CPPBackend:
         sig('ddl_allreduce_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
         sig('ddl_allreduce_submit_batch', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
             ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, vp, DONE_FN, ctypes.POINTER(vp))
+        sig('ddl_allreduce_submit_mem', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, ci, vp, DONE_FN, vp)
+        sig('ddl_allreduce_submit_batch_mem', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
+            ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, ci, vp, DONE_FN, ctypes.POINTER(vp))
+        sig('ddl_broadcast_submit_mem', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, ci, vp, DONE_FN, vp)
+        sig('ddl_allgather_submit_mem', ci, cid, ctypes.c_char_p, vp, sz, sz, ci, ci, vp, ALLOC_FN, DONE_FN, vp)
+        sig('ddl_control_channel_open', ctypes.c_longlong, ctypes.c_char_p, sz)
+        sig('ddl_control_channel_connect', ci, ctypes.c_longlong, ci, ci, ctypes.c_char_p)
+        sig('ddl_control_channel_negotiate', ci, ctypes.c_longlong, ctypes.c_char_p, ctypes.c_char_p, sz)
+        sig('ddl_control_channel_close', ci, ctypes.c_longlong)
         sig('ddl_wait_all', ci, cid)
         sig('ddl_broadcast_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
         sig('ddl_allgather_submit', ci, cid, ctypes.c_char_p, vp, sz, sz, ci, vp, ALLOC_FN, DONE_FN, vp)
@@ -117,6 +127,18 @@ class CPPBackend:
         sig('ddl_pack', ci, vp, ctypes.POINTER(vp), ctypes.POINTER(sz), ci, vp)
         sig('ddl_unpack', ci, ctypes.POINTER(vp), vp, ctypes.POINTER(sz), ci, vp)
         sig('ddl_local_ring_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, ci, vp)
+        # RCCL loopback (test / diagnostic: the RCCL transport on one GPU)
+        fp, lp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_longlong)
+        sig('ddl_rccl_loopback_init', ci, ci)
+        sig('ddl_rccl_loopback_split', ci, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci))
+        sig('ddl_rccl_loopback_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, vp)
+        sig('ddl_rccl_loopback_broadcast', ci, ci, ci, ctypes.POINTER(vp), sz, ci, vp)
+        sig('ddl_rccl_loopback_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
+            ctypes.POINTER(sz), ci, vp)
+        sig('ddl_rccl_loopback_max', ci, fp, ci, vp)
+        sig('ddl_rccl_loopback_tune', ci, ci, sz, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci), lp, fp, ci)
+        sig('ddl_rccl_loopback_stats', ci, ci, lp)
+        sig('ddl_rccl_loopback_finalize', ci)
         # schedule introspection
         sig('ddl_ring_count', ci, ci, ci)
         sig('ddl_ring_perm', ci, ci, ci, ci, ctypes.POINTER(ci))

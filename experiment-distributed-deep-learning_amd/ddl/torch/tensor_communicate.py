@@ -19,7 +19,8 @@ import torch
 from ddl.torch import cpp_backend as cb
 from ddl.torch.communicator import Communicator
 from ddl.torch.cpp_backend import CPPBackend, check
-from ddl.torch.util import current_stream_handle, ddl_dtype, require_device_tensor
+from ddl.torch.util import (current_stream_handle, ddl_dtype, memory_kind, require_device_tensor,
+                           stream_handle_for)
 
 
 def _comm(communicator):
@@ -166,34 +167,43 @@ def _on_done(status, user):
         h._event.set()
 
 
+def _same_memory(a: torch.Tensor, b: torch.Tensor, what: str) -> int:
+    ma, mb = memory_kind(a, f'{what} input'), memory_kind(b, f'{what} output')
+    if ma != mb:
+        raise ValueError(f'{what}: input and output must both be device or both be host tensors')
+    return ma
+
+
 def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator = None,
                     output: torch.Tensor = None) -> Handle:
-    """Register a keyed allreduce of a device tensor; returns a Handle.
+    """Register a keyed allreduce; returns a Handle.
 
     `name` plays the role of the TF op name: the same name on every rank identifies the same
     gradient, and only one request per name may be pending (TensorCommunicateRequest.h:21).
+    Device tensors stay in HBM; host (CPU) tensors — the reference's only kind, its op is
+    DEVICE_CPU (AllreduceOp.cc:68) — are fused through pinned staging to the GPU and back.
     """
     communicator = _comm(communicator)
-    require_device_tensor(tensor, 'allreduce_async input')
     out = torch.empty_like(tensor) if output is None else output
-    require_device_tensor(out, 'allreduce_async output')
+    mem = _same_memory(tensor, out, 'allreduce_async')
     uid = next(_ids)
     h = Handle(name, out, (tensor, out))
     with _pending_lock:
         _pending[uid] = h
-    st = CPPBackend.c_api().ddl_allreduce_submit(
+    st = CPPBackend.c_api().ddl_allreduce_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(),
-        ddl_dtype(tensor), cb.OP_SUM, current_stream_handle(tensor.device), _on_done, uid)
+        ddl_dtype(tensor), cb.OP_SUM, mem, stream_handle_for(tensor), _on_done, uid)
     if st != cb.STATUS_OK:
         with _pending_lock:
             _pending.pop(uid, None)
-        check(st, 'ddl_allreduce_submit')
+        check(st, 'ddl_allreduce_submit_mem')
     return h
 
 
 def allreduce_async_batch(tensors, names, communicator: Communicator = None, outputs=None):
     """Register several keyed allreduces at once (one engine wake-up, one input-ready event);
-    returns one Handle per tensor. Same key rules as `allreduce_async`."""
+    returns one Handle per tensor. Same key rules as `allreduce_async`; device and host tensors
+    may be mixed (one submission per memory kind)."""
     import ctypes
     communicator = _comm(communicator)
     tensors = list(tensors)
@@ -204,49 +214,49 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     k = len(tensors)
     if k == 0:
         return []
-    for t, o in zip(tensors, outputs):
-        require_device_tensor(t, 'allreduce_async_batch input')
-        require_device_tensor(o, 'allreduce_async_batch output')
+    mems = [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
     uids = [next(_ids) for _ in range(k)]
     handles = [Handle(n, o, (t, o)) for n, t, o in zip(names, tensors, outputs)]
     with _pending_lock:
         _pending.update(zip(uids, handles))
-    keys = (ctypes.c_char_p * k)(*[n.encode() for n in names])
-    ins = (ctypes.c_void_p * k)(*[t.data_ptr() for t in tensors])
-    outs = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outputs])
-    ns = (ctypes.c_size_t * k)(*[t.numel() for t in tensors])
-    dts = (ctypes.c_int * k)(*[ddl_dtype(t) for t in tensors])
-    users = (ctypes.c_void_p * k)(*uids)
-    st = CPPBackend.c_api().ddl_allreduce_submit_batch(
-        communicator.id, k, keys, ins, outs, ns, dts, cb.OP_SUM, current_stream_handle(tensors[0].device),
-        _on_done, users)
-    if st != cb.STATUS_OK:
-        with _pending_lock:
-            for u in uids:
-                _pending.pop(u, None)
-        check(st, 'ddl_allreduce_submit_batch')
+    for mem in sorted(set(mems)):
+        idx = [i for i in range(k) if mems[i] == mem]
+        m = len(idx)
+        keys = (ctypes.c_char_p * m)(*[names[i].encode() for i in idx])
+        ins = (ctypes.c_void_p * m)(*[tensors[i].data_ptr() for i in idx])
+        outs = (ctypes.c_void_p * m)(*[outputs[i].data_ptr() for i in idx])
+        ns = (ctypes.c_size_t * m)(*[tensors[i].numel() for i in idx])
+        dts = (ctypes.c_int * m)(*[ddl_dtype(tensors[i]) for i in idx])
+        users = (ctypes.c_void_p * m)(*[uids[i] for i in idx])
+        st = CPPBackend.c_api().ddl_allreduce_submit_batch_mem(
+            communicator.id, m, keys, ins, outs, ns, dts, cb.OP_SUM, mem, stream_handle_for(tensors[idx[0]]),
+            _on_done, users)
+        if st != cb.STATUS_OK:
+            with _pending_lock:
+                for i in idx:
+                    _pending.pop(uids[i], None)
+            check(st, 'ddl_allreduce_submit_batch_mem')
     return handles
 
 
 def broadcast_async(tensor: torch.Tensor, name: str, root_rank: int, communicator: Communicator = None,
                     output: torch.Tensor = None) -> Handle:
     """Keyed broadcast (the TF op's asynchronous path, TensorBroadcastRequest): `output`
-    (default: a new tensor; may be `tensor` itself) receives root's tensor."""
+    (default: a new tensor; may be `tensor` itself) receives root's tensor. Device or host."""
     communicator = _comm(communicator)
-    require_device_tensor(tensor, 'broadcast_async input')
     out = torch.empty_like(tensor) if output is None else output
-    require_device_tensor(out, 'broadcast_async output')
+    mem = _same_memory(tensor, out, 'broadcast_async')
     uid = next(_ids)
     h = Handle(name, out, (tensor, out))
     with _pending_lock:
         _pending[uid] = h
-    st = CPPBackend.c_api().ddl_broadcast_submit(
+    st = CPPBackend.c_api().ddl_broadcast_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(), ddl_dtype(tensor),
-        int(root_rank), current_stream_handle(tensor.device), _on_done, uid)
+        int(root_rank), mem, stream_handle_for(tensor), _on_done, uid)
     if st != cb.STATUS_OK:
         with _pending_lock:
             _pending.pop(uid, None)
-        check(st, 'ddl_broadcast_submit')
+        check(st, 'ddl_broadcast_submit_mem')
     return h
 
 
@@ -286,10 +296,11 @@ def _on_gather_done(status, user):
 
 def allgather_async(tensor: torch.Tensor, name: str, communicator: Communicator = None) -> Handle:
     """Keyed allgather (TensorAllgatherRequest): negotiated and fused with the other pending
-    allgathers of the same dtype; `handle.wait()` returns the gathered tensor."""
+    allgathers of the same dtype and memory kind; `handle.wait()` returns the gathered tensor
+    (on the input's device: HBM, or host memory for a CPU tensor)."""
     communicator = _comm(communicator)
-    require_device_tensor(tensor, 'allgather_async input')
     src = tensor if tensor.dim() > 0 else tensor.reshape(1)
+    mem = memory_kind(src, 'allgather_async input')
     row = 1
     for d in src.shape[1:]:
         row *= d
@@ -297,13 +308,13 @@ def allgather_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     h = _GatherHandle(name, src)
     with _pending_lock:
         _gathers[uid] = h
-    st = CPPBackend.c_api().ddl_allgather_submit(
-        communicator.id, name.encode(), src.data_ptr(), src.shape[0], row, ddl_dtype(src),
-        current_stream_handle(src.device), _on_alloc, _on_gather_done, uid)
+    st = CPPBackend.c_api().ddl_allgather_submit_mem(
+        communicator.id, name.encode(), src.data_ptr(), src.shape[0], row, ddl_dtype(src), mem,
+        stream_handle_for(src), _on_alloc, _on_gather_done, uid)
     if st != cb.STATUS_OK:
         with _pending_lock:
             _gathers.pop(uid, None)
-        check(st, 'ddl_allgather_submit')
+        check(st, 'ddl_allgather_submit_mem')
     return h
 
 
@@ -322,7 +333,8 @@ def broadcast_by_group(tensors, root_rank: int, communicator: Communicator = Non
 def broadcast_parameters(params, root_rank: int = 0, communicator: Communicator = None):
     """Initial weights from `root_rank` (the torch counterpart of broadcast_global_variables,
     tensor_communicate.py:111-129): `params` is a module's state_dict(), an iterable of
-    (name, tensor) pairs, or an iterable of tensors; device tensors are updated in place."""
+    (name, tensor) pairs, or an iterable of tensors; every tensor (device or host) is updated in
+    place."""
     if hasattr(params, 'items'):
         items = sorted(params.items())
     else:
@@ -330,11 +342,8 @@ def broadcast_parameters(params, root_rank: int = 0, communicator: Communicator 
         if items and not isinstance(items[0], tuple):
             items = [(f'{i:06d}', t) for i, t in enumerate(items)]
     ts = [t.data if hasattr(t, 'data') else t for _, t in items]
-    dev = [t for t in ts if t.is_cuda and t.numel() > 0]
-    broadcast_by_group(dev, root_rank, communicator, prefix='broadcast_parameters')
-    for t in ts:
-        if not t.is_cuda and t.numel() > 0:
-            t.copy_(broadcast(t, root_rank, communicator))
+    # device and host (CPU model) tensors alike, in place, as one negotiated round
+    broadcast_by_group([t for t in ts if t.numel() > 0], root_rank, communicator, prefix='broadcast_parameters')
     return params
 
 

@@ -28,6 +28,18 @@ def current_stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def memory_kind(t: torch.Tensor, what: str = 'tensor') -> int:
+    """ddl_memory of a contiguous tensor: device (HBM) or host (the reference's CPU tensors)."""
+    if not t.is_contiguous():
+        raise ValueError(f'{what} must be contiguous')
+    return cb.MEMORY_DEVICE if t.is_cuda else cb.MEMORY_HOST
+
+
+def stream_handle_for(t: torch.Tensor) -> int:
+    """The submitter's stream for a device tensor; 0 for host tensors (ready at submission)."""
+    return current_stream_handle(t.device) if t.is_cuda else 0
+
+
 def require_device_tensor(t: torch.Tensor, what: str = 'tensor') -> None:
     if not t.is_cuda:
         raise ValueError(f'{what} must be a device (HBM) tensor')

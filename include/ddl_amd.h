@@ -63,6 +63,12 @@ enum ddl_status {
     DDL_STATUS_DUPLICATE_KEY = 7 /* TensorCommunicateRequest.h:21: one pending request per key */
 };
 
+/* Where a keyed request's buffers live: SURVEY §8(b)'s device_ptr_flag. The reference's op is
+ * CPU-only (AllreduceOp.cc:68): its tensors are host memory, copied into the MPI buffer
+ * (MPIRingTokenCommunication.cc:548-733). Host requests are staged through pinned chunks to the
+ * device and back; device requests stay in HBM. */
+enum ddl_memory { DDL_MEMORY_DEVICE = 0, DDL_MEMORY_HOST = 1 };
+
 /* Communicator::AllreduceOperation (reference Communicator.h:22-24): SUM only. */
 enum ddl_allreduce_op { DDL_ALLREDUCE_OP_SUM = 0 };
 
@@ -93,14 +99,16 @@ int ddl_init(int rank, int size, int device, const void *unique_id, size_t len);
  * the autotuner's max-reduce go through host callbacks instead of RCCL, so the multi-process
  * engine — control channel, keyed handler, fusion, schedules, streams, kernels — can run as
  * several processes sharing one GPU (RCCL refuses two ranks on one device). `comm_tag` names
- * the communicator (0 = world, then one per split in creation order), so the callbacks can keep
- * concurrent communicators apart. The engine synchronises the group's stream, stages every
+ * the communicator (0 = world; splits agree on theirs), so the callbacks can keep concurrent
+ * communicators apart. The engine synchronises the group's stream, stages every
  * send into host memory, calls the group callback — which must complete the whole exchange on
  * the host buffers before it returns, 0 = success — and copies the received host buffers to
- * the device. Splits must give every rank the same color and key = rank. */
+ * the device. `peer` is a world rank (splits map their ranks); `comm_tag` differs between any two
+ * communicators that share a pair of ranks. `max` is no longer called (the autotuner agrees
+ * through `group`); it may be NULL. */
 typedef struct ddl_p2p_op {
     int send;     /* 1 send, 0 receive */
-    int peer;     /* rank in the communicator */
+    int peer;     /* world rank of the peer */
     int tag;      /* matches a send with its receive inside one group (posting order per tag) */
     void *ptr;    /* host staging buffer of `bytes` */
     size_t bytes;
@@ -126,11 +134,20 @@ int ddl_control_negotiate(const char *keys, char *out, size_t len);
 /* Negotiation rounds so far by token form: ids as strings, or as indices into the table of ids
  * agreed in earlier rounds (a repeated key set, e.g. every training step's gradients). */
 int ddl_control_stats(long long *string_rounds, long long *cached_rounds);
+/* Several independent token rings in one process (tools, CPU tests of per-communicator rings):
+ * _open listens and returns a handle (0 on failure) and "ip:port"; _connect joins the ring of
+ * `size` ranks; _negotiate is ddl_control_negotiate on that ring. Every communicator of size > 1
+ * made by split_communicator owns such a ring (RingTokenCommunicateController.cc:53-79). */
+long long ddl_control_channel_open(char *endpoint_out, size_t len);
+int ddl_control_channel_connect(long long channel, int rank, int size, const char *endpoints);
+int ddl_control_channel_negotiate(long long channel, const char *keys, char *out, size_t len);
+int ddl_control_channel_close(long long channel);
 int ddl_finalize(void);
 int ddl_is_initialized(void);
 
 /* Tunables: "algo" (0 multi-ring, 1 direct all-to-all), "slice_bytes", "rings", "max_slices",
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
+ * "host_copy_threads" (memcpy workers of the keyed host staging),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "reference_order" (1,
@@ -226,6 +243,21 @@ int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *co
                                const void *const *ins, void *const *outs, const size_t *elements,
                                const int *dtypes, int op, void *hip_stream, ddl_done_fn done,
                                void *const *users);
+/* The same four submissions with the memory kind of in / out (ddl_memory). Host buffers are
+ * ready at submission (no stream wait) and must stay valid until done; a keyed allgather's alloc
+ * then returns host memory. Host and device requests of one dtype fuse into separate plans
+ * (device groups first); with only host requests the plans are the reference's. */
+int ddl_allreduce_submit_mem(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                             int dtype, int op, int memory, void *hip_stream, ddl_done_fn done, void *user);
+int ddl_allreduce_submit_batch_mem(ddl_communicator_id id, int count, const char *const *keys,
+                                   const void *const *ins, void *const *outs, const size_t *elements,
+                                   const int *dtypes, int op, int memory, void *hip_stream, ddl_done_fn done,
+                                   void *const *users);
+int ddl_broadcast_submit_mem(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
+                             int dtype, int root, int memory, void *hip_stream, ddl_done_fn done, void *user);
+int ddl_allgather_submit_mem(ddl_communicator_id id, const char *key, const void *in, size_t first_dim,
+                             size_t row_elements, int dtype, int memory, void *hip_stream, ddl_alloc_fn alloc,
+                             ddl_done_fn done, void *user);
 /* Blocks until every request submitted on `id` so far has completed. */
 int ddl_wait_all(ddl_communicator_id id);
 
@@ -275,6 +307,29 @@ int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *
 int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream);
 int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
                          const size_t *displs, int dtype, void *hip_stream);
+
+/* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
+ * A one-rank RCCL communicator (ncclGetUniqueId + ncclCommInitRank, the calls ddl_init makes at
+ * size > 1) carries the matched send/recv pairs of P virtual ranks' programs as self-send /
+ * self-recv pairs, posted through the engine's RcclTransport::group in matching order — the
+ * data path that replaces MPI_Allreduce (MPICommunicator.cc:14-28) with RCCL doing the moves.
+ * _split runs ncclCommSplit (MPICommunicator.cc:92-101) on the current loopback communicator;
+ * the split becomes current (color < 0: *rank = -1, *size = 0, nothing changes). _max is the
+ * autotuner's cross-rank agreement (ncclAllReduce(MAX)); _tune runs the autotuner with the
+ * candidates over RCCL and that agreement. _stats: self pairs posted so far for P ranks. */
+int ddl_rccl_loopback_init(int device);
+int ddl_rccl_loopback_split(int color, int key, int *rank, int *size);
+int ddl_rccl_loopback_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements,
+                                int dtype, void *hip_stream);
+int ddl_rccl_loopback_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
+                                void *hip_stream);
+int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                                 const size_t *displs, int dtype, void *hip_stream);
+int ddl_rccl_loopback_max(float *values, int count, void *hip_stream);
+int ddl_rccl_loopback_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
+                           long long *configs, float *ms, int max_candidates);
+int ddl_rccl_loopback_stats(int nranks, long long *pairs);
+int ddl_rccl_loopback_finalize(void);
 
 /* ---- schedule introspection (host only, no GPU needed) -------------------------------- */
 int ddl_ring_count(int nranks, int max_rings);

@@ -149,6 +149,132 @@ def check_keyed_reference_order(ctx):
             assert got.tobytes() == want.tobytes(), (i, sizes[i])
 
 
+def check_split_communicators_keyed(ctx):
+    """One token ring and handler per communicator (RingTokenCommunicateController.cc:53-79):
+    keyed batches run at once on the world, on pairs {0,1}, {2,3}, ... (color rank // 2) and on a
+    same-size split with reversed keys, all under the SAME key names and submitted in per-rank
+    random orders. Each output equals MPICH's order over that communicator's ranks
+    (ddlo_fold_ref_order with the dtype group's bytes) — no cross-talk between rings. Then plain
+    allreduces on the splits (rank mapping of the data plane) with the autotuner on."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allreduce, allreduce_async_batch
+    pair = comm.split_communicator(r // 2, r)
+    same = comm.split_communicator(0, P - 1 - r)
+    members = {'world': list(range(P)), 'pair': [q for q in range(P) if q // 2 == r // 2],
+               'same': list(range(P - 1, -1, -1))}
+    assert (pair.size, pair.rank) == (len(members['pair']), members['pair'].index(r))
+    assert (same.size, same.rank) == (P, P - 1 - r)
+    comms = {'world': comm, 'pair': pair, 'same': same}
+    sizes = [7, 300, 5000, 70_001, 1, 4099]
+    dts = [h.DT_FLOAT, h.DT_INT32, h.DT_FLOAT, h.DT_DOUBLE, h.DT_FLOAT, h.DT_INT32]
+    for rnd in range(2):  # the second round goes by id-table index on every ring
+        handles, wants = [], []
+        for ci, (name, c) in enumerate(comms.items()):
+            xs = [[h.random_input(dts[i], n, 1000 * rnd + 100 * ci + 31 * i + q) for q in range(P)]
+                  for i, n in enumerate(sizes)]
+            mem = members[name]
+            gb = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
+            order = np.random.default_rng(7 * rnd + 13 * ci + r).permutation(len(sizes))
+            ts = [torch.from_numpy(xs[i][r]).cuda() for i in order]
+            handles += allreduce_async_batch(ts, [f'k_{i}' for i in order], c)
+            wants += [(name, i, ora.fold_ref_order(dts[i], [xs[i][q] for q in mem], gb[dts[i]])) for i in order]
+        for hd, (name, i, want) in zip(handles, wants):
+            got = hd.wait(timeout=120).cpu().numpy()
+            assert got.tobytes() == want.tobytes(), (rnd, name, i)
+    with h.config(lib, tune=1):
+        for name in ('pair', 'same'):
+            c = comms[name]
+            n = 1 << 18
+            xs = [h.random_input(h.DT_FLOAT, n, 77 + q, kind='exact') for q in range(P)]
+            got = allreduce(torch.from_numpy(xs[r]).cuda(), c).cpu().numpy()
+            want = np.sum(np.stack([xs[q] for q in members[name]]).astype(np.float64), axis=0).astype(np.float32)
+            assert np.array_equal(got, want), name
+    pair.detach()
+    same.detach()
+
+
+def check_keyed_host_requests(ctx):
+    """Keyed requests on host (CPU) tensors — the reference's only kind (its op is DEVICE_CPU,
+    AllreduceOp.cc:68): fused per dtype, staged through pinned 64 KiB chunks (many chunks, the
+    4 slots wrap), reduced on the GPU and unpacked back. Every element equals MPICH's order
+    for the host group's message (ddlo_fold_ref_order with the group's bytes), bit for bit. A
+    device request of the same dtype in the same batch forms its own group. Then keyed host
+    broadcasts (mixed roots) and allgathers (per-rank first dims)."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allgather_async, allreduce_async_batch, broadcast_async
+    sizes = [5, 300, 70_001, 4099, 1, 200_000, 513, 33_333]
+    dts = [h.DT_FLOAT, h.DT_DOUBLE, h.DT_INT32, h.DT_FLOAT, h.DT_FLOAT, h.DT_DOUBLE, h.DT_INT32, h.DT_FLOAT]
+    xs = [[h.random_input(dts[i], n, 900 + 31 * i + q) for q in range(P)] for i, n in enumerate(sizes)]
+    gb = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
+    dev_x = [h.random_input(h.DT_FLOAT, 4099, 4000 + q) for q in range(P)]
+    with h.config(lib, host_chunk_bytes=64 << 10, reference_order=1):
+        for rnd in range(2):
+            ts = [torch.from_numpy(xs[i][r].copy()) for i in range(len(sizes))]
+            order = np.random.default_rng(5 * rnd + r).permutation(len(sizes))
+            tensors = [ts[i] for i in order] + [torch.from_numpy(dev_x[r]).cuda()]
+            names = [f'host_{i}' for i in order] + ['dev_0']
+            outs = [t if (rnd == 1 and not t.is_cuda) else None for t in tensors]  # round 1: in place
+            hs = allreduce_async_batch(tensors, names, comm,
+                                       outputs=[o if o is not None else torch.empty_like(t) for o, t in zip(outs, tensors)])
+            for hd, i in zip(hs, order):
+                got = hd.wait(timeout=120)
+                assert not got.is_cuda
+                want = ora.fold_ref_order(dts[i], xs[i], gb[dts[i]])
+                assert got.numpy().tobytes() == want.tobytes(), (rnd, i)
+            assert hs[-1].wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, dev_x).tobytes()
+        hs, want = [], []
+        for i in range(9):
+            root, dt = i % P, [torch.float32, torch.int64, torch.float64][i % 3]
+            t = (torch.arange(5000 + 997 * i) + 100 * r).to(dt)
+            hs.append(broadcast_async(t, f'hb{i:02d}', root, comm))
+            want.append((torch.arange(5000 + 997 * i) + 100 * root).to(dt))
+        for hd, w in zip(hs, want):
+            got = hd.wait(timeout=120)
+            assert not got.is_cuda and torch.equal(got, w)
+        hs, want = [], []
+        for i in range(4):
+            dt = [torch.float32, torch.int32][i % 2]
+            t = (torch.arange((r + 1 + i) * 3).reshape(-1, 3) + 1000 * r).to(dt)
+            hs.append(allgather_async(t, f'hag{i}', comm))
+            want.append(torch.cat([(torch.arange((q + 1 + i) * 3).reshape(-1, 3) + 1000 * q).to(dt) for q in range(P)]))
+        for hd, w in zip(hs, want):
+            got = hd.wait(timeout=120)
+            assert not got.is_cuda and torch.equal(got, w)
+
+
+def check_dp_training_cpu_model(ctx):
+    """The DP wrapper on a CPU model (the reference's deployment: Keras on CPU tensors): initial
+    weights broadcast, every gradient a keyed host allreduce, replicas equal one full-batch fp64
+    step on the concatenated data."""
+    torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.parallelism.data import InitialParametersBroadcast, data_parallelism_distributed_optimizer_wrapper
+
+    def model_fn(seed):
+        torch.manual_seed(seed)
+        return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4)).double()
+    model = model_fn(99 + r)
+    InitialParametersBroadcast(model, 0, communicator=comm).broadcast()
+    ref = model_fn(99)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert not p.is_cuda and torch.equal(p, q)
+    opt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(model.parameters(), lr=0.1), comm)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(78)
+    for step in range(3):
+        xb = [torch.randn(8, 16, generator=g, dtype=torch.float64) for _ in range(P)]
+        yb = [torch.randn(8, 4, generator=g, dtype=torch.float64) for _ in range(P)]
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(xb[r]), yb[r]).backward()
+        opt.step()
+        ref_opt.zero_grad()
+        sum(torch.nn.functional.mse_loss(ref(xb[q]), yb[q]) for q in range(P)).div(P).backward()
+        ref_opt.step()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, rtol=1e-12, atol=1e-12)
+
+
 def check_keyed_broadcast_allgather(ctx):
     """Keyed broadcasts with mixed roots and dtypes, keyed allgathers with per-rank first dims."""
     torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
@@ -232,7 +358,8 @@ def check_dp_training(ctx):
 
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
-          check_keyed_reference_order, check_keyed_broadcast_allgather, check_host_resident, check_dp_training]
+          check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
+          check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model]
 
 
 def worker(rank, world, port, q):

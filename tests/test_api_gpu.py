@@ -263,3 +263,35 @@ def test_keyed_fusion_pipeline_large_segment(world, lib, data_plane_at_one_rank)
     hs = allreduce_async_batch(ts, ['a', 'b', 'c', 'd'], world)
     for w, h in zip(want, hs):
         assert torch.equal(h.wait(timeout=60), w)
+
+
+@pytest.mark.parametrize('chunk', [4096, 64 << 10, 32 << 20])
+def test_keyed_host_requests_data_plane(world, lib, chunk):
+    """Keyed requests on host tensors with the one-rank shortcut off: every plan goes through the
+    pinned-chunk pipeline (host pack -> H2D -> allreduce -> D2H -> host unpack; 4096 B chunks
+    make hundreds of chunks over 4 slots), in and out of place, every dtype, plus a device
+    request in the same batch; outputs equal the inputs bit for bit (one rank)."""
+    from ddl.torch.tensor_communicate import allreduce_async_batch, broadcast_async
+    keys = (b'one_rank_shortcut', b'host_chunk_bytes')
+    old = {k: lib.ddl_get_config(k) for k in keys}
+    try:
+        assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
+        assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
+        g = torch.Generator().manual_seed(chunk)
+        dts = [torch.float32, torch.float64, torch.int32, torch.float16, torch.bfloat16, torch.int64]
+        xs = [(torch.randn(n, generator=g) * 100).to(dts[i % 6]) for i, n in enumerate([1, 7, 1000, 65_537, 300_001,
+                                                                                       5, 2_000_003, 4096])]
+        keep = [x.clone() for x in xs]
+        outs = [x if i % 2 else torch.empty_like(x) for i, x in enumerate(xs)]
+        dev = torch.randn(1234, device='cuda')
+        hs = allreduce_async_batch(xs + [dev], [f'hk_{i}' for i in range(len(xs))] + ['hk_dev'], world,
+                                   outputs=outs + [torch.empty_like(dev)])
+        for h, k in zip(hs, keep):
+            got = h.wait(timeout=60)
+            assert not got.is_cuda and torch.equal(got, k)
+        assert torch.equal(hs[-1].wait(timeout=60), dev)
+        t = torch.arange(100_003, dtype=torch.float64)
+        assert torch.equal(broadcast_async(t, 'hk_b', 0, world).wait(timeout=60), t)
+    finally:
+        for k, v in old.items():
+            lib.ddl_set_config(k, v)

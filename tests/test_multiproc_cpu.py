@@ -276,3 +276,102 @@ def test_broadcast_allgather_programs_over_gloo(world, kind):
         p.join(timeout=60)
     for rank, ok, err in res:
         assert ok, f'rank {rank}: {err or "result differs from the oracle"}'
+
+
+def _rings_worker(rank, world, rings, keysets, eps_q, go_q, out_q):
+    """One process holding several token rings at once (ddl_control_channel_*): every ring it is a
+    member of negotiates on its own thread, concurrently with the others, under the same key
+    names — as a world communicator and its splits each run their own handler."""
+    try:
+        import threading
+        _setup_paths()
+        from ddl.torch.cpp_backend import CPPBackend
+        lib = CPPBackend.c_api()
+        lib.ddl_control_channel_open.restype = ctypes.c_longlong
+        lib.ddl_control_channel_open.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        lib.ddl_control_channel_connect.argtypes = [ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+        lib.ddl_control_channel_negotiate.argtypes = [ctypes.c_longlong, ctypes.c_char_p, ctypes.c_char_p,
+                                                      ctypes.c_size_t]
+        lib.ddl_control_channel_close.argtypes = [ctypes.c_longlong]
+        mine = {name: members for name, members in rings.items() if rank in members}
+        handles = {}
+        for name in mine:
+            ep = ctypes.create_string_buffer(256)
+            handles[name] = lib.ddl_control_channel_open(ep, 256)
+            assert handles[name], lib.ddl_last_error()
+            eps_q.put((name, rank, ep.value.decode()))
+        eps = go_q.get(timeout=60)  # name -> ';'-joined endpoints in ring-rank order
+        res, errs = {}, []
+
+        def run(name):
+            try:
+                members = mine[name]
+                me = members.index(rank)
+                assert lib.ddl_control_channel_connect(handles[name], me, len(members), eps[name].encode()) == 0
+                rounds = []
+                for keys in keysets[name][rank]:
+                    out = ctypes.create_string_buffer(1 << 16)
+                    st = lib.ddl_control_channel_negotiate(handles[name], '\n'.join(keys).encode(), out, len(out))
+                    assert st == 0, lib.ddl_last_error()
+                    rounds.append([k for k in out.value.decode().split('\n') if k])
+                res[name] = rounds
+            except Exception as e:  # noqa: BLE001
+                errs.append(f'{name}: {e!r}')
+        ths = [threading.Thread(target=run, args=(n,)) for n in mine]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=120)
+        for h in handles.values():
+            lib.ddl_control_channel_close(h)
+        out_q.put((rank, res, '; '.join(errs)))
+    except Exception as e:  # noqa: BLE001
+        out_q.put((rank, None, repr(e)))
+
+
+def test_token_rings_per_communicator_concurrent():
+    """4 processes, three rings negotiating at the same time with the same key names: the world
+    (ranks 0..3), the pairs {0,1} / {2,3}, and a same-size ring in reversed order — each agrees
+    on exactly the intersection of ITS members' key sets, with no cross-talk (missing #1 of the
+    round-1 review: one ring per communicator, RingTokenCommunicateController.cc:53-79)."""
+    world = 4
+    rings = {'world': [0, 1, 2, 3], 'pair0': [0, 1], 'pair1': [2, 3], 'same': [3, 2, 1, 0]}
+    rng = np.random.default_rng(17)
+    universe = [f'grad_{i:04d}' for i in range(80)]
+    keysets = {}
+    for name, members in rings.items():
+        keysets[name] = {}
+        for r in members:
+            rounds = []
+            for _ in range(4):  # rounds 2-3 repeat key sets: the cached-id form on each ring
+                ks = [k for k in universe if rng.random() < (0.7 if name != 'same' else 0.9)]
+                rng.shuffle(ks)
+                rounds.append(ks)
+            rounds[3] = list(rounds[2])
+            keysets[name][r] = rounds
+    ctx = mp.get_context('spawn')
+    eps_q, out_q = ctx.Queue(), ctx.Queue()
+    go = [ctx.Queue() for _ in range(world)]
+    procs = [ctx.Process(target=_rings_worker, args=(r, world, rings, keysets, eps_q, go[r], out_q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    nep = sum(len(m) for m in rings.values())
+    got = {}
+    for _ in range(nep):
+        name, r, ep = eps_q.get(timeout=60)
+        got[(name, r)] = ep
+    eps = {name: ';'.join(got[(name, r)] for r in members) for name, members in rings.items()}
+    for q in go:
+        q.put(eps)
+    res = dict((r, (rounds, err)) for r, rounds, err in (out_q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=30)
+    for name, members in rings.items():
+        for rd in range(4):
+            inter = set.intersection(*[set(keysets[name][r][rd]) for r in members])
+            want = sorted(inter, key=lambda s: s.encode())
+            for r in members:
+                rounds, err = res[r]
+                assert rounds is not None and not err, f'rank {r}: {err}'
+                assert rounds[name][rd] == want, f'ring {name} rank {r} round {rd}'
