@@ -93,11 +93,14 @@ def test_keyed_requests_fused(world, lib, threshold):
 
 
 def test_keyed_batch_c5_shape(world, lib):
-    """C5 shape: many buckets, byte sizes log-uniform in [4 KiB, 4 MiB] rounded to
-    256 B, fp32/fp16 mixed, keys grad_%05d in random order — one batch, fused, exact."""
+    """C5 shape: the full 4096 buckets, byte sizes log-uniform in [4 KiB, 4 MiB]
+    rounded to 256 B, fp32/fp16 mixed, keys grad_%05d in random order — one batch, with the
+    one-rank shortcut OFF, so negotiation, dtype groups, plans, the fusion pipeline's pack ->
+    allreduce -> unpack all run. The oracle at one rank is the input itself (MPI_Allreduce of
+    one rank); the 8-rank data plane of the same set is tests/test_configs_gpu.py."""
     from ddl.torch.tensor_communicate import allreduce_async_batch
     rng = np.random.default_rng(42)
-    k = 512
+    k = 4096
     sizes = np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=k)).astype(np.int64) // 256 * 256
     tensors, names = [], []
     for i in rng.permutation(k):
@@ -105,9 +108,14 @@ def test_keyed_batch_c5_shape(world, lib):
         n = int(sizes[i]) // (4 if dt == torch.float32 else 2)
         tensors.append(torch.randn(n, device='cuda').to(dt))
         names.append(f'grad_{i:05d}')
-    hs = allreduce_async_batch(tensors, names, world)
-    for t, h in zip(tensors, hs):
-        assert torch.equal(h.wait(60), t)
+    old = lib.ddl_get_config(b'one_rank_shortcut')
+    try:
+        assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
+        hs = allreduce_async_batch(tensors, names, world)
+        for t, h in zip(tensors, hs):
+            assert torch.equal(h.wait(60), t)
+    finally:
+        lib.ddl_set_config(b'one_rank_shortcut', old)
 
 
 def test_keyed_batch_duplicate_rejected_atomically(world):
