@@ -9,10 +9,11 @@ A step is one pass of the hot path over one bucket resident in HBM:
   * N = 1 (BASELINE configs[1], "1xMI355X: local reduce kernel only, fp32 bucket sweep"): the
     per-hop reduce kernel acc += in over a 256 MiB fp32 bucket; value = bucket GiB/s. A sweep
     4 KiB..1 GiB of the same kernel is reported beside it.
-  * N > 1 (configs[2], ring over xGMI, fp32 256 MiB per rank): one ddl_allreduce (ring
-    reduce-scatter + allgather over RCCL send/recv, HIP reduce kernel); value = N * bucket
-    GiB / max-over-ranks step time (whole job). RCCL's own ncclAllReduce is timed beside it as
-    a comparator.
+  * N > 1 (configs[2], 8xMI355X fp32 256 MiB bucket): one ddl_allreduce of every rank's bucket
+    (autotuned reduce-scatter / allgather over RCCL send/recv, HIP fold kernel, sums in MPICH's
+    order); value = allreduce algbw = bucket GiB / max-over-ranks step time (nccl-tests
+    convention), with busbw = 2(P-1)/P x algbw and its fraction of the link ceiling beside it.
+    RCCL's own ncclAllReduce is timed on the same buffers as a comparator.
 rank 0 prints ONE JSON line.
 """
 import argparse
@@ -58,7 +59,7 @@ def parse():
                          'bench code, its numbers are not measurements')
     ap.add_argument('--watchdog-s', type=float, default=420.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
-    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--cpu-seconds', type=float, default=6.0)
     ap.add_argument('--variant', type=int, default=-1,
                     help='reduce kernel variant bits (-1 default; 1 nt-load a, 2 nt-load b, 4 nt-store, 8 lds b)')
     return ap.parse_args()
@@ -74,9 +75,10 @@ def pmc_traffic(workload_key):
         return None
 
 
-def cpu_baseline(n_bytes_sample, seconds):
+def cpu_reduce_port(n_bytes_sample, seconds):
     """The oracle's MPI_SUM restatement (oracle/ddl_oracle.c, 1 thread) on a bounded sample of
-    the same workload: acc += in over a fp32 bucket of n_bytes_sample, repeated ~`seconds`."""
+    the N=1 kernel workload: acc += in over a fp32 bucket of n_bytes_sample, repeated ~`seconds`
+    (what MPICH's reduction op does per hop on the CPU; not the reference's whole path)."""
     import numpy as np
     lib = ctypes.CDLL(os.path.join(ROOT, 'oracle', 'build', 'libddl_oracle.so'))
     lib.ddlo_reduce_reps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -94,37 +96,59 @@ def cpu_baseline(n_bytes_sample, seconds):
     dt = time.perf_counter() - t0
     return {'value': round(n_bytes_sample * reps / dt / GiB, 3), 'unit': 'GiB/s', 'cores': 1, 'kind': 'port',
             'sample': f'oracle ddlo_sum2 acc+=in, fp32 {n_bytes_sample >> 20} MiB x {reps} reps '
-                      f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM on the reference data plane'}
+                      f'({dt:.1f} s, 1 thread) — restatement of MPICH MPI_SUM, the per-element op only'}
 
 
-def cpu_reference_path():
-    """The reference's whole CPU+MPI loopback path (3-lap token ring over MPI p2p, fusion memcpy,
-    MPI_Allreduce) as a labelled C restatement (oracle/ref_path_port.c; the reference itself is
-    unbuildable here), under MPICH with P ranks on the host cores: C1 (fp32[1024])
-    at P = 2 and 8, the C3 bucket shape (256 MiB fp32) at P = 2 and 8, and a bounded C5-like
-    many-tensor sample (fp32 only: the reference rejects fp16) at P = 8. About 10-20 s."""
+def _ref_path_leg(P, n, ntens, reps, timeout=180):
+    """One run of oracle/ref_path_port.c (the reference's CPU path: handler send/recv threads,
+    3-lap token, fusion memcpy, MPI_Allreduce) under MPICH with P ranks on the host cores."""
     import shutil
     import subprocess
     exe = os.path.join(ROOT, 'oracle', 'build', 'ref_path_port')
     mpiexec = '/opt/conda/bin/mpiexec'
     if not (os.path.exists(exe) and shutil.which(mpiexec)):
-        return {'value': None, 'reason': 'MPICH or oracle/build/ref_path_port missing on this host'}
+        return {'error': 'MPICH or oracle/build/ref_path_port missing on this host'}
     env = dict(os.environ)
     env['LD_LIBRARY_PATH'] = '/opt/conda/lib:' + env.get('LD_LIBRARY_PATH', '')
-    res = {'kind': 'port', 'what': 'oracle/ref_path_port.c: reference token ring + fusion + MPI_Allreduce '
-                                   '(MPICH 3.3.2 loopback), one rank per host core'}
+    env.setdefault('TMPDIR', '/tmp')
+    try:
+        p = subprocess.run([mpiexec, '-n', str(P), exe, str(n), str(ntens), str(reps)], capture_output=True,
+                           text=True, timeout=timeout, env=env)
+        r = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {'error': p.stderr[-300:]}
+    except Exception as e:  # never let the baseline leg break the bench line
+        r = {'error': repr(e)}
+    r['cores'] = P * 3  # threads: main + handler send + handler recv per rank
+    return r
+
+
+def cpu_baseline():
+    """cpu_baseline (the reference's own CPU+MPI loopback path on this box's host cores): the C3
+    bucket shape (256 MiB fp32) through oracle/ref_path_port.c at P = 2 MPI ranks — the
+    reference's handler threads, 3-lap token, fusion memcpy and MPI_Allreduce — best of 8 after
+    a warm-up (~10 s of CPU work)."""
+    r = _ref_path_leg(2, 64 << 20, 1, 8)
+    if 'GiBs' not in r:
+        return {'value': None, 'unit': 'GiB/s', 'cores': r.get('cores'), 'kind': 'port', 'error': r.get('error')}
+    return {'value': r['GiBs'], 'unit': 'GiB/s', 'cores': r['cores'], 'kind': 'port',
+            'sample': 'reference CPU path restated (oracle/ref_path_port.c): one 256 MiB fp32 bucket, 2 MPICH '
+                      f'ranks x 3 threads, best {r["best_ms"]} ms of 8 (mean {r["mean_ms"]} ms)',
+            'nproc': os.cpu_count()}
+
+
+def cpu_reference_path():
+    """The reference's whole CPU+MPI loopback path (oracle/ref_path_port.c: per-communicator
+    send / recv handler threads with the cond-var token queue, 3-lap ring token over MPI p2p,
+    fusion memcpy, MPI_Allreduce, per-round log lines) under MPICH with P ranks on the host
+    cores: C1 (fp32[1024]) at P = 2 and 8, the C3 bucket shape (256 MiB fp32) at
+    P = 8, and a bounded C5-like many-tensor sample (fp32 only: the reference rejects fp16) at
+    P = 8. About 10-20 s."""
+    res = {'kind': 'port', 'nproc': os.cpu_count(),
+           'what': 'oracle/ref_path_port.c: reference handler threads + token ring + fusion + MPI_Allreduce '
+                   '(MPICH 3.3.2 loopback), 3 threads per rank'}
     legs = (('C1_fp32_1024_P2', 2, 1024, 1, 200), ('C1_fp32_1024_P8', 8, 1024, 1, 100),
-            ('C3shape_fp32_256MiB_P2', 2, 64 << 20, 1, 3), ('C3shape_fp32_256MiB_P8', 8, 64 << 20, 1, 2),
-            ('C5like_fp32_512x256KiB_P8', 8, 64 << 10, 512, 2))
+            ('C3shape_fp32_256MiB_P8', 8, 64 << 20, 1, 2), ('C5like_fp32_512x256KiB_P8', 8, 64 << 10, 512, 2))
     for tag, P, n, ntens, reps in legs:
-        try:
-            p = subprocess.run([mpiexec, '-n', str(P), exe, str(n), str(ntens), str(reps)], capture_output=True,
-                               text=True, timeout=120, env=env)
-            r = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else {'error': p.stderr[-300:]}
-            r['cores'] = P
-            res[tag] = r
-        except Exception as e:  # never let the baseline leg break the bench line
-            res[tag] = {'error': repr(e)}
+        res[tag] = _ref_path_leg(P, n, ntens, reps)
     return res
 
 
@@ -242,8 +266,11 @@ def single_gpu(args):
     if not args.no_fusion:
         del sets
         out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5, forced=not args.no_forced_data_plane)
+        if not args.no_host:
+            out['keyed_host_c5'] = keyed_host_c5(lib, Communicator.world(), steps=3)
     if not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(64 << 20, args.cpu_seconds)
+        out['cpu_baseline'] = cpu_baseline()
+        out['cpu_reduce_op_port'] = cpu_reduce_port(64 << 20, args.cpu_seconds)
         out['cpu_reference_path'] = cpu_reference_path()
     emit(out)
 
@@ -391,6 +418,51 @@ def fusion_c5(lib, comm, dev, steps, k=4096, forced=True):
     return res
 
 
+def keyed_host_c5(lib, comm, steps, k=4096):
+    """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
+    buffers) through the keyed path: negotiation, dtype groups, plans, then per plan pinned-chunk
+    staging — host pack -> H2D -> allreduce -> D2H -> host unpack (ddl_allreduce_submit_batch_mem,
+    DDL_MEMORY_HOST). At one rank the data plane is forced (one_rank_shortcut = 0). The rate is
+    PCIe-bound (2 x bytes cross the host link); it is never `value`."""
+    import numpy as np
+    import torch
+    from ddl.torch.cpp_backend import DONE_FN, MEMORY_HOST, check
+    rng = np.random.default_rng(5)
+    sizes = (np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=k)).astype(np.int64) // 256) * 256
+    order = rng.permutation(k)
+    tensors, dts, keys = [], [], []
+    for i in order:
+        half = rng.random() < 0.5
+        n = int(sizes[i]) // (2 if half else 4)
+        tensors.append(torch.randn(n).to(torch.float16 if half else torch.float32))
+        dts.append(19 if half else 1)
+        keys.append(f'hgrad_{i:05d}'.encode())
+    total = sum(t.numel() * t.element_size() for t in tensors)
+    K, V = ctypes.c_char_p * k, ctypes.c_void_p * k
+    ptrs = V(*[t.data_ptr() for t in tensors])
+    args = (k, K(*keys), ptrs, ptrs, (ctypes.c_size_t * k)(*[t.numel() for t in tensors]), (ctypes.c_int * k)(*dts),
+            0, MEMORY_HOST, None, DONE_FN(), None)
+    old = lib.ddl_get_config(b'one_rank_shortcut')
+    try:
+        check(lib.ddl_set_config(b'one_rank_shortcut', 0), 'ddl_set_config')
+
+        def step():
+            check(lib.ddl_allreduce_submit_batch_mem(comm.id, *args), 'ddl_allreduce_submit_batch_mem')
+            check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
+        step()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        lib.ddl_set_config(b'one_rank_shortcut', old)
+    return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3), 'bucket_GiBs': round(total / GiB / dt, 2),
+            'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
+            'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
+            'path': 'pageable host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
+                    'allreduce, D2H, host unpack), in place'}
+
+
 def host_resident_rate(lib, comm, S, reps):
     """Deployment case: the bucket starts and ends in (pinned) host memory; ddl_allreduce_host
     pipelines H2D -> device ring -> D2H in 32 MiB chunks. PCIe-inclusive rate, never `value`."""
@@ -517,12 +589,12 @@ def multi_gpu(args):
     ms = sec * 1e3
     algbw = S / GiB / sec
     busbw_gbs = 2 * (world - 1) / world * S / sec / 1e9
-    link_ceiling = min(HBM_PEAK_GBS * 2 / 7, 7 * XGMI_LINK_GBS)  # SURVEY §8d, L = 7 links
+    ceiling = link_ceiling(world)
     avg_kernel_ms = kms.value / max(1, launches.value)
     achieved = kbytes.value / max(1e-9, kms.value / 1e3) / 1e9
     out = {
         'metric': 'device-resident allreduce GiB/s vs bucket size at 1/2/4/8 MI355X',
-        'value': round(world * S / GiB / sec, 2),
+        'value': round(algbw, 2),
         'unit': 'GiB/s',
         'n_gpus': world,
         'steps': args.steps,
@@ -538,9 +610,11 @@ def multi_gpu(args):
                                f'{args.bucket_mib} MiB bucket per rank, {world}xMI355X',
                    'bucket_bytes': S, 'parallelism': f'dp{world}',
                    'reference_order': lib.ddl_get_config(b'reference_order')},
+        'value_is': 'allreduce algbw: bucket bytes / max-over-ranks time per allreduce (GiB/s)',
         'algbw_GiBs': round(algbw, 2),
         'busbw_GBs': round(busbw_gbs, 2),
-        'link_roofline': {'bound': 'xgmi', 'ceiling_GBs': link_ceiling, 'frac': round(busbw_gbs / link_ceiling, 4)},
+        'link_roofline': dict(ceiling, frac=round(busbw_gbs / ceiling['busbw_ceiling_GBs'], 4),
+                              algbw_frac=round(algbw * GiB / 1e9 / ceiling['algbw_ceiling_GBs'], 4)),
         'autotune': tune,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
@@ -554,6 +628,10 @@ def multi_gpu(args):
     if args.rehearse:
         out['rehearsal'] = 'point-to-point over gloo host copies on one GPU: exercises the N>1 legs, NOT a measurement'
     state['out'] = out  # from here on a hung optional leg still reports the headline result
+    # parity on this node first, so no optional leg can hide it: every rank's result equals
+    # MPI_Allreduce's (MPICH 3.3.2 order) bit for bit, on both sides of MPICH's 2048-byte switch
+    state['leg'] = 'parity'
+    out['parity_vs_mpich_order'] = parity_leg(lib, comm, dist, torch, dev, stream, rank, world)
 
     state['leg'] = 'rccl_comparator'
     if not args.rehearse:
@@ -621,10 +699,6 @@ def multi_gpu(args):
     state['leg'] = 'fusion_c5'
     if not args.no_fusion:
         out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
-    # parity on this node: every rank's result equals MPI_Allreduce's (MPICH 3.3.2 order) bit
-    # for bit, on both sides of MPICH's 2048-byte switch, through the schedule the engine runs
-    state['leg'] = 'parity'
-    out['parity_vs_mpich_order'] = parity_leg(lib, comm, dist, torch, dev, stream, rank, world)
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
     # size class) next to RCCL's own ncclAllReduce on the same buffers
     state['leg'] = 'size_sweep'
@@ -666,6 +740,23 @@ def multi_gpu(args):
     finalize()
     dist.destroy_process_group()
     dog.cancel()
+
+
+def link_ceiling(P, S=None):
+    """Roofline of one allreduce at P ranks, in busbw = 2(P-1)/P x S / t terms.
+    The reference-order direct schedule (what runs at P > 2): each rank sends chunk-slices to its
+    P-1 peers at once in the reduce-scatter and again in the allgather, so each of its P-1 xGMI
+    links carries 2S/P per allreduce -> t >= 2S / (P x B_link), busbw <= (P-1) x B_link (the
+    same as P-1 edge-disjoint rings). HBM per rank: (5P-3)/P x S bytes (RS send reads + staging
+    writes, the fold's P inputs + 1 output, AG send reads + receive writes) -> busbw <=
+    2(P-1)/(5P-3) x HBM. The ceiling is the smaller."""
+    links = (P - 1) * XGMI_LINK_GBS
+    hbm = 2 * (P - 1) / (5 * P - 3) * HBM_PEAK_GBS
+    bus = min(links, hbm)
+    return {'bound': 'xgmi' if links <= hbm else 'hbm', 'busbw_ceiling_GBs': round(bus, 1),
+            'algbw_ceiling_GBs': round(bus * P / (2 * (P - 1)), 1), 'link_GBs': XGMI_LINK_GBS,
+            'links_used': P - 1, 'hbm_term_GBs': round(hbm, 1),
+            'formula': 'busbw <= min((P-1) x B_link, 2(P-1)/(5P-3) x HBM)'}
 
 
 def mpich_order_sum(xs, message_bytes):

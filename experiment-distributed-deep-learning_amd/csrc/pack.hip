@@ -39,37 +39,19 @@ __device__ inline void copy_bytes(char *dst, const char *src, uint32_t m) {
     for (uint32_t k = 0; k < m; ++k) dst[k] = src[k];
 }
 
-// Last segment with off <= x: wave-parallel search, 64 samples per round (2 rounds for 4096
-// segments instead of 12 dependent loads of a binary search). Called by all 64 lanes of a wave.
-__device__ int find_segment(const SegDesc *__restrict__ d, int count, uint64_t x) {
-    const int lane = threadIdx.x & 63;
-    int lo = 0, hi = count;  // answer in [lo, hi)
-    while (hi - lo > 1) {
-        const int step = (hi - lo + 63) / 64;
-        const int idx = lo + lane * step;
-        const bool ok = idx < hi && d[idx].off <= x;
-        const unsigned long long m = __ballot(ok);  // d[lo].off <= x, so lane 0 is always set
-        const int last = 63 - __builtin_clzll(m);
-        lo += last * step;
-        hi = min(lo + step, hi);
-    }
-    return lo;
-}
-
-// dir 0: gather segments -> flat; dir 1: scatter flat -> segments. One workgroup of THREADS
-// lanes per span of THREADS * 16 * kIters bytes of the flat buffer: wave 0 finds the span's first
-// segment and stages the next kSegs descriptors in LDS; every lane then resolves its kIters
-// chunks from LDS, issues all kIters loads, then all kIters stores (no dependent descriptor
-// loads between data accesses). Spans holding more than kSegs segments resolve the rest from
-// global memory. Small spans (2 chunks per lane, 4 KiB per 128-lane workgroup) keep the chunks
-// in flight a compact, interleaved window of each stream, as the reduce kernel's one-tile-per-
-// workgroup mapping does; tools/copy_tune.hip: 1R+1W copies reach 6.5 TB/s with 2-4 KiB tiles
-// per workgroup vs 5.3 TB/s with 64 KiB.
+// dir 0: gather segments -> flat; dir 1: scatter flat -> segments.
 // Segment-aligned tiling: every segment is cut into tiles of THREADS * 16 * kIters bytes that
 // restart at the segment start, so a tile never crosses a segment and its workgroup needs no
 // per-chunk search: tile_seg[t] (k_tile_index: one thread per tile, binary search of the
 // tile0 column) names the segment, one scalar descriptor load gives ptr / off / len, and lane l
-// moves bytes [16 l + it * THREADS * 16, ...) of the tile.
+// moves bytes [16 l + it * THREADS * 16, ...) of the tile. Small tiles (1 KiB per 64-lane
+// workgroup) keep the chunks in flight a compact window of each stream (tools/copy_tune.hip:
+// 1R+1W copies reach 6.5 TB/s with 1-2 KiB per workgroup vs 5.3 TB/s with 64 KiB).
+// XCD grouping: the dispatcher deals workgroups round-robin over the 8 XCDs, each with its own
+// L2, so with tile = blockIdx every XCD would fetch every 64-byte line of tile_seg (16 tiles)
+// and the descriptor it points at: 8x the index bytes from HBM (+3 % traffic on the C5 set,
+// r01 PMC). Inside each run of 128 workgroups, XCD x takes 16 consecutive tiles — one
+// tile_seg line — so each line is fetched once, and the window stays 128 tiles wide.
 __global__ void __launch_bounds__(256) k_tile_index(const SegDesc *__restrict__ d, int count, uint64_t tiles,
                                                     int *__restrict__ tile_seg) {
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -87,8 +69,13 @@ template <int DIR, int kIters, int THREADS>
 __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc *__restrict__ d,
                                                        const int *__restrict__ tile_seg) {
     constexpr uint64_t kTile = (uint64_t)THREADS * 16 * kIters;
-    const SegDesc sd = d[tile_seg[blockIdx.x]];
-    const uint64_t base = (uint64_t)(blockIdx.x - sd.tile0) * kTile;  // tile start inside the segment
+    constexpr unsigned kXcds = 8, kLine = 16, kRun = kXcds * kLine;
+    const unsigned bid = blockIdx.x;
+    const unsigned full = gridDim.x - gridDim.x % kRun;  // the tail keeps tile = blockIdx
+    const unsigned r = bid % kRun;
+    const unsigned tile = bid < full ? bid - r + (r % kXcds) * kLine + r / kXcds : bid;
+    const SegDesc sd = d[tile_seg[tile]];
+    const uint64_t base = (uint64_t)(tile - sd.tile0) * kTile;  // tile start inside the segment
     char *fl = flat + sd.off;
     char *tp = reinterpret_cast<char *>(sd.ptr);
     if (!sd.vec) {  // misaligned tensor: bytes
@@ -115,95 +102,6 @@ __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc
             if (DIR == 0) copy_bytes(fl + b, tp + b, m);
             else copy_bytes(tp + b, fl + b, m);
         }
-    }
-}
-
-template <int DIR, int kIters, bool NT_STORE, int THREADS, int kSegs>
-__global__ void __launch_bounds__(THREADS) k_segments(char *flat, const SegDesc *__restrict__ d, int count,
-                                                      uint64_t total) {
-    constexpr uint64_t kTileBytes = (uint64_t)THREADS * 16;
-    constexpr uint64_t kSpanBytes = kTileBytes * kIters;
-    static_assert(kSegs <= 64 && (kSegs & (kSegs - 1)) == 0, "LDS descriptor table: power of two <= 64");
-    __shared__ uint64_t s_off[kSegs + 1], s_len[kSegs], s_ptr[kSegs];
-    __shared__ int s_vec[kSegs];
-    __shared__ int s_seg0;
-    const uint64_t span0 = (uint64_t)blockIdx.x * kSpanBytes;
-    if (threadIdx.x < 64) {
-        const int seg0 = find_segment(d, count, span0);
-        const int i = seg0 + (int)threadIdx.x;
-        if (threadIdx.x < kSegs) {
-            if (i < count) {
-                s_off[threadIdx.x] = d[i].off;
-                s_len[threadIdx.x] = d[i].len;
-                s_ptr[threadIdx.x] = d[i].ptr;
-                s_vec[threadIdx.x] = (int)d[i].vec;
-            } else {
-                s_off[threadIdx.x] = ~0ull;
-                s_len[threadIdx.x] = 0;
-            }
-        }
-        if (threadIdx.x == 0) {
-            s_off[kSegs] = seg0 + kSegs < count ? d[seg0 + kSegs].off : ~0ull;
-            s_seg0 = seg0;
-        }
-    }
-    __syncthreads();
-    // resolve: the tensor-side address of each of this lane's 16-byte chunks (0 = padding or
-    // already copied by the byte path, which handles misaligned and partial chunks at once)
-    uint64_t addr[kIters];
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-        const uint64_t o = span0 + (uint64_t)it * kTileBytes + (uint64_t)threadIdx.x * 16;
-        addr[it] = 0;
-        if (o >= total) continue;
-        // branchless binary search of the LDS offsets (s_off[0] <= span0 <= o; entries past
-        // the table are ~0): s = last staged segment starting at or before o, 64 = beyond
-        int s = 0;
-#pragma unroll
-        for (int step = kSegs / 2; step > 0; step >>= 1) s = s_off[s + step] <= o ? s + step : s;
-        if (s == kSegs - 1 && s_off[kSegs] <= o) s = kSegs;
-        uint64_t off, len, ptr;
-        int vec;
-        if (s < kSegs) {
-            off = s_off[s];
-            len = s_len[s];
-            ptr = s_ptr[s];
-            vec = s_vec[s];
-        } else {  // dense span: keep walking in global memory
-            int g = s_seg0 + kSegs;
-            while (g + 1 < count && d[g + 1].off <= o) ++g;
-            off = d[g].off;
-            len = d[g].len;
-            ptr = d[g].ptr;
-            vec = (int)d[g].vec;
-        }
-        const uint64_t local = o - off;
-        if (local >= len) continue;  // padding between segments
-        if (vec && local + 16 <= len) {
-            addr[it] = ptr + local;
-        } else {
-            const uint32_t m = (uint32_t)(len - local < 16 ? len - local : 16);
-            if (DIR == 0) copy_bytes(flat + o, reinterpret_cast<const char *>(ptr + local), m);
-            else copy_bytes(reinterpret_cast<char *>(ptr + local), flat + o, m);
-        }
-    }
-    u32x4 v[kIters];
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-        if (!addr[it]) continue;
-        const char *src = DIR == 0 ? reinterpret_cast<const char *>(addr[it])
-                                   : flat + span0 + (uint64_t)it * kTileBytes + threadIdx.x * 16;
-        // every byte is read once: non-temporal loads (and stores, by default: the consumer —
-        // the collective or the optimizer — comes after the whole bucket is copied)
-        v[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-    }
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-        if (!addr[it]) continue;
-        char *fl = flat + span0 + (uint64_t)it * kTileBytes + threadIdx.x * 16;
-        u32x4 *dst = reinterpret_cast<u32x4 *>(DIR == 0 ? fl : reinterpret_cast<char *>(addr[it]));
-        if (NT_STORE) __builtin_nontemporal_store(v[it], dst);
-        else *dst = v[it];
     }
 }
 
@@ -257,18 +155,16 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     DDL_REQUIRE(flat && segs && bytes, DDL_STATUS_INVALID_ARGUMENT, "null pack arguments");
     const size_t need = (size_t)count * sizeof(SegDesc);
     Slot &sl = free_slot_();
-    // DDL_PACK_VARIANT (measurement only; tools/pack_tune.py, C5 bucket set, pack / unpack):
-    //   0: span kernel, 256 lanes x 16 chunks per 64 KiB span, in-kernel segment search  5.56 / 5.61 TB/s
-    //   1: segment tiles of 1 KiB, 64 lanes (default)                                     6.10 / 6.37
+    // DDL_PACK_VARIANT (measurement only; tools/pack_tune.py, C5 bucket set, pack / unpack, r01):
+    //   1: segment tiles of 1 KiB, 64 lanes (default)                                     6.10 / 6.37 TB/s
     //   2: segment tiles of 2 KiB, 128 lanes                                              6.09 / 6.29
     //   3: segment tiles of 4 KiB, 128 lanes x 2 chunks                                   5.74 / 6.30
-    // (spans of 2-8 KiB with the in-kernel search, with or without a precomputed first segment
-    // per span, measured 4.5-6.0: the per-chunk search and the LDS round trip cost more than
-    // the smaller window saves.)
+    // (the r01 span kernel — 64 KiB spans with an in-kernel segment search — measured 5.56 / 5.61
+    // and is gone; spans of 2-8 KiB with the search measured 4.5-6.0.)
     static const int variant = [] {
         const char *e = std::getenv("DDL_PACK_VARIANT");
         const int v = e ? std::atoi(e) : 1;
-        return v >= 0 && v <= 3 ? v : 1;
+        return v >= 1 && v <= 3 ? v : 1;
     }();
     if (need > sl.cap) {
         if (sl.host) DDL_HIP(hipHostFree(sl.host));
@@ -297,12 +193,7 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     DDL_HIP(hipMemcpyAsync(sl.dev, sl.host, need, hipMemcpyHostToDevice, stream));
     char *fl = static_cast<char *>(flat);
     const SegDesc *dd = static_cast<const SegDesc *>(sl.dev);
-    if (variant == 0) {
-        const uint64_t spans = (off + 65535) / 65536;
-        DDL_REQUIRE(spans < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
-        if (dir == 0) hipLaunchKernelGGL((k_segments<0, 16, true, 256, 64>), dim3((unsigned)spans), dim3(256), 0, stream, fl, dd, count, (uint64_t)off);
-        else hipLaunchKernelGGL((k_segments<1, 16, true, 256, 64>), dim3((unsigned)spans), dim3(256), 0, stream, fl, dd, count, (uint64_t)off);
-    } else if (tiles > 0) {
+    if (tiles > 0) {
         const size_t ib = tiles * sizeof(int);
         if (ib > sl.idx_cap) {
             if (sl.idx) DDL_HIP(hipFree(sl.idx));

@@ -1,5 +1,6 @@
-"""Pack/unpack kernel variants on the C5 bucket set (run on the GPU box):
-DDL_PACK_VARIANT bit 0 = non-temporal stores, bit 1 = 32 chunks per lane instead of 16."""
+"""Pack/unpack kernel variants on the C5 bucket set (run on the GPU box): DDL_PACK_VARIANT 1, 2,
+3 = segment tiles of 1 KiB (64 lanes, default), 2 KiB (128 lanes), 4 KiB (128 lanes x 2).
+`python tools/pack_tune.py child` runs the current variant once (e.g. under rocprofv3 --pmc)."""
 import ctypes
 import os
 import subprocess
@@ -8,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 if len(sys.argv) == 1:
-    for v in [int(x) for x in os.environ.get('VARIANTS', '0 1 2 3').split()]:
+    for v in [int(x) for x in os.environ.get('VARIANTS', '1 2 3').split()]:
         env = dict(os.environ, DDL_PACK_VARIANT=str(v))
         out = subprocess.run([sys.executable, __file__, 'child'], env=env, capture_output=True, text=True, timeout=300)
         print(f'variant {v}: {out.stdout.strip()} {out.stderr.strip()[-300:] if out.returncode else ""}', flush=True)

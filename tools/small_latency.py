@@ -1,0 +1,91 @@
+"""Small-bucket latency, host vs device (measurement tool, not shipped).
+
+For 4 KiB .. 4 MiB fp32 buckets:
+  * the per-hop reduce (ddl_reduce_local, one kernel launch): host enqueue us per call (no sync),
+    wall us per call back to back, device us between events;
+  * the allreduce of P = 8 virtual ranks over the RCCL loopback (one-shot and direct schedules,
+    reference order): the same three numbers per allreduce.
+Run it under `rocprofv3 --kernel-trace --stats` to get each kernel's own duration; the
+summariser (scripts/prof_small.py) splits the trace by grid size. Prints JSON lines.
+
+    python tools/small_latency.py [--reps 200] [--graph 0|1]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
+SIZES = [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20]
+
+
+def timed(fn, reps, torch, stream):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    t_host = time.perf_counter() - t0
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t_wall = time.perf_counter() - t0
+    return {'host_us': round(t_host / reps * 1e6, 2), 'wall_us': round(t_wall / reps * 1e6, 2),
+            'device_us': round(e0.elapsed_time(e1) / reps * 1e3, 2)}
+
+
+def main():
+    import torch
+    from ddl.torch.cpp_backend import CPPBackend, check
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reps', type=int, default=200)
+    ap.add_argument('--graph', type=int, default=-1, help='ddl config "graph_cache" (-1: leave as is)')
+    ap.add_argument('--P', type=int, default=8)
+    ap.add_argument('--no-loopback', action='store_true')
+    a = ap.parse_args()
+    lib = CPPBackend.c_api()
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    s = torch.cuda.current_stream(dev)
+    sh = s.cuda_stream
+    if a.graph >= 0:
+        check(lib.ddl_set_config(b'graph_cache', a.graph), 'ddl_set_config')
+    for size in SIZES:
+        m = size // 4
+        x, y = torch.zeros(m, device=dev), torch.ones(m, device=dev)
+        r = timed(lambda: check(lib.ddl_reduce_local(x.data_ptr(), y.data_ptr(), m, 1, sh), 'reduce'), a.reps, torch, s)
+        print(json.dumps(dict(r, what='reduce_local', bytes=size)), flush=True)
+    for size in SIZES:  # the P = 8 fold of one chunk (7 received inputs), MPICH order
+        m = size // 4
+        bufs = [torch.randn(m, device=dev) for _ in range(9)]
+        ins = (ctypes.c_void_p * 7)(*[t.data_ptr() for t in bufs[1:8]])
+        r = timed(lambda: check(lib.ddl_reduce_fold_ordered(bufs[8].data_ptr(), bufs[0].data_ptr(), ins, 7, m, 1, 1, sh),
+                                'fold'), a.reps, torch, s)
+        print(json.dumps(dict(r, what='fold_P8_chunk', bytes=size,
+                              fold_variant=os.environ.get('DDL_FOLD_VARIANT', 'default'))), flush=True)
+    if a.no_loopback:
+        return
+    check(lib.ddl_rccl_loopback_init(0), 'ddl_rccl_loopback_init')
+    P = a.P
+    check(lib.ddl_set_config(b'tune', 0), 'ddl_set_config')
+    for algo, name in ((2, 'oneshot'), (1, 'direct')):
+        check(lib.ddl_set_config(b'algo', algo), 'ddl_set_config')
+        for size in SIZES:
+            m = size // 4
+            ins = [torch.randn(m, device=dev) for _ in range(P)]
+            outs = [torch.empty_like(t) for t in ins]
+            send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+            recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+            r = timed(lambda: check(lib.ddl_rccl_loopback_allreduce(P, send, recv, m, 1, sh), 'loopback'),
+                      max(20, a.reps // 4), torch, s)
+            print(json.dumps(dict(r, what=f'loopback_allreduce_{name}_P{P}', bytes=size)), flush=True)
+    check(lib.ddl_rccl_loopback_finalize(), 'ddl_rccl_loopback_finalize')
+
+
+if __name__ == '__main__':
+    main()
