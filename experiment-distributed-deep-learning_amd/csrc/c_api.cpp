@@ -143,6 +143,14 @@ void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len)
     std::memcpy(out, res.c_str(), res.size() + 1);
 }
 
+// The submitter's input-ready event: device requests are ordered after hip_stream's current
+// position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
+std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
+    DDL_REQUIRE(memory == DDL_MEMORY_DEVICE || memory == DDL_MEMORY_HOST, DDL_STATUS_INVALID_ARGUMENT,
+                "memory must be DDL_MEMORY_DEVICE (0) or DDL_MEMORY_HOST (1), not " << memory);
+    return memory == DDL_MEMORY_HOST ? nullptr : std::make_shared<ReadyEvent>(as_stream(hip_stream));
+}
+
 }  // namespace
 
 extern "C" {
@@ -286,8 +294,9 @@ int ddl_set_config(const char *key, long long value) {
         Config &c = config();
         if (k == "slice_bytes") c.slice_bytes = value;
         else if (k == "algo") {
-            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect || value == kAlgoOneShot,
-                        DDL_STATUS_INVALID_ARGUMENT, "algo must be 0 (ring), 1 (direct) or 2 (one-shot)");
+            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect || value == kAlgoOneShot || value == kAlgoGatherFold,
+                        DDL_STATUS_INVALID_ARGUMENT,
+                        "algo must be 0 (ring), 1 (direct), 2 (one-shot) or 3 (gather-fold)");
             c.algo = value;
         } else if (k == "rings") c.rings = value;
         else if (k == "max_slices") c.max_slices = value;
@@ -497,16 +506,6 @@ int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int
         export_tune(r, chosen, count, configs, ms, max_candidates);
     });
 }
-
-namespace {
-// The submitter's input-ready event: device requests are ordered after hip_stream's current
-// position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
-std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
-    DDL_REQUIRE(memory == DDL_MEMORY_DEVICE || memory == DDL_MEMORY_HOST, DDL_STATUS_INVALID_ARGUMENT,
-                "memory must be DDL_MEMORY_DEVICE (0) or DDL_MEMORY_HOST (1), not " << memory);
-    return memory == DDL_MEMORY_HOST ? nullptr : std::make_shared<ReadyEvent>(as_stream(hip_stream));
-}
-}  // namespace
 
 int ddl_allreduce_submit_mem(ddl_communicator_id id, const char *key, const void *in, void *out, size_t elements,
                              int dtype, int op, int memory, void *hip_stream, ddl_done_fn done, void *user) {
@@ -804,6 +803,15 @@ int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *con
     });
 }
 
+int ddl_rccl_loopback_allgather(const void *send, void *recv, size_t bytes, void *hip_stream) {
+    return guarded([&] {
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        DDL_REQUIRE(l.comm != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_rccl_loopback_init has not been called");
+        RcclTransport(l.comm).allgather(GatherOp{send, recv, bytes}, as_stream(hip_stream));
+    });
+}
+
 int ddl_rccl_loopback_max(float *values, int count, void *hip_stream) {
     return guarded([&] {
         DDL_REQUIRE(values, DDL_STATUS_INVALID_ARGUMENT, "null values");
@@ -928,6 +936,14 @@ void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t
             decode(c.src, &sbuf, &soff);
             DDL_REQUIRE(sbuf == 0, DDL_STATUS_ERROR_UNKNOWN, "copy source outside the input");
             long long row[8] = {(long long)t, 4, -1, -1, dbuf, doff, (long long)(c.bytes / es), soff};
+            rows.insert(rows.end(), row, row + 8);
+        }
+        if (tk.gather.bytes) {
+            // {tick, 11, send buffer, send offset, recv buffer, recv offset, elements per rank, 0}
+            long long sbuf, soff, rbuf, roff;
+            decode(tk.gather.send, &sbuf, &soff);
+            decode(tk.gather.recv, &rbuf, &roff);
+            long long row[8] = {(long long)t, 11, sbuf, soff, rbuf, roff, (long long)(tk.gather.bytes / es), 0};
             rows.insert(rows.end(), row, row + 8);
         }
         for (const P2POp &op : tk.ops) {

@@ -65,7 +65,7 @@ Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std:
     std::unique_ptr<Transport> t;
     if (size_ > 1) {
         if (hooks_) {
-            cb_ = new CallbackTransport(hooks_, tag_, world_ranks_);
+            cb_ = new CallbackTransport(hooks_, tag_, world_ranks_, rank_, size_);
             t.reset(cb_);
         } else {
             t.reset(new RcclTransport(nccl_));
@@ -143,7 +143,10 @@ std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &b
     }
     // latency-bound buckets: one group (whole bucket to every peer) instead of two or more;
     // costs (P-1) x the bucket in wire bytes and staging, so only small buckets
-    if (bytes <= kOneShotMaxBytes) add(kAlgoOneShot, 1, 0, 1);
+    if (bytes <= kOneShotMaxBytes) {
+        add(kAlgoOneShot, 1, 0, 1);
+        add(kAlgoGatherFold, 1, 0, 1);  // the same fold after one ncclAllGather
+    }
     return c;
 }
 

@@ -20,6 +20,22 @@ void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     rccl_check(e, "ncclGroupEnd");
 }
 
+void RcclTransport::allgather(const GatherOp &g, hipStream_t stream) {
+    rccl_check(rccl().AllGather(g.send, g.recv, g.bytes, ncclInt8, comm_, stream), "ncclAllGather");
+}
+
+void CallbackTransport::allgather(const GatherOp &g, hipStream_t stream) {
+    char *recv = static_cast<char *>(g.recv);
+    DDL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * g.bytes, g.send, g.bytes, hipMemcpyDeviceToDevice, stream));
+    std::vector<P2POp> ops;
+    for (int d = 1; d < size_; ++d) {
+        const int to = (rank_ + d) % size_, from = (rank_ + size_ - d) % size_;
+        ops.push_back(P2POp{true, to, 0, const_cast<void *>(g.send), g.bytes});
+        ops.push_back(P2POp{false, from, 0, recv + (size_t)from * g.bytes, g.bytes});
+    }
+    group(ops, stream);
+}
+
 void CallbackTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     if (ops.empty()) return;
     DDL_HIP(hipStreamSynchronize(stream));  // the sends' data and the receive buffers are ready
@@ -186,8 +202,12 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
         }
         for (const CopyOp &c : tk.copies)
             DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, res_.comm));
-        if (transport_) transport_->group(tk.ops, res_.comm);
-        else DDL_REQUIRE(tk.ops.empty(), DDL_STATUS_ERROR_UNKNOWN, "no transport for a multi-rank program");
+        if (transport_) {
+            if (tk.gather.bytes) transport_->allgather(tk.gather, res_.comm);
+            transport_->group(tk.ops, res_.comm);
+        } else {
+            DDL_REQUIRE(tk.ops.empty() && !tk.gather.bytes, DDL_STATUS_ERROR_UNKNOWN, "no transport for a multi-rank program");
+        }
         if (tk.has_reduce) {
             DDL_HIP(hipEventRecord(res_.comm_ev[t], res_.comm));
             DDL_HIP(hipStreamWaitEvent(res_.compute, res_.comm_ev[t], 0));
@@ -303,6 +323,38 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             for (const CopyOp &c : tk.copies)
                 DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, rr.comm));
             DDL_HIP(hipEventRecord(rr.pre_ev[t], rr.comm));
+        }
+        // 1b) allgather ticks: rank q's block into every rank's recv at q * bytes, once q has
+        //     reached the tick (copies, or self pairs through RCCL on the loopback)
+        if (progs_[0].ticks[t].gather.bytes) {
+            std::vector<P2POp> pairs;
+            for (int r = 0; r < P_; ++r) {
+                const GatherOp &g = progs_[r].ticks[t].gather;
+                for (int q = 0; q < P_; ++q) {
+                    const GatherOp &src = progs_[q].ticks[t].gather;
+                    DDL_REQUIRE(src.bytes == g.bytes, DDL_STATUS_ERROR_UNKNOWN, "local world: allgather sizes differ");
+                    char *dst = static_cast<char *>(g.recv) + (size_t)q * g.bytes;
+                    if (loop_) {
+                        pairs.push_back(P2POp{true, 0, 0, const_cast<void *>(src.send), g.bytes});
+                        pairs.push_back(P2POp{false, 0, 0, dst, g.bytes});
+                    } else {
+                        DDL_HIP(hipStreamWaitEvent(res_[r]->comm, res_[q]->pre_ev[t], 0));
+                        DDL_HIP(hipMemcpyAsync(dst, src.send, g.bytes, hipMemcpyDeviceToDevice, res_[r]->comm));
+                    }
+                }
+            }
+            if (loop_) {
+                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(loop_stream_, res_[r]->pre_ev[t], 0));
+                loop_->group(pairs, loop_stream_);
+                DDL_HIP(hipEventRecord(loop_ev_[t], loop_stream_));
+                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, loop_ev_[t], 0));
+                loop_pairs_ += (long long)pairs.size() / 2;
+            } else {
+                // every rank's block is read by the others: none may run ahead and overwrite
+                for (int r = 0; r < P_; ++r) DDL_HIP(hipEventRecord(res_[r]->pre_ev[t], res_[r]->comm));
+                for (int r = 0; r < P_; ++r)
+                    for (int q = 0; q < P_; ++q) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, res_[q]->pre_ev[t], 0));
+            }
         }
         if (loop_) {
             // 2') every matched pair of the tick through RCCL as a self send / self recv, posted

@@ -24,12 +24,15 @@ public:
     virtual ~Transport() = default;
     // Post one tick's sends and recvs as one group on `stream`.
     virtual void group(const std::vector<P2POp> &ops, hipStream_t stream) = 0;
+    // Allgather of `bytes` per rank into recv (rank q's block at q * bytes) on `stream`.
+    virtual void allgather(const GatherOp &g, hipStream_t stream) = 0;
 };
 
 class RcclTransport : public Transport {
 public:
     explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
     void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
+    void allgather(const GatherOp &g, hipStream_t stream) override;  // ncclAllGather
 
 private:
     ncclComm_t comm_;
@@ -50,9 +53,12 @@ struct TestHooks {
 // peer itself when world_ranks is empty).
 class CallbackTransport : public Transport {
 public:
-    CallbackTransport(std::shared_ptr<TestHooks> hooks, long long tag, std::vector<int> world_ranks)
-        : hooks_(std::move(hooks)), tag_(tag), world_ranks_(std::move(world_ranks)) {}
+    CallbackTransport(std::shared_ptr<TestHooks> hooks, long long tag, std::vector<int> world_ranks, int rank,
+                      int size)
+        : hooks_(std::move(hooks)), tag_(tag), world_ranks_(std::move(world_ranks)), rank_(rank), size_(size) {}
     void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
+    // own block copied on the device, the others as one group of sends / recvs
+    void allgather(const GatherOp &g, hipStream_t stream) override;
     // One group of host-buffer operations straight to the callback (no device staging).
     void host_group(std::vector<ddl_p2p_op> &ops);
 
@@ -60,6 +66,7 @@ private:
     std::shared_ptr<TestHooks> hooks_;
     long long tag_;
     std::vector<int> world_ranks_;
+    int rank_, size_;
 };
 
 // Streams, events and staging memory of one rank (reused across calls).

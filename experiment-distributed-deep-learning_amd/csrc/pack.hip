@@ -67,11 +67,11 @@ __global__ void __launch_bounds__(256) k_tile_index(const SegDesc *__restrict__ 
 
 template <int DIR, int kIters, int THREADS>
 __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc *__restrict__ d,
-                                                       const int *__restrict__ tile_seg) {
+                                                       const int *__restrict__ tile_seg, int xcd_group) {
     constexpr uint64_t kTile = (uint64_t)THREADS * 16 * kIters;
     constexpr unsigned kXcds = 8, kLine = 16, kRun = kXcds * kLine;
     const unsigned bid = blockIdx.x;
-    const unsigned full = gridDim.x - gridDim.x % kRun;  // the tail keeps tile = blockIdx
+    const unsigned full = xcd_group ? gridDim.x - gridDim.x % kRun : 0;  // the tail keeps tile = blockIdx
     const unsigned r = bid % kRun;
     const unsigned tile = bid < full ? bid - r + (r % kXcds) * kLine + r / kXcds : bid;
     const SegDesc sd = d[tile_seg[tile]];
@@ -166,6 +166,11 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
         const int v = e ? std::atoi(e) : 1;
         return v >= 1 && v <= 3 ? v : 1;
     }();
+    // DDL_PACK_XCD=0 turns the XCD grouping of tiles off (measurement)
+    static const int xcd = [] {
+        const char *e = std::getenv("DDL_PACK_XCD");
+        return e ? (std::atoi(e) != 0) : 1;
+    }();
     if (need > sl.cap) {
         if (sl.host) DDL_HIP(hipHostFree(sl.host));
         if (sl.dev) DDL_HIP(hipFree(sl.dev));
@@ -206,13 +211,13 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
                            (uint64_t)tiles, ts);
         const dim3 g((unsigned)tiles);
         if (dir == 0) {
-            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<0, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts);
-            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<0, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts);
-            else hipLaunchKernelGGL((k_seg_tiles<0, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts);
+            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<0, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
+            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<0, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
+            else hipLaunchKernelGGL((k_seg_tiles<0, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts, xcd);
         } else {
-            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<1, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts);
-            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<1, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts);
-            else hipLaunchKernelGGL((k_seg_tiles<1, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts);
+            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<1, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
+            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<1, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
+            else hipLaunchKernelGGL((k_seg_tiles<1, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts, xcd);
         }
     }
     DDL_HIP(hipGetLastError());

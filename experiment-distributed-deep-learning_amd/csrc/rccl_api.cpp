@@ -69,6 +69,7 @@ const RcclApi &rccl() {
             bind(h, api.GroupStart, "ncclGroupStart");
             bind(h, api.GroupEnd, "ncclGroupEnd");
             bind(h, api.AllReduce, "ncclAllReduce");
+            bind(h, api.AllGather, "ncclAllGather");
             bind(h, api.GetVersion, "ncclGetVersion");
             bind(h, api.CommCount, "ncclCommCount");
             bind(h, api.CommUserRank, "ncclCommUserRank");

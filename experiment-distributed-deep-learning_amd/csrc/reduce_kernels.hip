@@ -231,15 +231,19 @@ int reduce_threads() {
     return v;
 }
 
-// Fold cache policy (DDL_FOLD_VARIANT, measurement): bit 0 non-temporal loads of the received
-// inputs, bit 1 non-temporal store. Default 3 (every operand streams once): 5.77 TB/s vs 5.50
-// plain on a P=8 chunk (32 MiB fp32, 7 inputs, rotating buffers).
-int fold_variant() {
-    static const int v = [] {
+// Fold cache policy: bit 0 non-temporal loads of the received inputs, bit 1 non-temporal store.
+// Large chunks stream every operand once: 3, 5.77 TB/s vs 5.50 plain on a P=8 chunk (32 MiB
+// fp32, 7 inputs, rotating buffers, r01). Chunks up to 8 MiB (the whole fold's operands fit the
+// 256 MiB Infinity Cache, where RCCL has just written the received slices) read through the
+// caches: 0, 4.6 vs 6.0 us on a 4 MiB chunk (profiles/r02/pack/small_fold_v*.jsonl).
+// DDL_FOLD_VARIANT (0..3) forces one policy for measurement.
+int fold_variant(size_t chunk_bytes) {
+    static const int forced = [] {
         const char *e = std::getenv("DDL_FOLD_VARIANT");
-        return e ? std::atoi(e) & 3 : 3;
+        return e ? std::atoi(e) & 3 : -1;
     }();
-    return v;
+    if (forced >= 0) return forced;
+    return chunk_bytes <= (8u << 20) ? 0 : 3;
 }
 
 // One 4 KiB tile of the output per workgroup: each lane folds its 16 bytes across a and the nb
@@ -314,9 +318,9 @@ void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
     } else {
         if (t.nb == NB) {
-            // cache policy (fold_variant): 3 = every operand non-temporal, measured fastest;
-            // 0 = plain, kept for comparison
-            if (fold_variant() == 0) launch_sumN_order<DT, NB, 0>(t, stream, tiles);
+            // cache policy (fold_variant): 3 = every operand non-temporal (large chunks),
+            // 0 = plain (chunks up to 8 MiB, in cache)
+            if (fold_variant((size_t)t.n * sizeof(typename Add<DT>::S)) == 0) launch_sumN_order<DT, NB, 0>(t, stream, tiles);
             else launch_sumN_order<DT, NB, 3>(t, stream, tiles);
         } else {
             launch_sumN_nb<DT, NB + 1>(t, stream, tiles);

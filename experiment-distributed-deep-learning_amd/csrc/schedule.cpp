@@ -150,6 +150,12 @@ void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg_in, int *R,
         *staging_stride = (n + 63) & ~size_t(63);
         return;
     }
+    if (cfg.algo == kAlgoGatherFold) {  // the allgather's blocks are contiguous: stride = block
+        *R = 1;
+        *K = 1;
+        *staging_stride = gather_stride(n, esize);
+        return;
+    }
     int r = cfg.algo == kAlgoDirect ? 1 : (int)rings_for(P, cfg.rings).size();
     // Small buckets: fewer rings so every message stays >= 64 KiB (latency-bound regime).
     const size_t bytes = n * esize;
@@ -177,8 +183,36 @@ size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cf
     int R, K;
     size_t stride;
     ring_shape(n, esize, P, cfg, &R, &K, &stride);
-    const size_t slots = cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 + fold_temp_slots(P) : 0) : 2 * (size_t)R;
-    return slots * stride;
+    return program_staging_slots(P, cfg.algo, R) * stride;
+}
+
+size_t program_staging_slots(int P, int algo, int R) {
+    if (P <= 1) return 0;
+    if (algo == kAlgoRing) return 2 * (size_t)R;
+    if (algo == kAlgoGatherFold) return (size_t)P + 1 + fold_temp_slots(P);
+    return (size_t)(P - 1 + fold_temp_slots(P));
+}
+
+int fold_temp_count(int K, int order) {
+    const int W = kMaxInputs + 1;
+    if (K <= W) return 0;
+    if (order == kFoldLeft) return 1;  // one running partial
+    int used = 0, level = K;
+    if (order == kFoldMpichTree) {  // pre-folded pairs
+        int pof2 = 1;
+        while (pof2 * 2 <= K) pof2 *= 2;
+        used += K - pof2;
+        level = pof2;
+    }
+    while (level > W) {  // block sums of aligned blocks of W (single leftovers pass through)
+        int next = 0;
+        for (int b = 0; b < level; b += W) {
+            if (std::min(level, b + W) - b > 1) ++used;
+            ++next;
+        }
+        level = next;
+    }
+    return used;
 }
 
 void plan_fold(std::vector<SegTableN> &steps, const std::vector<const void *> &xs, void *out, size_t n, int order,
@@ -242,7 +276,7 @@ void plan_fold(std::vector<SegTableN> &steps, const std::vector<const void *> &x
         level.swap(next);
     }
     step(level, kFoldBinomial, out);
-    DDL_REQUIRE(used <= fold_temp_slots((int)xs.size()), DDL_STATUS_ERROR_UNKNOWN, "fold temp slots exceeded");
+    DDL_REQUIRE(used == fold_temp_count((int)xs.size(), order), DDL_STATUS_ERROR_UNKNOWN, "fold temp slots miscounted");
 }
 
 namespace {
@@ -340,6 +374,37 @@ void build_oneshot(RingProgram &prog, int rank, int P, const char *inb, char *ou
     prog.ticks.push_back(std::move(join));
 }
 
+// Gather-fold for latency-bound buckets: tick 0 gathers every rank's bucket into staging slots
+// 0..P-1 (slot q = rank q's input; RCCL's ncclAllGather, one collective call instead of 2(P-1)
+// p2p ops in a group), then folds the P inputs in rank order (`in` for me) exactly as the
+// one-shot schedule does — same sum, bit for bit, on every rank. The blocks of an allgather are
+// contiguous, so the slot stride is the bucket itself when that keeps the slots 16-byte aligned
+// (the fold's vector loads); otherwise the input is first copied into the padded slot P and the
+// gather moves padded blocks. Tick 1 only waits for the fold (the caller's join covers it).
+void build_gatherfold(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
+                      size_t es, int order) {
+    const size_t stride = prog.staging_stride;
+    auto slot = [&](int q) { return stb + (size_t)q * stride * es; };
+    Tick t;
+    t.reduce.count = 0;
+    const void *src = inb;
+    if (stride != n) {  // padded blocks: gather from a padded copy of the input
+        t.copies.push_back(CopyOp{inb, slot(P), n * es});
+        src = slot(P);
+    }
+    t.gather = GatherOp{src, stb, stride * es};
+    t.has_reduce = true;
+    t.multi = true;
+    std::vector<const void *> xs;
+    for (int q = 0; q < P; ++q) xs.push_back(q == rank ? static_cast<const void *>(inb) : slot(q));
+    plan_fold(t.folds, xs, outb, n, order, [&](int j) { return static_cast<void *>(slot(P + 1 + j)); });
+    prog.ticks.push_back(std::move(t));
+    Tick join;
+    join.reduce.count = 0;
+    join.wait_reduce = 0;
+    prog.ticks.push_back(std::move(join));
+}
+
 }  // namespace
 
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
@@ -353,8 +418,7 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     prog.algo = cfg.algo;
     prog.ticks.clear();
     ring_shape(n, es, P, cfg, &prog.R, &prog.K, &prog.staging_stride);
-    prog.staging_slots =
-        cfg.algo != kAlgoRing ? (size_t)(P > 1 ? P - 1 + fold_temp_slots(P) : 0) : 2 * (size_t)prog.R;
+    prog.staging_slots = program_staging_slots(P, cfg.algo, prog.R);
     if (P <= 1 || n == 0) return;
     // fold order of the direct / one-shot N-input reduce (kFoldLeft: ring 0's order)
     // (fp16 / bf16, which the reference rejects, always fold left in fp32)
@@ -363,6 +427,11 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     if (cfg.algo == kAlgoOneShot) {
         build_oneshot(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
                       static_cast<char *>(staging), n, es, order);
+        return;
+    }
+    if (cfg.algo == kAlgoGatherFold) {
+        build_gatherfold(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
+                         static_cast<char *>(staging), n, es, order);
         return;
     }
     if (cfg.algo == kAlgoDirect) {

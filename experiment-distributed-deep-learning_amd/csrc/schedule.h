@@ -51,9 +51,18 @@ struct CopyOp {  // device-to-device copy posted on the comm stream before the t
     size_t bytes;
 };
 
+// A collective allgather posted on the comm stream after the tick's copies: every rank's
+// `bytes` at `send` land at recv + q * bytes on every rank q (ncclAllGather over RCCL).
+struct GatherOp {
+    const void *send = nullptr;
+    void *recv = nullptr;
+    size_t bytes = 0;
+};
+
 struct Tick {
     std::vector<CopyOp> copies;
     std::vector<P2POp> ops;
+    GatherOp gather;       // valid when gather.bytes > 0
     SegTable reduce;       // valid when has_reduce && !multi
     // valid when has_reduce && multi (direct / one-shot): N-input fold steps run in order; one
     // step up to 16 ranks, a chain or tree of steps through temp slots beyond (plan_fold)
@@ -68,6 +77,9 @@ enum Algo : int {
     kAlgoDirect = 1,  // every rank exchanges with every peer at once (fully connected mesh)
     kAlgoOneShot = 2, // small buckets: every rank sends its whole bucket to every peer in one
                       // group and folds all P inputs in rank order (one group instead of 2)
+    kAlgoGatherFold = 3, // small buckets: one ncclAllGather of the bucket (RCCL's low-latency
+                         // collective path instead of 2(P-1) grouped p2p ops), then the same
+                         // rank-order fold as one-shot
 };
 
 // Largest bucket the autotuner tries the one-shot schedule on.
@@ -105,7 +117,14 @@ inline RingConfig effective_config(RingConfig c, int P) {
 // fold_temp_slots(K) of them).
 void plan_fold(std::vector<SegTableN> &steps, const std::vector<const void *> &xs, void *out, size_t n, int order,
                const std::function<void *(int)> &temp);
-inline int fold_temp_slots(int K) { return K > kMaxInputs + 1 ? K : 0; }
+// Partial sums plan_fold(K inputs) needs in `order` (a dry run of its steps), and the most any
+// order needs (what staging reserves: the order also depends on dtype and message size).
+int fold_temp_count(int K, int order);
+inline int fold_temp_slots(int K) {
+    int m = 0;
+    for (int o : {kFoldLeft, kFoldMpichTree, kFoldBinomial}) m = fold_temp_count(K, o) > m ? fold_temp_count(K, o) : m;
+    return m;
+}
 
 // Per-rank tick list of one allreduce. `staging` must hold staging_elems(R, stride) elements:
 // two slots per ring (reduce-scatter step parity), ring j / parity q at (2j + q) * stride.
@@ -114,15 +133,20 @@ struct RingProgram {
     int P = 1, R = 1, K = 1, rank = 0, algo = kAlgoRing;
     size_t n = 0, esize = 0;
     size_t staging_stride = 0;  // elements per staging slot
-    size_t staging_slots = 0;   // ring: 2 per ring (step parity); direct / one-shot: P-1 (one per peer)
+    size_t staging_slots = 0;   // ring: 2 per ring (step parity); direct / one-shot: P-1 (one per peer);
+                                // gather-fold: P (one per rank) + 1 (padded copy of the input)
     std::vector<Tick> ticks;
 };
 
 // Number of rings and slices the schedule uses for this problem (direct: R = 1, K slices).
 void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg, int *R, int *K,
                 size_t *staging_stride);
-// Staging elements the program needs.
+// Staging elements the program needs, and its staging slots.
 size_t program_staging_elems(size_t n, size_t esize, int P, const RingConfig &cfg);
+size_t program_staging_slots(int P, int algo, int R);
+// Gather-fold slot stride (elements): the bucket itself when its byte size keeps every slot
+// 16-byte aligned, else the bucket rounded up to 64 elements (the input is copied in first).
+inline size_t gather_stride(size_t n, size_t esize) { return (n * esize) % 16 == 0 ? n : (n + 63) & ~size_t(63); }
 
 // Builds rank `rank`'s program. in/out are that rank's buffers, staging its scratch.
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,

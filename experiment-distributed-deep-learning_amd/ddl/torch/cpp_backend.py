@@ -135,6 +135,7 @@ class CPPBackend:
         sig('ddl_rccl_loopback_broadcast', ci, ci, ci, ctypes.POINTER(vp), sz, ci, vp)
         sig('ddl_rccl_loopback_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
             ctypes.POINTER(sz), ci, vp)
+        sig('ddl_rccl_loopback_allgather', ci, vp, vp, sz, vp)
         sig('ddl_rccl_loopback_max', ci, fp, ci, vp)
         sig('ddl_rccl_loopback_tune', ci, ci, sz, ci, vp, ctypes.POINTER(ci), ctypes.POINTER(ci), lp, fp, ci)
         sig('ddl_rccl_loopback_stats', ci, ci, lp)

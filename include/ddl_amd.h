@@ -145,7 +145,8 @@ int ddl_control_channel_close(long long channel);
 int ddl_finalize(void);
 int ddl_is_initialized(void);
 
-/* Tunables: "algo" (0 multi-ring, 1 direct all-to-all), "slice_bytes", "rings", "max_slices",
+/* Tunables: "algo" (0 multi-ring, 1 direct all-to-all, 2 one-shot, 3 gather-fold: one
+ * ncclAllGather then the rank-order fold), "slice_bytes", "rings", "max_slices",
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
  * "host_copy_threads" (memcpy workers of the keyed host staging),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
@@ -325,6 +326,9 @@ int ddl_rccl_loopback_broadcast(int nranks, int root, void *const *bufs, size_t 
                                 void *hip_stream);
 int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
                                  const size_t *displs, int dtype, void *hip_stream);
+/* RcclTransport::allgather (ncclAllGather, the gather-fold schedule's transport) on the one-rank
+ * loopback communicator: recv[0..bytes) = send. */
+int ddl_rccl_loopback_allgather(const void *send, void *recv, size_t bytes, void *hip_stream);
 int ddl_rccl_loopback_max(float *values, int count, void *hip_stream);
 int ddl_rccl_loopback_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
                            long long *configs, float *ms, int max_candidates);

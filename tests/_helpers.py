@@ -249,13 +249,21 @@ def simulate_moves(progs, bufs):
     return bufs
 
 
-def staging_size(progs):
-    """Elements of staging a set of program dumps touches (recv targets, fold inputs/outputs)."""
+def staging_size(progs, P=None):
+    """Elements of staging a set of program dumps touches (recv targets, fold inputs/outputs);
+    P = the number of ranks (default: one program per rank)."""
+    P = len(progs) if P is None else P
     st_size = 1
     for p in progs:
         for row in p:
             if row[1] in (0, 1) and row[4] == 2:
                 st_size = max(st_size, int(row[5] + row[6]))
+            elif row[1] == 4 and row[4] == 2:  # copy into staging
+                st_size = max(st_size, int(row[5] + row[6]))
+            elif row[1] == 11:  # gather: P blocks of row[6] elements into staging at row[5]
+                st_size = max(st_size, int(row[5] + P * row[6]))
+                if row[2] == 2:  # sent from a (padded) staging slot
+                    st_size = max(st_size, int(row[3] + row[6]))
             elif row[1] in (2, 3):
                 st_size = max(st_size, int(row[7] + row[6]))
             elif row[1] in GENERAL_FOLDS:
@@ -276,6 +284,7 @@ def simulate_ring(oracle, lib, dt, xs):
     bufs = [[x.copy(), np.zeros_like(x), np.zeros(st_size, dtype=x.dtype)] for x in xs]
     T = int(max(p[:, 0].max() for p in progs)) + 1 if P > 1 and n else 0
     for t in range(T):
+        run_copies_and_gathers(progs, bufs, t)
         sends = {}
         for r in range(P):
             for row in progs[r][progs[r][:, 0] == t]:
@@ -300,6 +309,29 @@ def simulate_ring(oracle, lib, dt, xs):
                                                             bufs[r][2][soff:soff + cnt])
             apply_folds(oracle, dt, rows, bufs[r])
     return [b[1] for b in bufs]
+
+
+def run_copies_and_gathers(progs, bufs, t):
+    """A tick's device copies (kind 4: buffer 0 -> dst buffer) and its allgather (kind 11: rank
+    q's block at (send buffer, offset) lands at recv offset + q * count on every rank), on host
+    buffers bufs[r] = [in, out, staging], in the order the executor posts them."""
+    P = len(progs)
+    for r in range(P):
+        for row in progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 4)]:
+            _, _, _, _, b, off, cnt, soff = row
+            bufs[r][b][off:off + cnt] = bufs[r][0][soff:soff + cnt]
+    blocks = []
+    for r in range(P):
+        rows = progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 11)]
+        if len(rows):
+            _, _, sb, so, _, _, cnt, _ = rows[0]
+            blocks.append(bufs[r][sb][so:so + cnt].copy())
+    if blocks:
+        assert len(blocks) == P, f'allgather at tick {t} not on every rank'
+        for r in range(P):
+            _, _, _, _, rb, ro, cnt, _ = progs[r][(progs[r][:, 0] == t) & (progs[r][:, 1] == 11)][0]
+            for q in range(P):
+                bufs[r][rb][ro + q * cnt:ro + (q + 1) * cnt] = blocks[q]
 
 
 # General N-input fold rows of a program dump: kind -> (oracle total_bytes argument, output

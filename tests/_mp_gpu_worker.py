@@ -50,7 +50,7 @@ def check_schedules_vs_oracle(ctx):
     import _helpers as h
     torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
     s = torch.cuda.current_stream().cuda_stream
-    cases = [(algo, ref) for ref in (1, 0) for algo in (0, 1, 2)]
+    cases = [(algo, ref) for ref in (1, 0) for algo in (0, 1, 2, 3)]
     with h.config(lib, tune=0, slice_bytes=64 << 10):
         for algo, ref in cases:
             with h.config(lib, algo=algo, reference_order=ref):
@@ -64,7 +64,7 @@ def check_schedules_vs_oracle(ctx):
                             want = ora.allreduce_ring(dt, xs, h.ring_perms(lib, P, R))
                         elif algo == 1:
                             want = ora.allreduce_direct(dt, xs)
-                        else:
+                        else:  # one-shot / gather-fold: left fold in rank order
                             want = ora.fold(dt, xs)
                         for in_place in (False, True):
                             a = _dev(torch, xs[r], 'cuda')

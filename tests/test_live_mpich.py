@@ -35,7 +35,7 @@ def test_oracle_reference_order_vs_live_mpich(oracle, P, dt, n):
 
 @pytest.mark.gpu
 @needs_mpich
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 def test_engine_reference_order_vs_live_mpich(lib, gpu, algo):
     import torch
     s = torch.cuda.current_stream().cuda_stream

@@ -50,11 +50,21 @@ def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
         xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
         prog = h.ring_program(lib, rank, world, n, dt)
         R, _ = h.ring_shape(lib, n, dt, world)
-        st = h.staging_size([prog])
+        st = h.staging_size([prog], world)
         bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
         view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
         for t in sorted(set(prog[:, 0].tolist())):
             rows = prog[prog[:, 0] == t]
+            for row in rows[rows[:, 1] == 4]:  # device copies (buffer 0 -> dst)
+                _, _, _, _, b, off, cnt, soff = row
+                bufs[b][off:off + cnt] = bufs[0][soff:soff + cnt]
+            for row in rows[rows[:, 1] == 11]:  # allgather (gather-fold): every rank's block
+                _, _, sb, so, rb, ro, cnt, _ = row
+                parts = [torch.empty(int(cnt), dtype=view(bufs[sb][:1]).dtype) for _ in range(world)]
+                dist.all_gather(parts, view(bufs[sb][so:so + cnt].copy()))
+                for qq, part in enumerate(parts):
+                    dst = bufs[rb][ro + qq * cnt:ro + (qq + 1) * cnt]
+                    dst[:] = part.numpy().view(dst.dtype)
             reqs = []
             for row in rows[rows[:, 1] == 1]:  # recvs first, then sends: no deadlock in gloo
                 _, _, peer, ring, b, off, cnt, _ = row
@@ -71,7 +81,7 @@ def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
         if ref_order and (algo != 0 or world > 2):  # MPICH's own order (a P = 2 ring is exact)
             want = ora.fold_ref_order(dt, xs)
         else:
-            want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo == 2 else
+            want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo in (2, 3) else
                     ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
         ok = bufs[1].tobytes() == want.tobytes()
         dist.destroy_process_group()
@@ -80,7 +90,7 @@ def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
         q.put((rank, False, repr(e)))
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('dt,n', [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)])
 def test_ring_program_over_gloo(world, dt, n, algo):
@@ -88,7 +98,7 @@ def test_ring_program_over_gloo(world, dt, n, algo):
     _run_ring_workers(world, dt, n, algo, 0)
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 @pytest.mark.parametrize('world', [2, 3])
 @pytest.mark.parametrize('dt,n', [(1, 50_000), (1, 300), (2, 4099)])
 def test_reference_order_program_over_gloo(world, dt, n, algo):

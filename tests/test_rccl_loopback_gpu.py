@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import (DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, NP, config, random_input, ring_perms,
+from _helpers import (DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, config, random_input, ring_perms,
                       ring_shape)
 
 pytestmark = pytest.mark.gpu
@@ -53,7 +53,7 @@ def _pairs(lib, P):
 
 @pytest.mark.parametrize('P', [3, 5, 8])
 @pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32], ids=lambda d: NAME[d])
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 def test_rccl_loopback_reference_order(loop, oracle, gpu, P, dt, algo):
     """Default reference order over the RCCL transport: every rank equals MPICH's order bit for
     bit, for messages up to 2048 bytes (binomial tree) and above (pre-fold + pairwise tree)."""
@@ -124,6 +124,18 @@ def test_rccl_loopback_broadcast_allgatherv(loop, oracle, gpu, P):
     torch.cuda.synchronize()
     for r in rs:
         assert r.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_rccl_loopback_ncclallgather_call(loop, gpu):
+    """RcclTransport::allgather — the gather-fold schedule's ncclAllGather — at one rank: the
+    block lands at offset 0 of recv, nothing beyond it is touched."""
+    lib = loop
+    x = torch.arange(1001, dtype=torch.int32, device=gpu)
+    y = torch.full((1100,), -7, dtype=torch.int32, device=gpu)
+    assert lib.ddl_rccl_loopback_allgather(x.data_ptr(), y.data_ptr(), 1001 * 4,
+                                           torch.cuda.current_stream().cuda_stream) == 0, lib.ddl_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(y[:1001], x) and bool((y[1001:] == -7).all())
 
 
 def test_rccl_loopback_tuner_agreement(loop, gpu):

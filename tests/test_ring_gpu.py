@@ -105,7 +105,7 @@ def test_local_ring_vs_mpich_golden(lib, gpu):
                 assert np.all(np.abs(o.astype(np.float64) - y.astype(np.float64)) <= bound), case
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 def test_reference_order_equals_mpich_golden_bit_for_bit(lib, gpu, algo):
     """The product default (reference_order 1): every golden case — MPICH 3.3.2's own
     MPI_Allreduce outputs at P = 2..8, fp32 / fp64 / integers, both sides of its 2048-byte
@@ -118,7 +118,7 @@ def test_reference_order_equals_mpich_golden_bit_for_bit(lib, gpu, algo):
                 assert o.tobytes() == y.tobytes(), case
 
 
-@pytest.mark.parametrize('algo', [1, 2])
+@pytest.mark.parametrize('algo', [1, 2, 3])
 @pytest.mark.parametrize('P', [3, 5, 6, 7, 8])
 @pytest.mark.parametrize('dt', [1, 2, 3], ids=lambda d: NAME[d])
 @pytest.mark.parametrize('n', [1, 300, 512, 513, 65_537, 1_000_003])
@@ -153,8 +153,8 @@ def test_reference_order_misaligned_fold(lib, oracle, gpu):
 
 @pytest.mark.parametrize('P', [4, 8])
 def test_reference_order_tuner_times_only_exact_schedules(lib, gpu, P):
-    """With reference_order the autotuner's candidates are direct / one-shot schedules only at
-    P > 2 (the configured ring becomes direct), deduplicated."""
+    """With reference_order the autotuner's candidates are direct / one-shot / gather-fold
+    schedules only at P > 2 (the configured ring becomes direct), deduplicated."""
     chosen, count = ctypes.c_int(), ctypes.c_int()
     cfgs = (ctypes.c_longlong * 64)()
     ms = (ctypes.c_float * 16)()
@@ -163,7 +163,7 @@ def test_reference_order_tuner_times_only_exact_schedules(lib, gpu, P):
                                 ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
     assert st == 0, lib.ddl_last_error()
     c = [tuple(cfgs[4 * i:4 * i + 4]) for i in range(count.value)]
-    assert {x[0] for x in c} == {1, 2} and len(set(c)) == len(c)
+    assert {x[0] for x in c} == {1, 2, 3} and len(set(c)) == len(c)
     assert c[0][0] == 1
 
 

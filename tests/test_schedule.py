@@ -285,7 +285,7 @@ def test_oneshot_program_shape(lib):
 
 
 # ---- reference order (reference_order = 1, the default) ----------------------------------------
-@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize('n', [1, 100, 512, 513, 4099, 50_000])
 @pytest.mark.parametrize('dt', ALL_DTYPES)
@@ -322,7 +322,7 @@ def test_reference_order_program_kinds(lib):
         assert set(prog[prog[:, 1] >= 3][:, 1]) == {7}
 
 
-@pytest.mark.parametrize('algo,ref_order', [(0, 1), (1, 1), (2, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize('algo,ref_order', [(0, 1), (1, 1), (2, 1), (3, 1), (1, 0), (2, 0), (3, 0)])
 @pytest.mark.parametrize('P', [17, 20, 31, 32, 33])
 @pytest.mark.parametrize('n', [1, 300, 513, 5000])
 @pytest.mark.parametrize('dt', [1, 2, 3, 19])
