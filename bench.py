@@ -761,21 +761,22 @@ def link_ceiling(P, S=None):
 
 def mpich_order_sum(xs, message_bytes):
     """MPI_Allreduce(MPI_SUM)'s per-element order in MPICH 3.3.2 (numpy, one rounding per add in
-    the element type): a binomial tree over ranks up to 2048 bytes, else the first 2*rem ranks
-    folded in pairs and a pairwise tree over the pof2 leaves. A check of the N>1 run only; the
-    tests pin the same order against MPICH itself (tests/test_live_mpich.py)."""
+    the element type): a binomial tree over ranks up to 2048 bytes (or when the element count is
+    below pof2), else the first 2*rem ranks folded in pairs and a pairwise tree over the pof2
+    leaves. A check of the N>1 run only; the tests pin the same order against MPICH itself
+    (tests/test_live_mpich.py)."""
     v = [x.copy() for x in xs]
     k = len(v)
-    if message_bytes <= 2048:
+    pof2 = 1
+    while pof2 * 2 <= k:
+        pof2 *= 2
+    if message_bytes <= 2048 or message_bytes // xs[0].itemsize < pof2:
         m = 1
         while m < k:
             for t in range(0, k - m, 2 * m):
                 v[t] = v[t] + v[t + m]
             m *= 2
         return v[0]
-    pof2 = 1
-    while pof2 * 2 <= k:
-        pof2 *= 2
     rem = k - pof2
     leaf = [v[2 * t] + v[2 * t + 1] for t in range(rem)] + v[2 * rem:]
     m = 1

@@ -107,9 +107,16 @@ enum FoldOrder : int {
                         // 2*rem inputs folded in pairs, then a pairwise tree over pof2 leaves
     kFoldBinomial = 2,  // MPICH 3.3.2 MPI_Allreduce up to 2048 bytes: binomial tree over ranks
 };
-// MPICH's order for an allreduce of `message_bytes` (MPIR_CVAR_ALLREDUCE_SHORT_MSG_SIZE = 2048).
-inline int mpich_fold_order(size_t message_bytes) {
-    return message_bytes <= 2048 ? kFoldBinomial : kFoldMpichTree;
+// MPICH's order for an allreduce of `message_bytes` of `esize`-byte elements over P ranks
+// (MPICH 3.3.2 MPIR_Allreduce_intra_auto): recursive doubling — the binomial order — when the
+// message is at most MPIR_CVAR_ALLREDUCE_SHORT_MSG_SIZE = 2048 bytes or its element count is
+// below pof2 (largest power of two <= P; above 2048 bytes that takes P >= 512), else
+// reduce-scatter + allgather (pre-fold + pairwise tree). Pinned by live MPICH runs up to P = 520
+// on one host (tests/golden, tests/test_live_mpich.py).
+inline int mpich_fold_order(size_t message_bytes, size_t esize, int P) {
+    size_t pof2 = 1;
+    while (pof2 * 2 <= (size_t)P) pof2 *= 2;
+    return message_bytes <= 2048 || message_bytes / esize < pof2 ? kFoldBinomial : kFoldMpichTree;
 }
 struct SegTableN {
     const void *a;

@@ -423,7 +423,8 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     // fold order of the direct / one-shot N-input reduce (kFoldLeft: ring 0's order)
     // (fp16 / bf16, which the reference rejects, always fold left in fp32)
     const bool half = dtype == DDL_HALF || dtype == DDL_BFLOAT16;
-    const int order = cfg.ref_order && !half ? mpich_fold_order(cfg.order_bytes ? cfg.order_bytes : n * es) : kFoldLeft;
+    const int order =
+        cfg.ref_order && !half ? mpich_fold_order(cfg.order_bytes ? cfg.order_bytes : n * es, es, P) : kFoldLeft;
     if (cfg.algo == kAlgoOneShot) {
         build_oneshot(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
                       static_cast<char *>(staging), n, es, order);

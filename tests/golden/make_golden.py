@@ -17,7 +17,7 @@ Cases:
   fp32_exact_P8           k * 2^-10 with |k| < 2^12: exactly summable, bit-exact at P=8.
   fp64_randn_P{2,4}, int64_rand_P4, uint64_rand_P2.
 
-usage: python tests/golden/make_golden.py
+usage: python tests/golden/make_golden.py [--bigp]   (--bigp: only golden_mpich_bigp.npz)
 """
 import json
 import os
@@ -116,8 +116,40 @@ CASES = [
 ]
 
 
+# More ranks than one node's GPUs, one host: MPICH's orders beyond P = 8, the
+# fold trees of more than 16 inputs, and MPICH's count < pof2 rule (recursive doubling above
+# 2048 bytes when the element count is below the largest power of two <= P: P = 520, 257 fp64
+# elements = 2056 bytes). Kept in their own file: the GPU runs P <= 64 virtual ranks.
+BIGP_CASES = [
+    ("fp32_randn_P17", "randn", "float32", 17, 3000),
+    ("fp32_randn_P20_small", "randn", "float32", 20, 511),
+    ("fp32_randn_P33", "randn", "float32", 33, 4099),
+    ("fp64_randn_P33_small", "randn", "float64", 33, 255),
+    ("int32_rand_P33", "randint", "int32", 33, 1031),
+    ("fp64_randn_P520_count_lt_pof2", "randn", "float64", 520, 257),
+]
+
+
+def make_bigp():
+    arrays, cases = {}, {}
+    for name, kind, dtype, P, n in BIGP_CASES:
+        x = make_inputs(kind, dtype, P, n)
+        y = run_mpich(x, dtype)
+        arrays[name + "__inputs"] = x
+        arrays[name + "__output"] = y
+        cases[name] = {"kind": kind, "dtype": dtype, "P": P, "n": n}
+        print(f"{name}: P={P} n={n} {dtype} out[0]={y[0]}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "golden_mpich_bigp.npz"), **arrays)
+    with open(os.path.join(HERE, "golden_manifest_bigp.json"), "w") as f:
+        json.dump({"generator": "MPICH 3.3.2 MPI_Allreduce(MPI_SUM) via oracle/mpi_allreduce_driver.c, one host",
+                   "seed": "numpy default_rng(1234 + 7919*rank)", "cases": cases}, f, indent=1, sort_keys=True)
+
+
 def main():
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "mpi"], check=True)
+    make_bigp()
+    if "--bigp" in sys.argv:
+        return 0
     arrays, manifest = {}, {"generator": "MPICH 3.3.2 MPI_Allreduce(MPI_SUM) via oracle/mpi_allreduce_driver.c",
                             "reference_call": "src/cpp/communicate/backend/mpi/MPICommunicator.cc:14-28",
                             "seed": "numpy default_rng(1234 + 7919*rank)", "cases": {}}

@@ -19,7 +19,9 @@ needs_mpich = pytest.mark.skipif(not live_mpich_available(), reason='MPICH / ora
 # (P, dtype, n): 2048-byte switch at n = 512 fp32 / 256 fp64; large messages up to 4 MiB
 CASES = [(3, DT_FLOAT, 700), (5, DT_FLOAT, 511), (5, DT_FLOAT, 512), (5, DT_FLOAT, 513), (5, DT_DOUBLE, 255),
          (5, DT_DOUBLE, 257), (6, DT_FLOAT, 3001), (7, DT_FLOAT, 100), (7, DT_DOUBLE, 9999), (5, DT_FLOAT, 1 << 20),
-         (7, DT_FLOAT, 300_007), (8, DT_FLOAT, 65_537), (5, DT_INT32, 4099), (2, DT_FLOAT, 12_345)]
+         (7, DT_FLOAT, 300_007), (8, DT_FLOAT, 65_537), (5, DT_INT32, 4099), (2, DT_FLOAT, 12_345),
+         # beyond one node's GPUs, one host (fold trees of more than 16 inputs)
+         (17, DT_FLOAT, 3000), (20, DT_FLOAT, 511), (33, DT_FLOAT, 4099), (33, DT_DOUBLE, 255)]
 
 
 def _inputs(P, dt, n):

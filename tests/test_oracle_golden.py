@@ -171,3 +171,36 @@ def test_bench_parity_check_matches_mpich_golden(oracle):
         xs, y = GOLD[case + '__inputs'], GOLD[case + '__output']
         got = bench.mpich_order_sum(list(xs), xs[0].nbytes)
         assert got.tobytes() == y.tobytes(), case
+
+
+# ---- beyond one node's GPUs: P = 17 .. 520 on one host (tests/golden/make_golden.py --bigp) ----
+GOLD_BIGP = np.load(os.path.join(HERE, 'golden', 'golden_mpich_bigp.npz'), allow_pickle=False)
+MANIFEST_BIGP = json.load(open(os.path.join(HERE, 'golden', 'golden_manifest_bigp.json')))
+
+
+@pytest.mark.parametrize('case', sorted(MANIFEST_BIGP['cases']))
+def test_reference_order_bit_exact_with_mpich_beyond_8_ranks(oracle, case):
+    """MPICH's order at P = 17, 20, 33 (non-power-of-two, both sides of 2048 bytes) and P = 520
+    (count < pof2: recursive doubling above 2048 bytes) equals the oracle bit for bit."""
+    meta = MANIFEST_BIGP['cases'][case]
+    xs, y = GOLD_BIGP[case + '__inputs'], GOLD_BIGP[case + '__output']
+    got = oracle.fold_ref_order(FROM_NP[meta['dtype']], list(xs))
+    assert got.tobytes() == y.tobytes(), case
+
+
+def test_count_below_pof2_rule_is_what_distinguishes_p520(oracle):
+    """At P = 520 a 257-element fp64 message (2056 B) is above MPICH's 2048-byte switch, but its
+    element count is below pof2 = 512, so MPICH reduces by recursive doubling: the size-only
+    rule (pre-fold + pairwise tree) would differ from MPICH's output."""
+    xs = list(GOLD_BIGP['fp64_randn_P520_count_lt_pof2__inputs'])
+    y = GOLD_BIGP['fp64_randn_P520_count_lt_pof2__output']
+    assert oracle.fold_ref_order(2, xs).tobytes() == y.tobytes()
+    pof2 = 512
+    rem = len(xs) - pof2
+    leaf = [xs[2 * t] + xs[2 * t + 1] for t in range(rem)] + xs[2 * rem:]
+    m = 1
+    while m < pof2:
+        for t in range(0, pof2, 2 * m):
+            leaf[t] = leaf[t] + leaf[t + m]
+        m *= 2
+    assert leaf[0].tobytes() != y.tobytes()

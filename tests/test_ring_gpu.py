@@ -408,3 +408,18 @@ def test_fold_trees_beyond_sixteen_ranks_on_gpu(lib, oracle, gpu, P, algo, ref, 
             want = oracle.allreduce_direct(dt, xs) if algo == 1 else oracle.fold(dt, xs)
         for r in range(P):
             assert outs[r].tobytes() == want.tobytes(), (n, r)
+
+
+def test_reference_order_mpich_golden_beyond_8_ranks(lib, gpu):
+    """MPICH's own outputs at P = 17, 20, 33 (one host, tests/golden/golden_mpich_bigp.npz) from
+    the GPU's virtual ranks bit for bit: fold trees of more than 16 inputs through staging
+    partials, every schedule."""
+    gold = np.load(os.path.join(HERE, 'golden', 'golden_mpich_bigp.npz'), allow_pickle=False)
+    meta = json.load(open(os.path.join(HERE, 'golden', 'golden_manifest_bigp.json')))['cases']
+    for algo in (0, 1, 2, 3):
+        with config(lib, algo=algo, reference_order=1, slice_bytes=64 << 10):
+            for case, m in sorted(meta.items()):
+                if m['P'] > 64:
+                    continue
+                for o in run_local(lib, gpu, list(gold[case + '__inputs'])):
+                    assert o.tobytes() == gold[case + '__output'].tobytes(), (algo, case)

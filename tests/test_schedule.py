@@ -398,3 +398,27 @@ def test_random_schedules_property(lib, oracle):
             want = oracle.fold(dt, xs)
         for r in range(P):
             assert outs[r].tobytes() == want.tobytes(), (trial, P, n, dt, kv, r)
+
+
+def _bigp_golden():
+    import json
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    gold = np.load(os.path.join(here, 'golden', 'golden_mpich_bigp.npz'), allow_pickle=False)
+    meta = json.load(open(os.path.join(here, 'golden', 'golden_manifest_bigp.json')))['cases']
+    return [(c, m, gold[c + '__inputs'], gold[c + '__output']) for c, m in sorted(meta.items())]
+
+
+@pytest.mark.parametrize('case,meta,xs,y', _bigp_golden(), ids=[c for c, *_ in _bigp_golden()])
+def test_programs_equal_mpich_beyond_8_ranks(lib, oracle, case, meta, xs, y):
+    """The engine's own programs at P = 17 .. 520 (one host's MPICH outputs, tests/golden):
+    executed with matched sends/recvs, every rank equals MPI_Allreduce bit for bit — the direct
+    schedule at every P (fold trees of up to 520 inputs in <= 16-input steps; MPICH's
+    count < pof2 rule at P = 520), one-shot and gather-fold up to 33 ranks."""
+    from _helpers import FROM_NP
+    dt = FROM_NP[meta['dtype']]
+    for algo in ((1, 2, 3) if meta['P'] <= 33 else (1,)):
+        with config(lib, algo=algo, reference_order=1):
+            outs = simulate_ring(oracle, lib, dt, list(xs))
+        for r, o in enumerate(outs):
+            assert o.tobytes() == y.tobytes(), (algo, r)
