@@ -155,7 +155,12 @@ std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
 
 extern "C" {
 
-int ddl_version(void) { return 1; }
+int ddl_version(void) { return 2; }
+
+#ifndef DDL_SRC_HASH
+#define DDL_SRC_HASH "unknown"
+#endif
+const char *ddl_build_info(void) { return "src=" DDL_SRC_HASH " arch=gfx950"; }
 const char *ddl_last_error(void) { return last_error(); }
 const char *ddl_dtype_name(int dtype) { return dtype_name(dtype); }
 size_t ddl_dtype_size(int dtype) { return dtype_size(dtype); }

@@ -86,6 +86,9 @@ typedef void *(*ddl_alloc_fn)(size_t first_dim, size_t bytes, void *user);
 
 /* ---- library / lifecycle ------------------------------------------------------- */
 int ddl_version(void);
+/* "src=<sha1 of the engine sources, 16 hex> arch=gfx950": which sources this library was built
+ * from (tests rebuild a stale library rather than test it). */
+const char *ddl_build_info(void);
 const char *ddl_last_error(void);
 const char *ddl_dtype_name(int dtype);
 size_t ddl_dtype_size(int dtype); /* 0 for unsupported */

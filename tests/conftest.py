@@ -17,16 +17,43 @@ def pytest_configure(config):
     config.addinivalue_line('markers', 'slow: longer CPU test')
 
 
-def _build_if_missing():
+def source_hash():
+    """sha1 (16 hex) of the engine sources as the Makefile computes it for ddl_build_info()."""
+    import glob
+    import hashlib
+    csrc = os.path.join(PKG, 'csrc')
+    names = sorted(os.path.basename(f) for pat in ('*.h', '*.cpp', '*.hip') for f in glob.glob(os.path.join(csrc, pat)))
+    h = hashlib.sha1()
+    for f in [os.path.join(csrc, n) for n in names] + [os.path.join(ROOT, 'include', 'ddl_amd.h')]:
+        with open(f, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _library_build_id(path):
+    """The source hash baked into the library, read from the file (loading it here, before torch,
+    would bind the engine to a second HIP runtime)."""
+    import re
+    try:
+        with open(path, 'rb') as fh:
+            m = re.search(rb'src=([0-9a-f]{16}) arch=gfx950', fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def _build_if_stale():
+    """The library under test must be built from these sources: built when missing, rebuilt when
+    its baked-in source hash differs (a stale prebuilt .so is never tested)."""
     lib = os.path.join(PKG, 'lib', 'libddl_amd.so')
     ora = os.path.join(ROOT, 'oracle', 'build', 'libddl_oracle.so')
-    if not os.path.exists(lib):
-        subprocess.run(['make', '-C', os.path.join(PKG, 'csrc'), '-j8'], check=True)
+    if not os.path.exists(lib) or _library_build_id(lib) != source_hash():
+        subprocess.run(['make', '-C', os.path.join(PKG, 'csrc'), '-j8', '-B'], check=True)
     if not os.path.exists(ora):
         subprocess.run(['make', '-C', os.path.join(ROOT, 'oracle')], check=True)
 
 
-_build_if_missing()
+_build_if_stale()
 
 
 @pytest.fixture(scope='session')

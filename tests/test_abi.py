@@ -85,3 +85,12 @@ def test_python_config_module(lib):
     assert config.snapshot() == snap
     with pytest.raises(DDLError):
         config.set('no_such_key', 1)
+
+
+def test_library_is_built_from_these_sources(lib):
+    """ddl_build_info() carries the sha1 of the engine sources the library was compiled from;
+    it must be this tree's (conftest rebuilds a stale library before any test runs)."""
+    import conftest
+    lib.ddl_build_info.restype = ctypes.c_char_p
+    info = lib.ddl_build_info().decode()
+    assert info == f'src={conftest.source_hash()} arch=gfx950', info

@@ -226,6 +226,25 @@ def test_plans_match_reference_plan_walk(lib, oracle):
         assert got == ref, (el, esz, limit)
 
 
+def test_make_plans_even_cap_deliberate_divergence(lib, oracle):
+    """An even cap can end a multi-request plan exactly on a request boundary. The reference then
+    advances `requestPlannedBegin += 1` (MPIRingTokenCommunication.cc:534-536), so the next plan
+    starts AGAIN at the request just finished — it is packed and reduced twice (in place, the
+    second pass would add the already-reduced values). The engine continues after it
+    (pe + 1). Hand-checked: 3 x fp32[4] (16 B each), cap 32 B."""
+    import ctypes
+    el, esz, cap = [4, 4, 4], [4, 4, 4], 32
+    assert oracle.make_plan(el, esz, cap) == [(0, 0, 1, 4), (1, 0, 2, 4)]  # the reference's walk
+    out = (ctypes.c_size_t * 64)()
+    np_ = ctypes.c_size_t()
+    assert lib.ddl_make_plans((ctypes.c_size_t * 3)(*el), (ctypes.c_size_t * 3)(*esz), 3, cap, out, 16,
+                              ctypes.byref(np_)) == 0
+    got = [tuple(out[4 * i:4 * i + 4]) for i in range(np_.value)]
+    assert got == [(0, 0, 1, 4), (2, 0, 2, 4)]  # every request exactly once
+    # with the reference's odd cap (2^31 - 1) and even element sizes the boundary case cannot
+    # occur, and the two walks agree (test_make_plans_matches_oracle)
+
+
 def test_plan_cap_2gib_single_plan_for_large_bucket(oracle):
     """With the reference's cap (2^31-1 bytes) a 256 MiB fp32 bucket is one plan (C3), and a
     C5-like mixed set splits where the reference would."""
