@@ -9,9 +9,11 @@
 // fused bucket keeps the ring's 16-byte vector alignment). The segment table lives in device
 // memory (uploaded with one async copy from a pinned staging table). Default mapping: every
 // segment is cut into 1 KiB tiles that restart at the segment start, one 64-lane workgroup per
-// tile, the tile's segment from a per-tile index built on the device (k_tile_index, k_seg_tiles).
+// tile, the tile's segment from a one-byte-per-tile index built on the device (k_tile_index,
+// k_seg_tiles).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -47,13 +49,18 @@ __device__ inline void copy_bytes(char *dst, const char *src, uint32_t m) {
 // moves bytes [16 l + it * THREADS * 16, ...) of the tile. Small tiles (1 KiB per 64-lane
 // workgroup) keep the chunks in flight a compact window of each stream (tools/copy_tune.hip:
 // 1R+1W copies reach 6.5 TB/s with 1-2 KiB per workgroup vs 5.3 TB/s with 64 KiB).
-// XCD grouping: the dispatcher deals workgroups round-robin over the 8 XCDs, each with its own
-// L2, so with tile = blockIdx every XCD would fetch every 64-byte line of tile_seg (16 tiles)
-// and the descriptor it points at: 8x the index bytes from HBM (+3 % traffic on the C5 set,
-// r01 PMC). Inside each run of 128 workgroups, XCD x takes 16 consecutive tiles — one
-// tile_seg line — so each line is fetched once, and the window stays 128 tiles wide.
+// Tile -> segment map, compact: the dispatcher deals workgroups round-robin over the 8 XCDs,
+// each with its own L2, so every 128-byte line of a per-tile index is fetched by all 8 (r01: an
+// int32 per tile cost +3.2 % HBM traffic on the C5 set). The map is therefore one byte per tile,
+// the segment's distance from a per-128-tile base (kIdxBlock), so a line covers 128 tiles:
+// seg = base[tile / 128] + delta[tile]. When some block spans more than 255 segments (runs of
+// empty segments) the host falls back to an int32 per tile. Remapping tiles to XCDs instead cut
+// the traffic too but slowed the copy 4-5 % (profiles/r02/pack/pack_xcd_ab.txt).
+constexpr uint32_t kIdxBlock = 128;
+
+template <bool NARROW>
 __global__ void __launch_bounds__(256) k_tile_index(const SegDesc *__restrict__ d, int count, uint64_t tiles,
-                                                    int *__restrict__ tile_seg) {
+                                                    const uint32_t *__restrict__ base, void *__restrict__ map) {
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= tiles) return;
     int lo = 0, hi = count;  // last segment with tile0 <= t (segments without tiles share tile0)
@@ -62,19 +69,22 @@ __global__ void __launch_bounds__(256) k_tile_index(const SegDesc *__restrict__ 
         if (d[mid].tile0 <= t) lo = mid;
         else hi = mid;
     }
-    tile_seg[t] = lo;
+    if (NARROW) static_cast<uint8_t *>(map)[t] = (uint8_t)(lo - (int)base[t / kIdxBlock]);
+    else static_cast<int *>(map)[t] = lo;
 }
 
-template <int DIR, int kIters, int THREADS>
+template <int DIR, int kIters, int THREADS, bool NARROW>
 __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc *__restrict__ d,
-                                                       const int *__restrict__ tile_seg, int xcd_group) {
+                                                       const uint32_t *__restrict__ blk_base,
+                                                       const void *__restrict__ map) {
     constexpr uint64_t kTile = (uint64_t)THREADS * 16 * kIters;
-    constexpr unsigned kXcds = 8, kLine = 16, kRun = kXcds * kLine;
-    const unsigned bid = blockIdx.x;
-    const unsigned full = xcd_group ? gridDim.x - gridDim.x % kRun : 0;  // the tail keeps tile = blockIdx
-    const unsigned r = bid % kRun;
-    const unsigned tile = bid < full ? bid - r + (r % kXcds) * kLine + r / kXcds : bid;
-    const SegDesc sd = d[tile_seg[tile]];
+    const unsigned tile = blockIdx.x;
+    // the byte is read as its aligned dword (a scalar load; a byte load would go through the
+    // vector memory path and delay the whole tile)
+    const int seg = NARROW ? (int)(blk_base[tile / kIdxBlock] +
+                                   ((static_cast<const uint32_t *>(map)[tile / 4] >> (8 * (tile % 4))) & 0xffu))
+                           : static_cast<const int *>(map)[tile];
+    const SegDesc sd = d[seg];
     const uint64_t base = (uint64_t)(tile - sd.tile0) * kTile;  // tile start inside the segment
     char *fl = flat + sd.off;
     char *tp = reinterpret_cast<char *>(sd.ptr);
@@ -102,6 +112,25 @@ __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc
             if (DIR == 0) copy_bytes(fl + b, tp + b, m);
             else copy_bytes(tp + b, fl + b, m);
         }
+    }
+}
+
+template <int DIR, bool NARROW>
+void launch_dir(int variant, dim3 g, hipStream_t stream, char *fl, const SegDesc *dd, const uint32_t *db,
+                const void *map) {
+    if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<DIR, 1, 128, NARROW>), g, dim3(128), 0, stream, fl, dd, db, map);
+    else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<DIR, 2, 128, NARROW>), g, dim3(128), 0, stream, fl, dd, db, map);
+    else hipLaunchKernelGGL((k_seg_tiles<DIR, 1, 64, NARROW>), g, dim3(64), 0, stream, fl, dd, db, map);
+}
+
+void launch_tiles(int dir, int variant, bool narrow, dim3 g, hipStream_t stream, char *fl, const SegDesc *dd,
+                  const uint32_t *db, const void *map) {
+    if (dir == 0) {
+        if (narrow) launch_dir<0, true>(variant, g, stream, fl, dd, db, map);
+        else launch_dir<0, false>(variant, g, stream, fl, dd, db, map);
+    } else {
+        if (narrow) launch_dir<1, true>(variant, g, stream, fl, dd, db, map);
+        else launch_dir<1, false>(variant, g, stream, fl, dd, db, map);
     }
 }
 
@@ -153,7 +182,6 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
                         hipStream_t stream) {
     if (count <= 0) return;
     DDL_REQUIRE(flat && segs && bytes, DDL_STATUS_INVALID_ARGUMENT, "null pack arguments");
-    const size_t need = (size_t)count * sizeof(SegDesc);
     Slot &sl = free_slot_();
     // DDL_PACK_VARIANT (measurement only; tools/pack_tune.py, C5 bucket set, pack / unpack, r01):
     //   1: segment tiles of 1 KiB, 64 lanes (default)                                     6.10 / 6.37 TB/s
@@ -166,11 +194,14 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
         const int v = e ? std::atoi(e) : 1;
         return v >= 1 && v <= 3 ? v : 1;
     }();
-    // DDL_PACK_XCD=0 turns the XCD grouping of tiles off (measurement)
-    static const int xcd = [] {
-        const char *e = std::getenv("DDL_PACK_XCD");
-        return e ? (std::atoi(e) != 0) : 1;
-    }();
+    // segment-aligned tiles (variants 1..3): tile bytes per workgroup; tile0 = running tile count
+    const uint64_t seg_tile = variant == 2 ? 2048 : variant == 3 ? 4096 : 1024;
+    uint64_t tiles = 0;
+    for (int i = 0; i < count; ++i) tiles += (bytes[i] + seg_tile - 1) / seg_tile;
+    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
+    const uint64_t nblk = (tiles + kIdxBlock - 1) / kIdxBlock;
+    const size_t table = (size_t)count * sizeof(SegDesc);
+    const size_t need = table + nblk * sizeof(uint32_t);  // descriptors, then the block bases
     if (need > sl.cap) {
         if (sl.host) DDL_HIP(hipHostFree(sl.host));
         if (sl.dev) DDL_HIP(hipFree(sl.dev));
@@ -179,46 +210,52 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
         DDL_HIP(hipHostMalloc(&sl.host, sl.cap, hipHostMallocDefault));
         DDL_HIP(hipMalloc(&sl.dev, sl.cap));
     }
-    // segment-aligned tiles (variants 1..3): tile bytes per workgroup; tile0 = running tile count
-    const uint64_t seg_tile = variant == 2 ? 2048 : variant == 3 ? 4096 : 1024;
     SegDesc *t = static_cast<SegDesc *>(sl.host);
-    uint64_t off = 0, tiles = 0;
+    uint32_t *bases = reinterpret_cast<uint32_t *>(static_cast<char *>(sl.host) + table);
+    uint64_t off = 0, tl = 0;
     for (int i = 0; i < count; ++i) {
         DDL_REQUIRE(bytes[i] == 0 || segs[i], DDL_STATUS_INVALID_ARGUMENT, "null segment " << i);
         t[i].ptr = reinterpret_cast<uint64_t>(segs[i]);
         t[i].off = off;
         t[i].len = bytes[i];
         t[i].vec = (reinterpret_cast<uintptr_t>(segs[i]) & 15u) == 0;
-        t[i].tile0 = (uint32_t)tiles;
+        t[i].tile0 = (uint32_t)tl;
         off += (bytes[i] + 255) & ~uint64_t(255);
-        tiles += (bytes[i] + seg_tile - 1) / seg_tile;
+        tl += (bytes[i] + seg_tile - 1) / seg_tile;
     }
-    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
     if (off == 0) return;
+    // block b's base: the segment of tile b * 128 (the last one with tile0 <= it, as
+    // k_tile_index resolves); narrow when no block spans more than 255 segments
+    // (DDL_PACK_INDEX=32 forces the int32 index, for measurement)
+    static const bool wide_only = [] {
+        const char *e = std::getenv("DDL_PACK_INDEX");
+        return e && std::atoi(e) == 32;
+    }();
+    bool narrow = !wide_only;
+    for (uint64_t b = 0, s0 = 0, s1 = 0; b < nblk; ++b) {
+        const uint64_t first = b * kIdxBlock, last = std::min(tiles, first + kIdxBlock) - 1;
+        while (s0 + 1 < (uint64_t)count && t[s0 + 1].tile0 <= first) ++s0;
+        if (s1 < s0) s1 = s0;
+        while (s1 + 1 < (uint64_t)count && t[s1 + 1].tile0 <= last) ++s1;
+        bases[b] = (uint32_t)s0;
+        if (s1 - s0 > 255) narrow = false;
+    }
     DDL_HIP(hipMemcpyAsync(sl.dev, sl.host, need, hipMemcpyHostToDevice, stream));
     char *fl = static_cast<char *>(flat);
     const SegDesc *dd = static_cast<const SegDesc *>(sl.dev);
+    const uint32_t *db = reinterpret_cast<const uint32_t *>(static_cast<char *>(sl.dev) + table);
     if (tiles > 0) {
-        const size_t ib = tiles * sizeof(int);
+        const size_t ib = narrow ? (tiles + 3) & ~uint64_t(3) : tiles * sizeof(int);
         if (ib > sl.idx_cap) {
             if (sl.idx) DDL_HIP(hipFree(sl.idx));
             sl.idx = nullptr;
             sl.idx_cap = ib + ib / 2;
             DDL_HIP(hipMalloc(&sl.idx, sl.idx_cap));
         }
-        int *ts = static_cast<int *>(sl.idx);
-        hipLaunchKernelGGL(k_tile_index, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, stream, dd, count,
-                           (uint64_t)tiles, ts);
-        const dim3 g((unsigned)tiles);
-        if (dir == 0) {
-            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<0, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
-            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<0, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
-            else hipLaunchKernelGGL((k_seg_tiles<0, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts, xcd);
-        } else {
-            if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<1, 1, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
-            else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<1, 2, 128>), g, dim3(128), 0, stream, fl, dd, ts, xcd);
-            else hipLaunchKernelGGL((k_seg_tiles<1, 1, 64>), g, dim3(64), 0, stream, fl, dd, ts, xcd);
-        }
+        const dim3 ig((unsigned)((tiles + 255) / 256)), g((unsigned)tiles);
+        if (narrow) hipLaunchKernelGGL(k_tile_index<true>, ig, dim3(256), 0, stream, dd, count, (uint64_t)tiles, db, sl.idx);
+        else hipLaunchKernelGGL(k_tile_index<false>, ig, dim3(256), 0, stream, dd, count, (uint64_t)tiles, db, sl.idx);
+        launch_tiles(dir, variant, narrow, g, stream, fl, dd, db, sl.idx);
     }
     DDL_HIP(hipGetLastError());
     DDL_HIP(hipEventRecord(sl.ready, stream));

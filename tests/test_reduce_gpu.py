@@ -123,18 +123,21 @@ def test_pack_unpack_roundtrip(lib, gpu):
         off += (s + 255) // 256 * 256
 
 
-@pytest.mark.parametrize('case', ['dense_tiny', 'many_segments', 'unaligned', 'zero_lengths'])
+@pytest.mark.parametrize('case', ['dense_tiny', 'many_segments', 'unaligned', 'zero_lengths', 'empty_runs'])
 def test_pack_unpack_layouts(lib, gpu, case):
-    """Segment tables the span kernel must resolve: > 64 segments per 64 KiB span (global-walk
-    fallback), > 4096 segments (3 search rounds), byte-misaligned pointers (byte path), and
-    zero-length segments sharing an offset with their successor."""
-    rng = np.random.default_rng(hash(case) % 1000)
+    """Segment tables the tile index must resolve: one-tile segments (128 segments per index
+    block), > 4096 segments, byte-misaligned pointers (byte path), zero-length segments sharing a
+    tile with their successor, and runs of 300 empty segments inside one 128-tile block (more
+    than a byte's reach: the int32 index fallback)."""
+    rng = np.random.default_rng(sum(map(ord, case)))
     if case == 'dense_tiny':
         sizes = [int(s) for s in rng.integers(1, 300, size=3000)]
     elif case == 'many_segments':
         sizes = [int(s) for s in rng.integers(1, 5000, size=9000)]
     elif case == 'unaligned':
         sizes = [int(s) for s in rng.integers(1, 40_000, size=200)]
+    elif case == 'empty_runs':
+        sizes = ([3000, 17] + [0] * 300 + [5, 2048]) * 3 + [70_001]
     else:
         sizes = [0, 5, 0, 0, 300, 0, 70_000, 0, 17]
     pool = torch.from_numpy(rng.integers(0, 255, size=sum(sizes) + 16 * len(sizes) + 64, dtype=np.uint8)).to(gpu)

@@ -1,0 +1,29 @@
+"""Keyed host-tensor C5 batch (bench.keyed_host_c5) vs the memcpy workers of the pinned staging
+pipeline ("host_copy_threads") and its chunk size (measurement tool, not shipped)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
+
+
+def main():
+    import torch
+    import bench
+    from ddl.torch.communicator import Communicator
+    from ddl.torch.cpp_backend import CPPBackend, check
+    torch.cuda.set_device(0)
+    lib = CPPBackend.c_api()
+    comm = Communicator.world()
+    for threads, chunk in ((0, 32), (3, 32), (7, 32), (15, 32), (15, 16), (15, 64), (23, 32)):
+        check(lib.ddl_set_config(b'host_copy_threads', threads), 'cfg')
+        check(lib.ddl_set_config(b'host_chunk_bytes', chunk << 20), 'cfg')
+        r = bench.keyed_host_c5(lib, comm, steps=2)
+        print(json.dumps({'host_copy_threads': threads, 'chunk_MiB': chunk, 'ms': r['ms'], 'GiBs': r['bucket_GiBs']}),
+              flush=True)
+
+
+if __name__ == '__main__':
+    main()
