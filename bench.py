@@ -572,7 +572,7 @@ def multi_gpu(args):
     check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
           'ddl_tune_result')
     if chosen.value >= 0:
-        cands = [{'algo': ['ring', 'direct', 'oneshot'][cfgs[4 * i]], 'rings': cfgs[4 * i + 1],
+        cands = [{'algo': algo_name(cfgs[4 * i]), 'rings': cfgs[4 * i + 1],
                   'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
                   'ms': round(tms[i], 4)} for i in range(min(count.value, 16))]
         tune = {'chosen': cands[chosen.value], 'candidates': cands}
@@ -613,13 +613,14 @@ def multi_gpu(args):
         'value_is': 'allreduce algbw: bucket bytes / max-over-ranks time per allreduce (GiB/s)',
         'algbw_GiBs': round(algbw, 2),
         'busbw_GBs': round(busbw_gbs, 2),
-        'link_roofline': dict(ceiling, frac=round(busbw_gbs / ceiling['busbw_ceiling_GBs'], 4),
-                              algbw_frac=round(algbw * GiB / 1e9 / ceiling['algbw_ceiling_GBs'], 4)),
+        'link_roofline': (None if ceiling is None else
+                          dict(ceiling, frac=round(busbw_gbs / ceiling['busbw_ceiling_GBs'], 4),
+                               algbw_frac=round(algbw * GiB / 1e9 / ceiling['algbw_ceiling_GBs'], 4))),
         'autotune': tune,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'kernel': (f'k_sumN_tile<float,{world - 1}> (direct reduce-scatter fold)'
-                                if tune and tune['chosen']['algo'] == 'direct' else
+                     'kernel': (f'k_sumN_tile<float,{world - 1}> ({tune["chosen"]["algo"]} fold)'
+                                if tune and tune['chosen']['algo'] != 'ring' else
                                 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
                      'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},
         'check': {'sum_of_recv_min': cs_min.item(), 'sum_of_recv_max': cs_max.item(),
@@ -631,106 +632,133 @@ def multi_gpu(args):
     # parity on this node first, so no optional leg can hide it: every rank's result equals
     # MPI_Allreduce's (MPICH 3.3.2 order) bit for bit, on both sides of MPICH's 2048-byte switch
     state['leg'] = 'parity'
-    out['parity_vs_mpich_order'] = parity_leg(lib, comm, dist, torch, dev, stream, rank, world)
+    try:
+        out['parity_vs_mpich_order'] = parity_leg(lib, comm, dist, torch, dev, stream, rank, world)
+    except Exception as e:
+        out['parity_vs_mpich_order'] = {'bit_exact': False, 'error': repr(e)[:400]}
 
     state['leg'] = 'rccl_comparator'
-    if not args.rehearse:
-        sec_rccl = timed(1, max(5, args.steps // 2), 3)
-        out['rccl_allreduce_comparator'] = {'ms': round(sec_rccl * 1e3, 4),
-                                            'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
+    try:
+        if not args.rehearse:
+            sec_rccl = timed(1, max(5, args.steps // 2), 3)
+            out['rccl_allreduce_comparator'] = {'ms': round(sec_rccl * 1e3, 4),
+                                                'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['rccl_comparator'] = repr(e)[:400]
     # fixed schedules, tuner off (every rank sets the same values in the same order: the
     # schedule must be identical on all ranks)
     state['leg'] = 'schedule_sweep'
-    sweep = []
-    if not args.no_config_sweep:
-        keys = ('algo', 'rings', 'slice_bytes', 'tune', 'reference_order')
-        defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
-        lib.ddl_set_config(b'tune', 0)
-        # each schedule as such (with reference_order a ring at P > 2 would run as direct)
-        lib.ddl_set_config(b'reference_order', 0)
-        for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
-                                       (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64)):
-            if algo == 1 and world < 3:
-                continue
-            lib.ddl_set_config(b'algo', algo)
-            lib.ddl_set_config(b'rings', rings)
-            lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
-            t = timed(0, max(5, args.steps // 4), 2)
-            sweep.append({'algo': ['ring', 'direct', 'oneshot'][algo], 'rings': rings, 'slice_MiB': slice_mib,
-                          'ms': round(t * 1e3, 4), 'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
-            out['schedule_sweep'] = sweep
-        for k, v in defaults.items():
-            lib.ddl_set_config(k.encode(), v)
+    try:
+        sweep = []
+        if not args.no_config_sweep:
+            keys = ('algo', 'rings', 'slice_bytes', 'tune', 'reference_order')
+            defaults = {k: lib.ddl_get_config(k.encode()) for k in keys}
+            lib.ddl_set_config(b'tune', 0)
+            # each schedule as such (with reference_order a ring at P > 2 would run as direct)
+            lib.ddl_set_config(b'reference_order', 0)
+            try:
+                for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
+                                               (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64)):
+                    if algo == 1 and world < 3:
+                        continue
+                    lib.ddl_set_config(b'algo', algo)
+                    lib.ddl_set_config(b'rings', rings)
+                    lib.ddl_set_config(b'slice_bytes', slice_mib << 20)
+                    t = timed(0, max(5, args.steps // 4), 2)
+                    sweep.append({'algo': algo_name(algo), 'rings': rings, 'slice_MiB': slice_mib,
+                                  'ms': round(t * 1e3, 4),
+                                  'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2)})
+                    out['schedule_sweep'] = sweep
+            finally:  # every rank restores the same shared config
+                for k, v in defaults.items():
+                    lib.ddl_set_config(k.encode(), v)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['schedule_sweep'] = repr(e)[:400]
     # C4: fp16, 1 GiB as 64 x 16 MiB buckets, one ddl_allreduce per bucket
     state['leg'] = 'c4'
-    if not args.no_c4:
-        nb = (16 << 20) // 2
-        c4_bufs = [torch.randn(nb, device=dev, generator=g).half() for _ in range(64)]
+    try:
+        if not args.no_c4:
+            nb = (16 << 20) // 2
+            c4_bufs = [torch.randn(nb, device=dev, generator=g).half() for _ in range(64)]
 
-        def c4_step():
-            for b in c4_bufs:
-                check(lib.ddl_allreduce(comm.id, b.data_ptr(), b.data_ptr(), nb, 19, 0, stream.cuda_stream),
-                      'ddl_allreduce')
-        t = timed_fn(c4_step, 3, 1)
-        out['c4_fp16_64x16MiB'] = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
-                                   'algbw_GiBs': round((1 << 30) / GiB / t, 2),
-                                   'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
-        del c4_bufs
+            def c4_step():
+                for b in c4_bufs:
+                    check(lib.ddl_allreduce(comm.id, b.data_ptr(), b.data_ptr(), nb, 19, 0, stream.cuda_stream),
+                          'ddl_allreduce')
+            t = timed_fn(c4_step, 3, 1)
+            out['c4_fp16_64x16MiB'] = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
+                                       'algbw_GiBs': round((1 << 30) / GiB / t, 2),
+                                       'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
+            del c4_bufs
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['c4'] = repr(e)[:400]
     # broadcast (root 0) and allgather of the same bucket size (§8f #3)
     state['leg'] = 'broadcast_allgather'
-    if not args.no_collectives:
-        bc = recv.clone()
-        t_b = timed_fn(lambda: check(lib.ddl_broadcast(comm.id, bc.data_ptr(), n, DT_FLOAT, 0, stream.cuda_stream),
-                                     'ddl_broadcast'), max(5, args.steps // 4), 2)
-        per = n // world
-        t_g = timed_fn(lambda: check(lib.ddl_allgather(comm.id, send.data_ptr(), per, recv.data_ptr(), per, DT_FLOAT,
-                                                       stream.cuda_stream), 'ddl_allgather'),
-                       max(5, args.steps // 4), 2)
-        out['broadcast_allgather'] = {
-            'broadcast': {'bytes': S, 'ms': round(t_b * 1e3, 4), 'algbw_GiBs': round(S / GiB / t_b, 2),
-                          'root_link_bytes': 2 * S // world},
-            'allgather': {'bytes_out': per * world * 4, 'ms': round(t_g * 1e3, 4),
-                          'algbw_GiBs': round(per * world * 4 / GiB / t_g, 2),
-                          'busbw_GBs': round((world - 1) * per * 4 / t_g / 1e9, 2)}}
-        del bc
+    try:
+        if not args.no_collectives:
+            bc = recv.clone()
+            t_b = timed_fn(lambda: check(lib.ddl_broadcast(comm.id, bc.data_ptr(), n, DT_FLOAT, 0, stream.cuda_stream),
+                                         'ddl_broadcast'), max(5, args.steps // 4), 2)
+            per = n // world
+            t_g = timed_fn(lambda: check(lib.ddl_allgather(comm.id, send.data_ptr(), per, recv.data_ptr(), per, DT_FLOAT,
+                                                           stream.cuda_stream), 'ddl_allgather'),
+                           max(5, args.steps // 4), 2)
+            out['broadcast_allgather'] = {
+                'broadcast': {'bytes': S, 'ms': round(t_b * 1e3, 4), 'algbw_GiBs': round(S / GiB / t_b, 2),
+                              'root_link_bytes': 2 * S // world},
+                'allgather': {'bytes_out': per * world * 4, 'ms': round(t_g * 1e3, 4),
+                              'algbw_GiBs': round(per * world * 4 / GiB / t_g, 2),
+                              'busbw_GBs': round((world - 1) * per * 4 / t_g / 1e9, 2)}}
+            del bc
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['broadcast_allgather'] = repr(e)[:400]
     state['leg'] = 'host_resident'
-    if not args.no_host:
-        out['host_resident'] = host_resident_rate(lib, comm, S, reps=4)
+    try:
+        if not args.no_host:
+            out['host_resident'] = host_resident_rate(lib, comm, S, reps=4)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['host_resident'] = repr(e)[:400]
     state['leg'] = 'fusion_c5'
-    if not args.no_fusion:
-        out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
+    try:
+        if not args.no_fusion:
+            out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['fusion_c5'] = repr(e)[:400]
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
     # size class) next to RCCL's own ncclAllReduce on the same buffers
     state['leg'] = 'size_sweep'
-    if not args.no_size_sweep:
-        curve = []
-        for sz in [(4 << 10) << (2 * k) for k in range(10)]:  # 4 KiB, 16 KiB, ..., 1 GiB
-            if sz > args.size_sweep_max_mib << 20:
-                break
-            m = sz // 4
-            a = torch.randn(m, device=dev, generator=g)
-            b = torch.empty_like(a)
-            reps = int(min(200, max(5, (64 << 20) // sz)))
+    try:
+        if not args.no_size_sweep:
+            curve = []
+            for sz in [(4 << 10) << (2 * k) for k in range(10)]:  # 4 KiB, 16 KiB, ..., 1 GiB
+                if sz > args.size_sweep_max_mib << 20:
+                    break
+                m = sz // 4
+                a = torch.randn(m, device=dev, generator=g)
+                b = torch.empty_like(a)
+                reps = int(min(200, max(5, (64 << 20) // sz)))
 
-            def one(variant, a=a, b=b, m=m):
-                check(lib.ddl_allreduce_variant(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0,
-                                                stream.cuda_stream, variant), 'ddl_allreduce_variant')
-            t_ours = timed_fn(lambda: one(0), reps, 3)
-            t_rccl = t_ours if args.rehearse else timed_fn(lambda: one(1), reps, 3)
-            chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
-            check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
-                  'ddl_tune_result')
-            pick = None
-            if chosen.value >= 0:
-                i = chosen.value
-                pick = f"{['ring', 'direct', 'oneshot'][cfgs[4 * i]]}/r{cfgs[4 * i + 1]}/s{cfgs[4 * i + 2] >> 10}K"
-            curve.append({'bytes': sz, 'us': round(t_ours * 1e6, 1), 'algbw_GiBs': round(sz / GiB / t_ours, 3),
-                          'busbw_GBs': round(2 * (world - 1) / world * sz / t_ours / 1e9, 2),
-                          'rccl_us': round(t_rccl * 1e6, 1),
-                          'rccl_busbw_GBs': round(2 * (world - 1) / world * sz / t_rccl / 1e9, 2),
-                          'schedule': pick})
-            out['size_sweep_fp32'] = curve
-            del a, b
+                def one(variant, a=a, b=b, m=m):
+                    check(lib.ddl_allreduce_variant(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0,
+                                                    stream.cuda_stream, variant), 'ddl_allreduce_variant')
+                t_ours = timed_fn(lambda: one(0), reps, 3)
+                t_rccl = t_ours if args.rehearse else timed_fn(lambda: one(1), reps, 3)
+                chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
+                check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
+                      'ddl_tune_result')
+                pick = None
+                if chosen.value >= 0:
+                    i = chosen.value
+                    pick = f"{algo_name(cfgs[4 * i])}/r{cfgs[4 * i + 1]}/s{cfgs[4 * i + 2] >> 10}K"
+                curve.append({'bytes': sz, 'us': round(t_ours * 1e6, 1), 'algbw_GiBs': round(sz / GiB / t_ours, 3),
+                              'busbw_GBs': round(2 * (world - 1) / world * sz / t_ours / 1e9, 2),
+                              'rccl_us': round(t_rccl * 1e6, 1),
+                              'rccl_busbw_GBs': round(2 * (world - 1) / world * sz / t_rccl / 1e9, 2),
+                              'schedule': pick})
+                out['size_sweep_fp32'] = curve
+                del a, b
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['size_sweep'] = repr(e)[:400]
     state['leg'] = 'finalize'
     if rank == 0:
         emit(out)
@@ -742,6 +770,13 @@ def multi_gpu(args):
     dog.cancel()
 
 
+ALGO_NAMES = ('ring', 'direct', 'oneshot', 'gatherfold')  # schedule.h enum Algo
+
+
+def algo_name(a):
+    return ALGO_NAMES[a] if 0 <= a < len(ALGO_NAMES) else f'algo{a}'
+
+
 def link_ceiling(P, S=None):
     """Roofline of one allreduce at P ranks, in busbw = 2(P-1)/P x S / t terms.
     The reference-order direct schedule (what runs at P > 2): each rank sends chunk-slices to its
@@ -749,7 +784,9 @@ def link_ceiling(P, S=None):
     links carries 2S/P per allreduce -> t >= 2S / (P x B_link), busbw <= (P-1) x B_link (the
     same as P-1 edge-disjoint rings). HBM per rank: (5P-3)/P x S bytes (RS send reads + staging
     writes, the fold's P inputs + 1 output, AG send reads + receive writes) -> busbw <=
-    2(P-1)/(5P-3) x HBM. The ceiling is the smaller."""
+    2(P-1)/(5P-3) x HBM. The ceiling is the smaller. None at P = 1 (no exchange)."""
+    if P < 2:
+        return None
     links = (P - 1) * XGMI_LINK_GBS
     hbm = 2 * (P - 1) / (5 * P - 3) * HBM_PEAK_GBS
     bus = min(links, hbm)
