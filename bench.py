@@ -158,6 +158,38 @@ VARIANTS = {'default': -1, 'plain': 0, 'nt_load_a': 1, 'nt_load_ab': 3, 'nt_all'
             'lds_stage_b_nt_a': 9}
 
 
+GRAPH_SWEEP_MAX = 8 << 20  # sweep points also timed as hipGraph replays (launch-bound sizes)
+
+
+def graph_reduce_us(lib, bufs, m, variant, per_graph=64, replays=20):
+    """Per-bucket time of `per_graph` reduce launches captured into one hipGraph (torch.cuda.graph
+    on a side stream: hipStreamBeginCapture) and replayed: the kernels back to back with no host
+    launch in between — what a captured training step gets for its small buckets."""
+    import torch
+    from ddl.torch.cpp_backend import check
+    gs = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph, stream=gs):
+        for i in range(per_graph):
+            acc, inp = bufs[i % len(bufs)]
+            check(lib.ddl_reduce_sum2_variant(variant, acc.data_ptr(), acc.data_ptr(), inp.data_ptr(), m, DT_FLOAT,
+                                              gs.cuda_stream), 'ddl_reduce_sum2_variant (captured)')
+    best = float('inf')
+    for _ in range(3):
+        with torch.cuda.stream(gs):
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(gs)
+            for _ in range(replays):
+                graph.replay()
+            e1.record(gs)
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / (replays * per_graph))
+    del graph
+    return best
+
+
 def single_gpu(args):
     import torch
     from ddl.torch.cpp_backend import CPPBackend, check
@@ -222,8 +254,12 @@ def single_gpu(args):
             for _ in range(3):
                 step(m=m, bufs=bufs)
             t = min(timed_kernel_ms(reps, m=m, bufs=bufs) for _ in range(3)) / 1e3  # best of 3 rounds
-            sweep.append({'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
-                          'hbm_GBs': round(3 * size / t / 1e9, 1)})
+            point = {'bytes': size, 'us': round(t * 1e6, 2), 'bucket_GiBs': round(size / t / GiB, 2),
+                     'hbm_GBs': round(3 * size / t / 1e9, 1)}
+            if size <= GRAPH_SWEEP_MAX:  # launch-bound sizes: the same launches replayed from a hipGraph
+                tg = graph_reduce_us(lib, bufs, m, args.variant) / 1e6
+                point.update(graph_us=round(tg * 1e6, 2), graph_bucket_GiBs=round(size / tg / GiB, 2))
+            sweep.append(point)
             del bufs
             size *= 2  # 4 KiB * 2^k up to 1 GiB, 19 points
         extra['sweep_fp32'] = sweep
@@ -759,6 +795,40 @@ def multi_gpu(args):
                 del a, b
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['size_sweep'] = repr(e)[:400]
+    # the latency-bound end of the curve again with the allreduces captured into a hipGraph
+    # (each size class was tuned above, outside the capture): no host enqueue per call
+    state['leg'] = 'size_sweep_graph'
+    try:
+        if not args.no_size_sweep:
+            gcurve = []
+            for sz in [(4 << 10) << (2 * k) for k in range(6)]:  # 4 KiB .. 4 MiB
+                if sz > args.size_sweep_max_mib << 20:
+                    break
+                m = sz // 4
+                a = torch.randn(m, device=dev, generator=g)
+                b = torch.empty_like(a)
+                per_graph, replays = 16, 10
+                gs = torch.cuda.Stream()
+                with torch.cuda.stream(gs):  # warm: tuned class, staging and events sized
+                    check(lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0, gs.cuda_stream),
+                          'ddl_allreduce')
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=gs):
+                    for _ in range(per_graph):
+                        check(lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), m, DT_FLOAT, 0, gs.cuda_stream),
+                              'ddl_allreduce (captured)')
+
+                def replay(graph=graph, gs=gs):
+                    with torch.cuda.stream(gs):
+                        graph.replay()
+                t = timed_fn(replay, replays, 1) / per_graph
+                gcurve.append({'bytes': sz, 'us': round(t * 1e6, 1), 'algbw_GiBs': round(sz / GiB / t, 3),
+                               'busbw_GBs': round(2 * (world - 1) / world * sz / t / 1e9, 2)})
+                out['size_sweep_graph_fp32'] = gcurve
+                del graph, a, b
+    except Exception as e:  # e.g. the rehearsal's host-synchronising transport cannot be captured
+        out.setdefault('leg_errors', {})['size_sweep_graph'] = repr(e)[:400]
     state['leg'] = 'finalize'
     if rank == 0:
         emit(out)

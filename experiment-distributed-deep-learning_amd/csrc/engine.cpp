@@ -234,7 +234,12 @@ RingConfig Communicator::ring_config(size_t n, int dtype, hipStream_t stream) {
     }
     const int cls = size_class(n * dtype_size(dtype));
     auto it = tuned_.find(cls);
-    if (it == tuned_.end()) it = tuned_.emplace(cls, tune_(n, dtype, stream, base)).first;
+    if (it == tuned_.end()) {
+        // tuning times candidates and synchronises: inside a graph capture the configured
+        // schedule is captured instead (the class is tuned by its first call outside one)
+        if (stream_capturing(stream)) return base;
+        it = tuned_.emplace(cls, tune_(n, dtype, stream, base)).first;
+    }
     return it->second.candidates[it->second.chosen];
 }
 

@@ -5,6 +5,11 @@
 
 namespace ddl {
 
+bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
 void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     if (ops.empty()) return;
     const RcclApi &api = rccl();
@@ -92,8 +97,11 @@ void RankResources::ensure_events(size_t ticks) {
     }
 }
 
-void *RankResources::ensure_staging(size_t bytes) {
+void *RankResources::ensure_staging(size_t bytes, bool capturing) {
     if (bytes > staging_bytes_) {
+        DDL_REQUIRE(!capturing, DDL_STATUS_INVALID_ARGUMENT,
+                    "the staging buffer would grow (to " << bytes << " B) inside a stream capture: run this "
+                    "collective once before capturing it");
         if (staging_) {
             // a previous call may still read it on the device
             DDL_HIP(hipStreamSynchronize(comm));
@@ -168,7 +176,7 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
         if (in != out) DDL_HIP(hipMemcpyAsync(out, in, n * es, hipMemcpyDeviceToDevice, user));
         return;
     }
-    void *staging = res_.ensure_staging(program_staging_elems(n, es, size_, cfg) * es);
+    void *staging = res_.ensure_staging(program_staging_elems(n, es, size_, cfg) * es, stream_capturing(user));
     build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
     run_(dtype, user);
 }
@@ -190,29 +198,43 @@ void RingExecutor::allgatherv(const void *send, void *recv, const size_t *counts
 
 void RingExecutor::run_(int dtype, hipStream_t user) {
     if (prog_.ticks.empty()) return;
+    // Inside a graph capture the ticks are posted in order on the captured stream itself (every
+    // dependency of the program points backwards in tick order, so stream order implies it).
+    // Posted on the forked comm / compute streams, the program made hipStreamEndCapture segfault
+    // in the HIP runtime torch loads (7.0.2; tools/graph_probe.py), although every fork / join
+    // shape it uses passes alone (tools/capture_patterns.hip) — DESIGN §9. A graph is for
+    // latency-bound buckets, where the reduce / exchange overlap inside one call buys little.
+    const bool serial = stream_capturing(user);
+    DDL_REQUIRE(!serial || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
+                "this communicator's transport synchronises the host and cannot be captured into a graph");
+    const bool timing = timing_ && !serial;
+    hipStream_t comm = serial ? user : res_.comm, compute = serial ? user : res_.compute;
     res_.ensure_events(prog_.ticks.size());
-    DDL_HIP(hipEventRecord(res_.fork_ev, user));
-    DDL_HIP(hipStreamWaitEvent(res_.comm, res_.fork_ev, 0));
-    DDL_HIP(hipStreamWaitEvent(res_.compute, res_.fork_ev, 0));
+    if (!serial) {
+        DDL_HIP(hipEventRecord(res_.fork_ev, user));
+        DDL_HIP(hipStreamWaitEvent(comm, res_.fork_ev, 0));
+        DDL_HIP(hipStreamWaitEvent(compute, res_.fork_ev, 0));
+    }
     for (size_t t = 0; t < prog_.ticks.size(); ++t) {
         const Tick &tk = prog_.ticks[t];
-        if (tk.wait_reduce >= 0) {
+        if (tk.wait_reduce >= 0 && !serial) {
             int w = last_reduce_at_or_before(prog_, tk.wait_reduce);
-            if (w >= 0) DDL_HIP(hipStreamWaitEvent(res_.comm, res_.red_ev[w], 0));
+            if (w >= 0) DDL_HIP(hipStreamWaitEvent(comm, res_.red_ev[w], 0));
         }
-        for (const CopyOp &c : tk.copies)
-            DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, res_.comm));
+        for (const CopyOp &c : tk.copies) DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, comm));
         if (transport_) {
-            if (tk.gather.bytes) transport_->allgather(tk.gather, res_.comm);
-            transport_->group(tk.ops, res_.comm);
+            if (tk.gather.bytes) transport_->allgather(tk.gather, comm);
+            transport_->group(tk.ops, comm);
         } else {
             DDL_REQUIRE(tk.ops.empty() && !tk.gather.bytes, DDL_STATUS_ERROR_UNKNOWN, "no transport for a multi-rank program");
         }
         if (tk.has_reduce) {
-            DDL_HIP(hipEventRecord(res_.comm_ev[t], res_.comm));
-            DDL_HIP(hipStreamWaitEvent(res_.compute, res_.comm_ev[t], 0));
+            if (!serial) {
+                DDL_HIP(hipEventRecord(res_.comm_ev[t], comm));
+                DDL_HIP(hipStreamWaitEvent(compute, res_.comm_ev[t], 0));
+            }
             std::pair<hipEvent_t, hipEvent_t> tp{nullptr, nullptr};
-            if (timing_) {
+            if (timing) {
                 if (free_pairs_.empty()) {
                     DDL_HIP(hipEventCreate(&tp.first));
                     DDL_HIP(hipEventCreate(&tp.second));
@@ -220,20 +242,21 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
                     tp = free_pairs_.back();
                     free_pairs_.pop_back();
                 }
-                DDL_HIP(hipEventRecord(tp.first, res_.compute));
+                DDL_HIP(hipEventRecord(tp.first, compute));
             }
-            const double bytes = launch_tick_reduce(tk, dtype, res_.compute);
-            if (timing_) {
-                DDL_HIP(hipEventRecord(tp.second, res_.compute));
+            const double bytes = launch_tick_reduce(tk, dtype, compute);
+            if (timing) {
+                DDL_HIP(hipEventRecord(tp.second, compute));
                 timed_.push_back(tp);
                 timed_bytes_.push_back(bytes);
             }
-            DDL_HIP(hipEventRecord(res_.red_ev[t], res_.compute));
+            if (!serial) DDL_HIP(hipEventRecord(res_.red_ev[t], compute));
         }
     }
+    if (serial) return;
     // the last tick waited for the last reduce (allreduce) or there is none, so the comm
     // stream's tail covers everything
-    DDL_HIP(hipEventRecord(res_.join_ev, res_.comm));
+    DDL_HIP(hipEventRecord(res_.join_ev, comm));
     DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
 }
 
@@ -272,8 +295,9 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
         if (in[0] != out[0]) DDL_HIP(hipMemcpyAsync(out[0], in[0], n * es, hipMemcpyDeviceToDevice, user));
         return;
     }
+    const bool capture = stream_capturing(user);
     for (int r = 0; r < P_; ++r) {
-        void *st = res_[r]->ensure_staging(program_staging_elems(n, es, P_, cfg) * es);
+        void *st = res_[r]->ensure_staging(program_staging_elems(n, es, P_, cfg) * es, capture);
         build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
     }
     run_(dtype, user);
@@ -305,11 +329,23 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         loop_ev_.push_back(e);
     }
+    // under a graph capture every rank's work goes on the captured stream in posting order
+    // (as RingExecutor::run_ does): event waits are then implied by stream order
+    const bool serial = stream_capturing(user);
+    auto comm = [&](int r) { return serial ? user : res_[r]->comm; };
+    auto compute = [&](int r) { return serial ? user : res_[r]->compute; };
+    auto loop_stream = [&] { return serial ? user : loop_stream_; };
+    auto record = [&](hipEvent_t e, hipStream_t st) {
+        if (!serial) DDL_HIP(hipEventRecord(e, st));
+    };
+    auto wait = [&](hipStream_t st, hipEvent_t e) {
+        if (!serial) DDL_HIP(hipStreamWaitEvent(st, e, 0));
+    };
     hipEvent_t fork = res_[0]->fork_ev;
-    DDL_HIP(hipEventRecord(fork, user));
+    record(fork, user);
     for (int r = 0; r < P_; ++r) {
-        DDL_HIP(hipStreamWaitEvent(res_[r]->comm, fork, 0));
-        DDL_HIP(hipStreamWaitEvent(res_[r]->compute, fork, 0));
+        wait(comm(r), fork);
+        wait(compute(r), fork);
     }
     for (size_t t = 0; t < T; ++t) {
         // 1) each rank's comm stream reaches the tick (after its reduce dependency)
@@ -318,11 +354,11 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             RankResources &rr = *res_[r];
             if (tk.wait_reduce >= 0) {
                 int w = last_reduce_at_or_before(progs_[r], tk.wait_reduce);
-                if (w >= 0) DDL_HIP(hipStreamWaitEvent(rr.comm, rr.red_ev[w], 0));
+                if (w >= 0) wait(comm(r), rr.red_ev[w]);
             }
             for (const CopyOp &c : tk.copies)
-                DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, rr.comm));
-            DDL_HIP(hipEventRecord(rr.pre_ev[t], rr.comm));
+                DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, comm(r)));
+            record(rr.pre_ev[t], comm(r));
         }
         // 1b) allgather ticks: rank q's block into every rank's recv at q * bytes, once q has
         //     reached the tick (copies, or self pairs through RCCL on the loopback)
@@ -338,22 +374,22 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                         pairs.push_back(P2POp{true, 0, 0, const_cast<void *>(src.send), g.bytes});
                         pairs.push_back(P2POp{false, 0, 0, dst, g.bytes});
                     } else {
-                        DDL_HIP(hipStreamWaitEvent(res_[r]->comm, res_[q]->pre_ev[t], 0));
-                        DDL_HIP(hipMemcpyAsync(dst, src.send, g.bytes, hipMemcpyDeviceToDevice, res_[r]->comm));
+                        wait(comm(r), res_[q]->pre_ev[t]);
+                        DDL_HIP(hipMemcpyAsync(dst, src.send, g.bytes, hipMemcpyDeviceToDevice, comm(r)));
                     }
                 }
             }
             if (loop_) {
-                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(loop_stream_, res_[r]->pre_ev[t], 0));
-                loop_->group(pairs, loop_stream_);
-                DDL_HIP(hipEventRecord(loop_ev_[t], loop_stream_));
-                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, loop_ev_[t], 0));
+                for (int r = 0; r < P_; ++r) wait(loop_stream(), res_[r]->pre_ev[t]);
+                loop_->group(pairs, loop_stream());
+                record(loop_ev_[t], loop_stream());
+                for (int r = 0; r < P_; ++r) wait(comm(r), loop_ev_[t]);
                 loop_pairs_ += (long long)pairs.size() / 2;
             } else {
                 // every rank's block is read by the others: none may run ahead and overwrite
-                for (int r = 0; r < P_; ++r) DDL_HIP(hipEventRecord(res_[r]->pre_ev[t], res_[r]->comm));
+                for (int r = 0; r < P_; ++r) record(res_[r]->pre_ev[t], comm(r));
                 for (int r = 0; r < P_; ++r)
-                    for (int q = 0; q < P_; ++q) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, res_[q]->pre_ev[t], 0));
+                    for (int q = 0; q < P_; ++q) wait(comm(r), res_[q]->pre_ev[t]);
             }
         }
         if (loop_) {
@@ -371,10 +407,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 }
             }
             if (!pairs.empty()) {
-                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(loop_stream_, res_[r]->pre_ev[t], 0));
-                loop_->group(pairs, loop_stream_);
-                DDL_HIP(hipEventRecord(loop_ev_[t], loop_stream_));
-                for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(res_[r]->comm, loop_ev_[t], 0));
+                for (int r = 0; r < P_; ++r) wait(loop_stream(), res_[r]->pre_ev[t]);
+                loop_->group(pairs, loop_stream());
+                record(loop_ev_[t], loop_stream());
+                for (int r = 0; r < P_; ++r) wait(comm(r), loop_ev_[t]);
                 loop_pairs_ += (long long)pairs.size() / 2;
             }
         } else {
@@ -387,16 +423,15 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 for (const P2POp &op : progs_[r].ticks[t].ops) {
                     if (op.send) continue;
                     const P2POp &match = match_(r, t, op, seen);
-                    DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->pre_ev[t], 0));
-                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, rr.comm));
+                    wait(comm(r), res_[op.peer]->pre_ev[t]);
+                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, comm(r)));
                 }
-                DDL_HIP(hipEventRecord(rr.post_ev[t], rr.comm));
+                record(rr.post_ev[t], comm(r));
             }
             // 3) a group completes for the sender only once its receivers have the data
             for (int r = 0; r < P_; ++r) {
-                RankResources &rr = *res_[r];
                 for (const P2POp &op : progs_[r].ticks[t].ops)
-                    if (op.send) DDL_HIP(hipStreamWaitEvent(rr.comm, res_[op.peer]->post_ev[t], 0));
+                    if (op.send) wait(comm(r), res_[op.peer]->post_ev[t]);
             }
         }
         // 4) reduce of the received slices
@@ -404,15 +439,15 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             const Tick &tk = progs_[r].ticks[t];
             RankResources &rr = *res_[r];
             if (!tk.has_reduce) continue;
-            DDL_HIP(hipEventRecord(rr.comm_ev[t], rr.comm));
-            DDL_HIP(hipStreamWaitEvent(rr.compute, rr.comm_ev[t], 0));
-            launch_tick_reduce(tk, dtype, rr.compute);
-            DDL_HIP(hipEventRecord(rr.red_ev[t], rr.compute));
+            record(rr.comm_ev[t], comm(r));
+            wait(compute(r), rr.comm_ev[t]);
+            launch_tick_reduce(tk, dtype, compute(r));
+            record(rr.red_ev[t], compute(r));
         }
     }
     for (int r = 0; r < P_; ++r) {
-        DDL_HIP(hipEventRecord(res_[r]->join_ev, res_[r]->comm));
-        DDL_HIP(hipStreamWaitEvent(user, res_[r]->join_ev, 0));
+        record(res_[r]->join_ev, comm(r));
+        wait(user, res_[r]->join_ev);
     }
 }
 

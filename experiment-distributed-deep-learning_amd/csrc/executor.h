@@ -26,13 +26,23 @@ public:
     virtual void group(const std::vector<P2POp> &ops, hipStream_t stream) = 0;
     // Allgather of `bytes` per rank into recv (rank q's block at q * bytes) on `stream`.
     virtual void allgather(const GatherOp &g, hipStream_t stream) = 0;
+    // Whether group() / allgather() only enqueue stream work (so they can be captured into a
+    // hipGraph); a transport that synchronises the host cannot.
+    virtual bool capturable() const = 0;
 };
+
+// True while `s` is being captured into a hipGraph (hipStreamBeginCapture, torch.cuda.graph).
+// The engine then enqueues graph-safe work only: no allocation, no host synchronisation, no
+// autotuning — the calls that need those must run once outside the capture first (the same
+// warm-up rule as for any captured workload).
+bool stream_capturing(hipStream_t s);
 
 class RcclTransport : public Transport {
 public:
     explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
     void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
     void allgather(const GatherOp &g, hipStream_t stream) override;  // ncclAllGather
+    bool capturable() const override { return true; }
 
 private:
     ncclComm_t comm_;
@@ -59,6 +69,7 @@ public:
     void group(const std::vector<P2POp> &ops, hipStream_t stream) override;
     // own block copied on the device, the others as one group of sends / recvs
     void allgather(const GatherOp &g, hipStream_t stream) override;
+    bool capturable() const override { return false; }
     // One group of host-buffer operations straight to the callback (no device staging).
     void host_group(std::vector<ddl_p2p_op> &ops);
 
@@ -78,7 +89,8 @@ public:
     RankResources &operator=(const RankResources &) = delete;
 
     void ensure_events(size_t ticks);
-    void *ensure_staging(size_t bytes);
+    // Staging of at least `bytes`; growing it is refused while the caller's stream is captured.
+    void *ensure_staging(size_t bytes, bool capturing = false);
 
     int device;
     hipStream_t comm = nullptr, compute = nullptr;
@@ -114,7 +126,8 @@ public:
     KernelStats collect_stats();  // synchronises the recorded timing events, then resets
 
 private:
-    void run_(int dtype, hipStream_t user);  // posts prog_ on the streams, forked from / joined to user
+    // posts prog_ on the streams, forked from / joined to user (graph-safe when user is captured)
+    void run_(int dtype, hipStream_t user);
 
     int rank_, size_;
     std::unique_ptr<Transport> transport_;

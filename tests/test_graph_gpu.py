@@ -1,0 +1,149 @@
+"""The data plane inside hipGraphs (torch.cuda.graph = hipStreamBeginCapture on the caller's
+stream): one replay of a captured training step runs the engine's kernels and RCCL groups with no
+host work per call — the small-bucket lever the host launch rate sets.
+
+The engine is graph-safe by construction (executor.cpp `stream_capturing`): under capture it
+enqueues only stream work (fork / join of its comm and compute streams through events, kernels,
+RCCL groups), takes the size class's tuned schedule or the configured one without tuning, and
+refuses — loudly, before enqueueing anything — to grow its staging buffer or to capture a
+transport that synchronises the host. Warm up once outside the capture, as for any captured
+workload.
+
+Bar: every replay bit-exact vs the oracle on fresh inputs written into the captured buffers —
+MPICH's order (ddlo_fold_ref_order) for the allreduce over P virtual ranks whose moves go through
+a real RCCL communicator (ddl_rccl_loopback_*), the restatement of MPI_SUM for the reduce kernel."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import DT_DOUBLE, DT_FLOAT, DT_INT32, NAME, config, random_input
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def test_reduce_kernel_graph_replay(lib, oracle, gpu):
+    """K reduce launches captured into one graph; each replay on new data equals acc + in."""
+    n, K = 100_003, 6
+    s = torch.cuda.Stream()
+    accs = [torch.empty(n, device=gpu) for _ in range(K)]
+    ins = [torch.empty(n, device=gpu) for _ in range(K)]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        for a, b in zip(accs, ins):  # warm-up outside the capture
+            assert lib.ddl_reduce_local(a.data_ptr(), b.data_ptr(), n, DT_FLOAT, s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        for a, b in zip(accs, ins):
+            assert lib.ddl_reduce_local(a.data_ptr(), b.data_ptr(), n, DT_FLOAT, s.cuda_stream) == 0, \
+                lib.ddl_last_error()
+    for rep in range(3):
+        xa = [random_input(DT_FLOAT, n, 11 + rep * 100 + k) for k in range(K)]
+        xb = [random_input(DT_FLOAT, n, 12 + rep * 100 + k) for k in range(K)]
+        for k in range(K):
+            accs[k].copy_(_t(xa[k], gpu))
+            ins[k].copy_(_t(xb[k], gpu))
+        g.replay()
+        torch.cuda.synchronize()
+        for k in range(K):
+            assert accs[k].cpu().numpy().tobytes() == oracle.sum2(DT_FLOAT, xa[k], xb[k]).tobytes(), (rep, k)
+
+
+def test_world_allreduce_graph_replay(lib, gpu):
+    """The world communicator (one process: out = in) captured and replayed."""
+    from ddl.torch.communicator import Communicator
+    comm = Communicator.world()
+    n = 4097
+    s = torch.cuda.Stream()
+    a = torch.empty(n, device=gpu)
+    b = torch.empty(n, device=gpu)
+    with torch.cuda.stream(s):
+        assert lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), n, DT_FLOAT, 0, s.cuda_stream) == 0
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        assert lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), n, DT_FLOAT, 0, s.cuda_stream) == 0
+    for rep in range(2):
+        a.copy_(torch.randn(n, device=gpu))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+
+
+@pytest.fixture(scope='module')
+def loop(lib, gpu):
+    st = lib.ddl_rccl_loopback_init(0)
+    assert st == 0, lib.ddl_last_error()
+    yield lib
+    assert lib.ddl_rccl_loopback_finalize() == 0, lib.ddl_last_error()
+
+
+def _loop_allreduce(lib, ins, outs, n, dt, stream):
+    P = len(ins)
+    send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+    recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+    return lib.ddl_rccl_loopback_allreduce(P, send, recv, n, dt, stream)
+
+
+TORCH_DT = {DT_FLOAT: torch.float32, DT_DOUBLE: torch.float64, DT_INT32: torch.int32}
+
+
+@pytest.mark.parametrize('P', [3, 5, 8])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32], ids=lambda d: NAME[d])
+@pytest.mark.parametrize('algo', [1, 2, 3])
+def test_rccl_allreduce_graph_replay(loop, oracle, gpu, P, dt, algo):
+    """P virtual ranks' allreduce, moves through RCCL, captured once and replayed on fresh
+    inputs: every rank equals MPICH's order bit for bit on both sides of the 2048-byte switch,
+    out of place and in place."""
+    lib = loop
+    s = torch.cuda.Stream()
+    with config(lib, algo=algo, reference_order=1, tune=0, slice_bytes=64 << 10):
+        for n in (300, 70_001):
+            for in_place in (False, True):
+                ins = [torch.zeros(n, dtype=TORCH_DT[dt], device=gpu) for _ in range(P)]
+                outs = ins if in_place else [torch.empty_like(t) for t in ins]
+                with torch.cuda.stream(s):  # warm-up: sizes staging and events
+                    assert _loop_allreduce(lib, ins, outs, n, dt, s.cuda_stream) == 0, lib.ddl_last_error()
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    assert _loop_allreduce(lib, ins, outs, n, dt, s.cuda_stream) == 0, lib.ddl_last_error()
+                for rep in range(2):
+                    xs = [random_input(dt, n, 7 + 31 * rep + 7919 * r + n) for r in range(P)]
+                    for r in range(P):
+                        ins[r].copy_(_t(xs[r], gpu))
+                    g.replay()
+                    torch.cuda.synchronize()
+                    want = oracle.fold_ref_order(dt, xs).tobytes()
+                    for r in range(P):
+                        assert outs[r].cpu().numpy().tobytes() == want, (n, in_place, rep, r)
+                del g
+
+
+def test_capture_refuses_to_grow_staging(loop, gpu):
+    """A first call inside a capture would have to allocate staging: refused with a status and a
+    message, nothing enqueued, the capture still ends cleanly."""
+    lib = loop
+    P, n = 4, 3_000_001  # larger than every earlier call: the staging must grow
+    s = torch.cuda.Stream()
+    ins = [torch.zeros(n, device=gpu) for _ in range(P)]
+    outs = [torch.empty_like(t) for t in ins]
+    g = torch.cuda.CUDAGraph()
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=64 << 10):
+        small = [t[:10] for t in ins], [t[:10] for t in outs]
+        with torch.cuda.stream(s):  # the 4-rank world exists (streams, events) before the capture
+            assert _loop_allreduce(lib, small[0], small[1], 10, DT_FLOAT, s.cuda_stream) == 0
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            st = _loop_allreduce(lib, ins, outs, n, DT_FLOAT, s.cuda_stream)
+        assert st != 0
+        assert 'capture' in lib.ddl_last_error().decode()
+        # outside the capture the same call works
+        with torch.cuda.stream(s):
+            assert _loop_allreduce(lib, ins, outs, n, DT_FLOAT, s.cuda_stream) == 0, lib.ddl_last_error()
+        torch.cuda.synchronize()
