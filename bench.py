@@ -694,8 +694,9 @@ def multi_gpu(args):
             lib.ddl_set_config(b'reference_order', 0)
             try:
                 for algo, rings, slice_mib in ((0, 8, 2), (0, 1, 2), (0, 8, 1), (0, 8, 4), (0, 8, 8), (0, 3, 2),
-                                               (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64)):
-                    if algo == 1 and world < 3:
+                                               (0, 8, 64), (1, 1, 2), (1, 1, 8), (1, 1, 64), (4, 1, 2), (4, 1, 8),
+                                               (4, 1, 64)):
+                    if algo in (1, 4) and world < 3:
                         continue
                     lib.ddl_set_config(b'algo', algo)
                     lib.ddl_set_config(b'rings', rings)
@@ -840,7 +841,7 @@ def multi_gpu(args):
     dog.cancel()
 
 
-ALGO_NAMES = ('ring', 'direct', 'oneshot', 'gatherfold')  # schedule.h enum Algo
+ALGO_NAMES = ('ring', 'direct', 'oneshot', 'gatherfold', 'direct_gather')  # schedule.h enum Algo
 
 
 def algo_name(a):

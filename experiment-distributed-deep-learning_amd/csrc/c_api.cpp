@@ -299,9 +299,8 @@ int ddl_set_config(const char *key, long long value) {
         Config &c = config();
         if (k == "slice_bytes") c.slice_bytes = value;
         else if (k == "algo") {
-            DDL_REQUIRE(value == kAlgoRing || value == kAlgoDirect || value == kAlgoOneShot || value == kAlgoGatherFold,
-                        DDL_STATUS_INVALID_ARGUMENT,
-                        "algo must be 0 (ring), 1 (direct), 2 (one-shot) or 3 (gather-fold)");
+            DDL_REQUIRE(value >= kAlgoRing && value <= kAlgoDirectGather, DDL_STATUS_INVALID_ARGUMENT,
+                        "algo must be 0 (ring), 1 (direct), 2 (one-shot), 3 (gather-fold) or 4 (direct-gather)");
             c.algo = value;
         } else if (k == "rings") c.rings = value;
         else if (k == "max_slices") c.max_slices = value;
@@ -944,11 +943,13 @@ void dump_program(const RingProgram &prog, size_t es, long long *ops_out, size_t
             rows.insert(rows.end(), row, row + 8);
         }
         if (tk.gather.bytes) {
-            // {tick, 11, send buffer, send offset, recv buffer, recv offset, elements per rank, 0}
+            // {tick, 11, send buffer, send offset, recv buffer, recv offset, elements per rank,
+            //  the tick's reduce wait (-1: none)}
             long long sbuf, soff, rbuf, roff;
             decode(tk.gather.send, &sbuf, &soff);
             decode(tk.gather.recv, &rbuf, &roff);
-            long long row[8] = {(long long)t, 11, sbuf, soff, rbuf, roff, (long long)(tk.gather.bytes / es), 0};
+            long long row[8] = {(long long)t, 11, sbuf, soff, rbuf, roff, (long long)(tk.gather.bytes / es),
+                                tk.wait_reduce};
             rows.insert(rows.end(), row, row + 8);
         }
         for (const P2POp &op : tk.ops) {

@@ -140,6 +140,13 @@ std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &b
         add(kAlgoDirect, 1, 512u << 10, 16);
         add(kAlgoDirect, 1, 8u << 20, 8);
         add(kAlgoDirect, 1, 64u << 20, 8);
+        // the same reduce-scatter, the allgather as one ncclAllGather (RCCL's collective
+        // kernels instead of K groups of 2(P-1) p2p ops), where the chunks are equal
+        if (direct_gather_eligible(bytes, 1, P)) {
+            add(kAlgoDirectGather, 1, 2u << 20, 8);
+            add(kAlgoDirectGather, 1, 8u << 20, 8);
+            add(kAlgoDirectGather, 1, 64u << 20, 8);
+        }
     }
     // latency-bound buckets: one group (whole bucket to every peer) instead of two or more;
     // costs (P-1) x the bucket in wire bytes and staging, so only small buckets

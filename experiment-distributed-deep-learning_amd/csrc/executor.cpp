@@ -31,7 +31,8 @@ void RcclTransport::allgather(const GatherOp &g, hipStream_t stream) {
 
 void CallbackTransport::allgather(const GatherOp &g, hipStream_t stream) {
     char *recv = static_cast<char *>(g.recv);
-    DDL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * g.bytes, g.send, g.bytes, hipMemcpyDeviceToDevice, stream));
+    if (recv + (size_t)rank_ * g.bytes != g.send)  // in place: the own block is already there
+        DDL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * g.bytes, g.send, g.bytes, hipMemcpyDeviceToDevice, stream));
     std::vector<P2POp> ops;
     for (int d = 1; d < size_; ++d) {
         const int to = (rank_ + d) % size_, from = (rank_ + size_ - d) % size_;
@@ -370,6 +371,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                     const GatherOp &src = progs_[q].ticks[t].gather;
                     DDL_REQUIRE(src.bytes == g.bytes, DDL_STATUS_ERROR_UNKNOWN, "local world: allgather sizes differ");
                     char *dst = static_cast<char *>(g.recv) + (size_t)q * g.bytes;
+                    if (dst == src.send) continue;  // in place: rank q's own block
                     if (loop_) {
                         pairs.push_back(P2POp{true, 0, 0, const_cast<void *>(src.send), g.bytes});
                         pairs.push_back(P2POp{false, 0, 0, dst, g.bytes});

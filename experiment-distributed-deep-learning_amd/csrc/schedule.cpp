@@ -156,7 +156,7 @@ void ring_shape(size_t n, size_t esize, int P, const RingConfig &cfg_in, int *R,
         *staging_stride = gather_stride(n, esize);
         return;
     }
-    int r = cfg.algo == kAlgoDirect ? 1 : (int)rings_for(P, cfg.rings).size();
+    int r = is_direct(cfg.algo) ? 1 : (int)rings_for(P, cfg.rings).size();
     // Small buckets: fewer rings so every message stays >= 64 KiB (latency-bound regime).
     const size_t bytes = n * esize;
     while (r > 1 && bytes / ((size_t)r * (size_t)P) < (64u << 10)) --r;
@@ -288,7 +288,7 @@ namespace {
 // rank order (x_me = in) in MPICH's tree. AG tick k (waits the fold of slice k): send my
 // reduced slice to every peer, receive theirs straight into out.
 void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *outb, char *stb, size_t n,
-                  size_t es, int order, bool rank_order) {
+                  size_t es, int order, bool rank_order, bool collective_ag) {
     const int K = prog.K;
     const Range mine = chunk_range(n, es, P, 1, 0, rank);
     for (int k = 0; k < K; ++k) {
@@ -327,6 +327,17 @@ void build_direct(RingProgram &prog, int rank, int P, const char *inb, char *out
             });
         }
         prog.ticks.push_back(std::move(t));
+    }
+    if (collective_ag) {
+        // every chunk is n / P elements at q * n / P (direct_gather_eligible): one in-place
+        // allgather of the reduced chunks once the last fold has run (the compute stream is in
+        // order, so waiting for the last fold waits for all of them)
+        Tick t;
+        t.reduce.count = 0;
+        t.wait_reduce = K - 1;
+        t.gather = GatherOp{outb + mine.begin * es, outb, mine.size() * es};
+        prog.ticks.push_back(std::move(t));
+        return;
     }
     for (int k = 0; k < K; ++k) {
         Tick t;
@@ -435,9 +446,10 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
                          static_cast<char *>(staging), n, es, order);
         return;
     }
-    if (cfg.algo == kAlgoDirect) {
+    if (is_direct(cfg.algo)) {
         build_direct(prog, rank, P, static_cast<const char *>(in), static_cast<char *>(out),
-                     static_cast<char *>(staging), n, es, order, cfg.ref_order != 0);
+                     static_cast<char *>(staging), n, es, order, cfg.ref_order != 0,
+                     cfg.algo == kAlgoDirectGather && direct_gather_eligible(n, es, P));
         return;
     }
     const int R = prog.R, K = prog.K;

@@ -80,7 +80,19 @@ enum Algo : int {
     kAlgoGatherFold = 3, // small buckets: one ncclAllGather of the bucket (RCCL's low-latency
                          // collective path instead of 2(P-1) grouped p2p ops), then the same
                          // rank-order fold as one-shot
+    kAlgoDirectGather = 4, // the direct reduce-scatter (p2p ticks + rank-order folds), then ONE
+                           // in-place ncclAllGather of the reduced chunks instead of K p2p
+                           // allgather ticks; needs equal chunks (direct_gather_eligible), else
+                           // it runs as kAlgoDirect
 };
+
+// Direct-gather's allgather is one collective over equal, contiguous chunks: every chunk of
+// chunk_range(n, es, P, 1, 0, q) has n / P elements exactly when the bucket is a whole number of
+// P-granule groups.
+inline bool direct_gather_eligible(size_t n, size_t esize, int P) {
+    return P > 1 && n > 0 && (n * esize) % (kGranuleBytes * (size_t)P) == 0;
+}
+inline bool is_direct(int algo) { return algo == kAlgoDirect || algo == kAlgoDirectGather; }
 
 // Largest bucket the autotuner tries the one-shot schedule on.
 constexpr size_t kOneShotMaxBytes = 1u << 20;

@@ -149,7 +149,8 @@ int ddl_finalize(void);
 int ddl_is_initialized(void);
 
 /* Tunables: "algo" (0 multi-ring, 1 direct all-to-all, 2 one-shot, 3 gather-fold: one
- * ncclAllGather then the rank-order fold), "slice_bytes", "rings", "max_slices",
+ * ncclAllGather then the rank-order fold, 4 direct-gather: the direct reduce-scatter then one
+ * in-place ncclAllGather of the reduced chunks when they are equal), "slice_bytes", "rings", "max_slices",
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
  * "host_copy_threads" (memcpy workers of the keyed host staging),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack

@@ -260,8 +260,9 @@ def staging_size(progs, P=None):
                 st_size = max(st_size, int(row[5] + row[6]))
             elif row[1] == 4 and row[4] == 2:  # copy into staging
                 st_size = max(st_size, int(row[5] + row[6]))
-            elif row[1] == 11:  # gather: P blocks of row[6] elements into staging at row[5]
-                st_size = max(st_size, int(row[5] + P * row[6]))
+            elif row[1] == 11:  # gather: P blocks of row[6] elements into (row[4], row[5])
+                if row[4] == 2:
+                    st_size = max(st_size, int(row[5] + P * row[6]))
                 if row[2] == 2:  # sent from a (padded) staging slot
                     st_size = max(st_size, int(row[3] + row[6]))
             elif row[1] in (2, 3):

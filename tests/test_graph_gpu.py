@@ -95,7 +95,7 @@ TORCH_DT = {DT_FLOAT: torch.float32, DT_DOUBLE: torch.float64, DT_INT32: torch.i
 
 @pytest.mark.parametrize('P', [3, 5, 8])
 @pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32], ids=lambda d: NAME[d])
-@pytest.mark.parametrize('algo', [1, 2, 3])
+@pytest.mark.parametrize('algo', [1, 2, 3, 4])
 def test_rccl_allreduce_graph_replay(loop, oracle, gpu, P, dt, algo):
     """P virtual ranks' allreduce, moves through RCCL, captured once and replayed on fresh
     inputs: every rank equals MPICH's order bit for bit on both sides of the 2048-byte switch,
@@ -103,7 +103,7 @@ def test_rccl_allreduce_graph_replay(loop, oracle, gpu, P, dt, algo):
     lib = loop
     s = torch.cuda.Stream()
     with config(lib, algo=algo, reference_order=1, tune=0, slice_bytes=64 << 10):
-        for n in (300, 70_001):
+        for n in (300, 70_001, 128 * 840):  # 128 * 840: equal chunks (direct-gather's allgather)
             for in_place in (False, True):
                 ins = [torch.zeros(n, dtype=TORCH_DT[dt], device=gpu) for _ in range(P)]
                 outs = ins if in_place else [torch.empty_like(t) for t in ins]

@@ -98,9 +98,9 @@ def test_ring_program_over_gloo(world, dt, n, algo):
     _run_ring_workers(world, dt, n, algo, 0)
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2, 3])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3, 4])
 @pytest.mark.parametrize('world', [2, 3])
-@pytest.mark.parametrize('dt,n', [(1, 50_000), (1, 300), (2, 4099)])
+@pytest.mark.parametrize('dt,n', [(1, 50_000), (1, 300), (2, 4099), (1, 128 * 840)])
 def test_reference_order_program_over_gloo(world, dt, n, algo):
     """reference_order 1 (the default): every rank ends with MPICH's own order (binomial tree at
     <= 2048 bytes, the pre-fold + pairwise tree above), whichever schedule is asked for."""

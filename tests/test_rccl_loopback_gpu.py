@@ -53,14 +53,14 @@ def _pairs(lib, P):
 
 @pytest.mark.parametrize('P', [3, 5, 8])
 @pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32], ids=lambda d: NAME[d])
-@pytest.mark.parametrize('algo', [0, 1, 2, 3])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3, 4])
 def test_rccl_loopback_reference_order(loop, oracle, gpu, P, dt, algo):
     """Default reference order over the RCCL transport: every rank equals MPICH's order bit for
     bit, for messages up to 2048 bytes (binomial tree) and above (pre-fold + pairwise tree)."""
     lib = loop
     before = _pairs(lib, P)
     with config(lib, algo=algo, reference_order=1, tune=0, slice_bytes=64 << 10):
-        for n in (1, 300, 4099, 300_001):
+        for n in (1, 300, 4099, 300_001, 128 * 840):  # the last: equal chunks (direct-gather)
             xs = [random_input(dt, n, 17 * algo + 1234 + 7919 * r + n) for r in range(P)]
             want = oracle.fold_ref_order(dt, xs)
             for in_place in (False, True):

@@ -116,14 +116,15 @@ def test_reference_order_equals_mpich_golden_bit_for_bit(lib, gpu, algo):
                 assert o.tobytes() == y.tobytes(), case
 
 
-@pytest.mark.parametrize('algo', [1, 2, 3])
+@pytest.mark.parametrize('algo', [1, 2, 3, 4])
 @pytest.mark.parametrize('P', [3, 5, 6, 7, 8])
 @pytest.mark.parametrize('dt', [1, 2, 3], ids=lambda d: NAME[d])
-@pytest.mark.parametrize('n', [1, 300, 512, 513, 65_537, 1_000_003])
+@pytest.mark.parametrize('n', [1, 300, 512, 513, 65_537, 1_000_003, 128 * 840])
 @pytest.mark.parametrize('in_place', [False, True])
 def test_reference_order_matches_oracle(lib, oracle, gpu, algo, P, dt, n, in_place):
     """The ordered fold kernels (binomial, pre-fold + pairwise tree) through the direct and
-    one-shot programs vs the oracle's MPICH-order restatement, in and out of place, ragged."""
+    one-shot programs vs the oracle's MPICH-order restatement, in and out of place, ragged
+    (128 * 840 elements: equal chunks at every P here, so direct-gather's collective allgather)."""
     xs = [random_input(dt, n, 61 + 5 * r) for r in range(P)]
     with config(lib, algo=algo, reference_order=1, slice_bytes=256 << 10):
         outs = run_local(lib, gpu, xs, in_place=in_place)

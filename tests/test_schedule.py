@@ -114,9 +114,9 @@ def _overlap(a0, a1, b0, b1):
     return a0 < b1 and b0 < a1
 
 
-@pytest.mark.parametrize('algo,ref_order', [(0, 0), (1, 0), (2, 0), (1, 1), (2, 1)])
+@pytest.mark.parametrize('algo,ref_order', [(0, 0), (1, 0), (2, 0), (1, 1), (2, 1), (4, 0), (4, 1)])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 7, 8, 17, 33])
-@pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5])
+@pytest.mark.parametrize('n', [777, 40_961, 1_000_003, (256 << 20) // 4 + 4096 * 3 + 5, 64 * 33 * 8 * 64])
 @pytest.mark.parametrize('slice_bytes', [64 << 10, 2 << 20])
 def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
     """Comm tick T runs after the reduce it waits on (W) and every earlier reduce (the compute
@@ -133,6 +133,14 @@ def test_schedule_has_no_stream_races(lib, algo, ref_order, P, n, slice_bytes):
                 t_, kind_, _, _, sb, so, c_, oo = row
                 ob = GENERAL_FOLDS[int(kind_)][1]  # 1: the output buffer, 2: a staging partial
                 red.setdefault(int(t_), []).append(('gen', int(sb), int(so), int(c_), int(oo), ob))
+            # an allgather (kind 11, direct-gather) as the send of its block and the receive of
+            # all P blocks, with the tick's reduce wait
+            gathers = []
+            for g in prog[prog[:, 1] == 11]:
+                t_, _, sb, so, rb, ro, c_, w_ = g
+                gathers += [[t_, 0, -1, -1, sb, so, c_, w_], [t_, 1, -1, -1, rb, ro, P * c_, w_]]
+            if gathers:
+                prog = np.concatenate([prog, np.array(gathers, dtype=prog.dtype)])
             w_eff = -1  # the comm stream is in order: a tick inherits every earlier tick's wait
             for t in sorted(set(prog[:, 0].tolist())):
                 ops = prog[(prog[:, 0] == t) & (prog[:, 1] <= 1)]
@@ -304,9 +312,9 @@ def test_oneshot_program_shape(lib):
 
 
 # ---- reference order (reference_order = 1, the default) ----------------------------------------
-@pytest.mark.parametrize('algo', [0, 1, 2, 3])
+@pytest.mark.parametrize('algo', [0, 1, 2, 3, 4])
 @pytest.mark.parametrize('P', [2, 3, 4, 5, 6, 7, 8])
-@pytest.mark.parametrize('n', [1, 100, 512, 513, 4099, 50_000])
+@pytest.mark.parametrize('n', [1, 100, 512, 513, 4099, 50_000, 128 * 840])
 @pytest.mark.parametrize('dt', ALL_DTYPES)
 def test_reference_order_programs_compute_mpich_order(lib, oracle, algo, P, n, dt):
     """With reference_order every schedule's programs, executed with matched sends/recvs, give
@@ -321,6 +329,30 @@ def test_reference_order_programs_compute_mpich_order(lib, oracle, algo, P, n, d
     want = oracle.fold_ref_order(dt, xs)
     for r in range(P):
         assert outs[r].tobytes() == want.tobytes(), f'rank {r}'
+
+
+@pytest.mark.parametrize('P', [2, 3, 5, 8])
+def test_direct_gather_program_shape(lib, P):
+    """Direct-gather (algo 4): the direct reduce-scatter ticks, then ONE in-place allgather of the
+    reduced chunks (kind 11, send = out at rank * n / P, recv = out, n / P per rank) waiting for
+    the last fold — where the chunks are equal; elsewhere the direct program itself."""
+    n = 128 * 840  # fp32: 430080 B = 1680 granules, a multiple of every P here
+    with config(lib, algo=1, reference_order=1, slice_bytes=64 << 10):
+        direct = [ring_program(lib, r, P, n, DT_FLOAT) for r in range(P)]
+        ragged = [ring_program(lib, r, P, n + 64, DT_FLOAT) for r in range(P)]
+    with config(lib, algo=4, reference_order=1, slice_bytes=64 << 10):
+        progs = [ring_program(lib, r, P, n, DT_FLOAT) for r in range(P)]
+        ragged4 = [ring_program(lib, r, P, n + 64, DT_FLOAT) for r in range(P)]
+    for r in range(P):
+        g = progs[r][progs[r][:, 1] == 11]
+        assert len(g) == 1
+        t, _, sb, so, rb, ro, cnt, wait = g[0]
+        assert (sb, so, rb, ro, cnt) == (1, r * n // P, 1, 0, n // P)
+        assert t == progs[r][:, 0].max() and not ((progs[r][:, 0] == t) & (progs[r][:, 1] <= 1)).any()
+        rs = direct[r][direct[r][:, 0] < t]
+        assert np.array_equal(progs[r][progs[r][:, 0] < t], rs)  # the same reduce-scatter
+        assert wait == rs[rs[:, 1] <= 1][:, 0].max()  # the last reduce-scatter tick's fold
+        assert np.array_equal(ragged4[r], ragged[r])  # unequal chunks: the direct program
 
 
 def test_reference_order_program_kinds(lib):
