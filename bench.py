@@ -603,14 +603,14 @@ def multi_gpu(args):
     # the autotuner's record for this bucket (tuned during the first warmup call)
     tune = None
     chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
-    cfgs = (ctypes.c_longlong * 64)()
-    tms = (ctypes.c_float * 16)()
-    check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
+    cfgs = (ctypes.c_longlong * 128)()
+    tms = (ctypes.c_float * 32)()
+    check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 32),
           'ddl_tune_result')
     if chosen.value >= 0:
         cands = [{'algo': algo_name(cfgs[4 * i]), 'rings': cfgs[4 * i + 1],
                   'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
-                  'ms': round(tms[i], 4)} for i in range(min(count.value, 16))]
+                  'ms': round(tms[i], 4)} for i in range(min(count.value, 32))]
         tune = {'chosen': cands[chosen.value], 'candidates': cands}
     # correctness spot check: every rank's sum must match (checksum of checksums)
     step(0)
@@ -781,7 +781,7 @@ def multi_gpu(args):
                 t_ours = timed_fn(lambda: one(0), reps, 3)
                 t_rccl = t_ours if args.rehearse else timed_fn(lambda: one(1), reps, 3)
                 chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
-                check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 16),
+                check(lib.ddl_tune_result(comm.id, sz, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 32),
                       'ddl_tune_result')
                 pick = None
                 if chosen.value >= 0:

@@ -152,8 +152,9 @@ def test_reference_order_misaligned_fold(lib, oracle, gpu):
 
 @pytest.mark.parametrize('P', [4, 8])
 def test_reference_order_tuner_times_only_exact_schedules(lib, gpu, P):
-    """With reference_order the autotuner's candidates are direct / one-shot / gather-fold
-    schedules only at P > 2 (the configured ring becomes direct), deduplicated."""
+    """With reference_order the autotuner's candidates are direct / one-shot / gather-fold /
+    direct-gather schedules only at P > 2 (the configured ring becomes direct), deduplicated;
+    direct-gather only where the chunks are equal (64 KiB at P = 4, 8: yes; 64 KiB + 256 B: no)."""
     chosen, count = ctypes.c_int(), ctypes.c_int()
     cfgs = (ctypes.c_longlong * 64)()
     ms = (ctypes.c_float * 16)()
@@ -162,8 +163,13 @@ def test_reference_order_tuner_times_only_exact_schedules(lib, gpu, P):
                                 ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
     assert st == 0, lib.ddl_last_error()
     c = [tuple(cfgs[4 * i:4 * i + 4]) for i in range(count.value)]
-    assert {x[0] for x in c} == {1, 2, 3} and len(set(c)) == len(c)
+    assert {x[0] for x in c} == {1, 2, 3, 4} and len(set(c)) == len(c)
     assert c[0][0] == 1
+    with config(lib, reference_order=1, algo=0):
+        st = lib.ddl_local_tune(P, (64 << 10) + 64, DT_FLOAT, torch.cuda.current_stream().cuda_stream,
+                                ctypes.byref(chosen), ctypes.byref(count), cfgs, ms, 16)
+    assert st == 0, lib.ddl_last_error()
+    assert {cfgs[4 * i] for i in range(count.value)} == {1, 2, 3}
 
 
 @pytest.mark.parametrize('P', [2, 4, 8])
@@ -281,10 +287,11 @@ def test_reduce_sumN_kernel_all_input_counts(lib, oracle, gpu):
         assert outs[0].tobytes() == want.tobytes(), P
 
 
-@pytest.mark.parametrize('P,ncand', [(2, 4), (4, 9), (8, 9)])
+@pytest.mark.parametrize('P,ncand', [(2, 4), (4, 12), (8, 12)])
 def test_local_autotune_candidates(lib, gpu, P, ncand):
     """The autotuner's procedure on P virtual ranks: the configured schedule is candidate 0,
-    every candidate is timed, the chosen one is the fastest."""
+    every candidate is timed, the chosen one is the fastest (4 MiB: equal chunks at P = 4, 8, so
+    the direct-gather candidates too)."""
     chosen, count = ctypes.c_int(), ctypes.c_int()
     cfgs = (ctypes.c_longlong * 64)()
     ms = (ctypes.c_float * 16)()
@@ -298,7 +305,7 @@ def test_local_autotune_candidates(lib, gpu, P, ncand):
     assert all(t > 0 for t in times)
     assert times[chosen.value] == min(times)
     algos = {cfgs[4 * i] for i in range(count.value)}
-    assert algos == ({0, 1} if P > 2 else {0})
+    assert algos == ({0, 1, 4} if P > 2 else {0})
 
 
 # ---- one-shot schedule: algo = 2 --------------------------------------------------------------
