@@ -1,0 +1,40 @@
+"""Pinned-chunk size of the host-resident paths (measurement tool, not shipped).
+For each `host_chunk_bytes` — interleaved over rounds — times ddl_allreduce_host on a pinned
+256 MiB fp32 bucket (bench.host_resident_rate) and the C5 set as pageable host tensors through
+the keyed path (bench.keyed_host_c5), one rank, data plane forced. One JSON line per point:
+    python tools/host_chunk_tune.py [rounds] [MiB,MiB,...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    mibs = [int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [4, 8, 16, 32, 64]
+    import torch
+    import bench
+    from ddl.torch.communicator import Communicator
+    from ddl.torch.cpp_backend import CPPBackend, check
+    torch.cuda.set_device(0)
+    lib = CPPBackend.c_api()
+    comm = Communicator.world()
+    default = lib.ddl_get_config(b'host_chunk_bytes')
+    try:
+        for r in range(rounds):
+            for m in mibs:
+                check(lib.ddl_set_config(b'host_chunk_bytes', m << 20), 'ddl_set_config')
+                hr = bench.host_resident_rate(lib, comm, 256 << 20, reps=10)
+                kc = bench.keyed_host_c5(lib, comm, steps=3)
+                print(json.dumps({'round': r, 'host_chunk_MiB': m, 'host_resident_ms': hr['ms'],
+                                  'host_resident_GiBs': hr['bucket_GiBs'], 'keyed_host_c5_ms': kc['ms'],
+                                  'keyed_host_c5_GiBs': kc['bucket_GiBs']}), flush=True)
+    finally:
+        lib.ddl_set_config(b'host_chunk_bytes', default)
+
+
+if __name__ == '__main__':
+    main()
