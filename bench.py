@@ -61,7 +61,8 @@ def parse():
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=6.0)
     ap.add_argument('--variant', type=int, default=-1,
-                    help='reduce kernel variant bits (-1 default; 1 nt-load a, 2 nt-load b, 4 nt-store, 8 lds b)')
+                    help='reduce kernel variant bits (-1 default; 1 nt-load a, 2 nt-load b, 4 nt-store, 8 lds b, '
+                         '16 write-through store)')
     return ap.parse_args()
 
 
@@ -155,7 +156,7 @@ def cpu_reference_path():
 NSETS = 3  # rotating buffer sets: >= 2 x 768 MiB of traffic between reuses of one set, so the
            # 256 MiB Infinity Cache cannot serve a re-read (MI355X_MICROARCH.md §Infinity Cache)
 VARIANTS = {'default': -1, 'plain': 0, 'nt_load_a': 1, 'nt_load_ab': 3, 'nt_all': 7, 'lds_stage_b': 8,
-            'lds_stage_b_nt_a': 9}
+            'lds_stage_b_nt_a': 9, 'wt_store': 16, 'nt_load_ab_wt_store': 19}
 
 
 GRAPH_SWEEP_MAX = 8 << 20  # sweep points also timed as hipGraph replays (launch-bound sizes)

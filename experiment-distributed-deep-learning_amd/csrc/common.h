@@ -137,7 +137,8 @@ enum ReduceVariant : int {
     kNtLoadB = 2,   // non-temporal loads of operand b (the received chunk)
     kNtStore = 4,   // non-temporal stores of out
     kLdsStageB = 8, // operand b staged through LDS by global_load_lds_dwordx4
-    kVariantMask = 15,
+    kWtStore = 16,  // write-through stores of out (sc0 sc1: the line leaves the XCD's L2)
+    kVariantMask = 31,
 };
 int default_variant(size_t bytes);  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2), by bucket size
 int ring_variant();     // reduce-scatter step of the ring

@@ -5,17 +5,21 @@
 // Memory-bound vector add: no MFMA. Algorithmic HBM bytes per element = 3 * sizeof(T)
 // (two reads, one write).
 //
-// Layout / mapping (measured in profiles/r01/reduce_tune_*.txt):
-//   * one workgroup = 256 lanes = one 4 KiB tile of each operand: lane l moves bytes
-//     [16l, 16l+16) of the tile with one global_load_dwordx4 per operand and one
-//     global_store_dwordx4. The grid has one workgroup per tile (no grid-stride loop): the
-//     dispatcher hands out workgroups in order, so the tiles in flight form one compact
-//     address window and every HBM page opened is drained by neighbouring workgroups.
-//     This measured 5.9-6.1 TB/s vs 4.6 for an 8-workgroups-per-CU grid-stride loop.
+// Layout / mapping (measured in profiles/r01/reduce_tune_*.txt and
+// profiles/r02/reduce_policy/):
+//   * one workgroup = 128 lanes = one 2 KiB tile of each operand (DDL_REDUCE_THREADS): lane l
+//     moves bytes [16l, 16l+16) of the tile with one buffer_load_dwordx4 per operand and one
+//     buffer_store_dwordx4 (one descriptor per operand tile). The grid has one workgroup per
+//     tile (no grid-stride loop): the dispatcher hands out workgroups in order, so the tiles in
+//     flight form one compact address window and every HBM page opened is drained by
+//     neighbouring workgroups. This measured 5.9-6.1 TB/s vs 4.6 for an 8-workgroups-per-CU
+//     grid-stride loop.
 //   * up to kMaxSegments independent (out, a, b, n) problems per launch (one per ring):
 //     blockIdx.y = segment, workgroups past a segment's last tile exit at once.
-//   * cache policy per operand: non-temporal loads of the once-read operands keep the
-//     256 MiB Infinity Cache for data that is re-read (kNtLoad*, measured +4% at 1 GiB).
+//   * cache bits per access (default_variant by bucket size): non-temporal loads of the
+//     once-read operands, and write-through (sc0 sc1) stores of out below 256 MiB — the line
+//     leaves the XCD's L2 at once instead of waiting there to be written back (+3-14 % at
+//     32-128 MiB); non-temporal stores from 256 MiB.
 //   * the n mod V tail (V = elements per 16 B) is done by the lanes of the last tile, one
 //     element each: no epilogue launch. Misaligned buffers take a scalar grid-stride kernel.
 //   * fp16 adds with v_pk_add_f16 (IEEE, round-to-nearest-even, denormals kept) — identical to
@@ -113,7 +117,15 @@ __device__ __forceinline__ u32x4 load_v(const u32x4 *p) {
     else return *p;
 }
 
-// out = a + b, one 4 KiB tile per workgroup. out may alias a or b (no __restrict__): each lane
+// gfx950 buffer-access cache bits (the aux operand of the raw buffer builtins) and the third
+// descriptor dword of a raw 32-bit buffer
+constexpr int kAuxSc0 = 1, kAuxNt = 2, kAuxSc1 = 16;
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr int store_aux(int variant) {
+    return ((variant & kNtStore) ? kAuxNt : 0) | ((variant & kWtStore) ? (kAuxSc0 | kAuxSc1) : 0);
+}
+
+// out = a + b, one tile per workgroup. out may alias a or b (no __restrict__): each lane
 // reads its own 16 bytes of a and b before it writes the same 16 bytes of out.
 template <int DT, int VARIANT, int THREADS>
 __global__ void __launch_bounds__(THREADS) k_sum2_tile(SegTable t) {
@@ -145,12 +157,19 @@ __global__ void __launch_bounds__(THREADS) k_sum2_tile(SegTable t) {
             else o[i] = r;
         }
     } else {
-        if (i < nv) {
-            const u32x4 x = load_v<(VARIANT & kNtLoadA) != 0>(a + i);
-            const u32x4 y = load_v<(VARIANT & kNtLoadB) != 0>(b + i);
-            const u32x4 r = A::vec(x, y);
-            if constexpr ((VARIANT & kNtStore) != 0) __builtin_nontemporal_store(r, o + i);
-            else o[i] = r;
+        // raw buffer accesses, one descriptor per operand tile: the aux word carries the cache
+        // bits per access (nt / sc0 sc1 write-through), lanes past the tile's last vector read 0
+        // and drop their store (num_records), and each lane's address is a 32-bit offset
+        const uint64_t base = tile * kTileVec;
+        if (base < nv) {
+            const int bytes = (int)((nv - base < kTileVec ? nv - base : kTileVec) * 16);
+            const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(a + base), 0, bytes, kRsrcWord3);
+            const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(b + base), 0, bytes, kRsrcWord3);
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc(o + base, 0, bytes, kRsrcWord3);
+            const int off = (int)threadIdx.x * 16;
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, (VARIANT & kNtLoadA) ? kAuxNt : 0);
+            const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, (VARIANT & kNtLoadB) ? kAuxNt : 0);
+            __builtin_amdgcn_raw_buffer_store_b128(A::vec(x, y), ro, off, 0, store_aux(VARIANT));
         }
     }
     // tail: the n mod V elements past the last full vector, one per lane of the tile holding nv
@@ -471,12 +490,16 @@ void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) {
     DDL_HIP(hipGetLastError());
 }
 
-// Standalone reduce (acc += in over whole buckets) of `bytes` per operand. Large buckets stream
-// through once, so all accesses are non-temporal (measured 6.47 TB/s vs 5.75 plain, 256 MiB
-// fp32, rotating buffers; 6.41 vs 5.92 at 64 MiB). Below kNtMinBytes plain accesses win (16 MiB:
-// 5.83 vs 5.62 TB/s; 1-4 MiB: 0.2-0.4 us less per launch; tools/small_sweep.py) — the operands
-// of a small bucket are likely still in the Infinity Cache from whoever produced them.
-constexpr size_t kNtMinBytes = 32u << 20;
+// Standalone reduce (acc += in over whole buckets) of `bytes` per operand, by bucket size
+// (3 rotating buffer sets per size, profiles/r02/reduce_policy/):
+//   * from 256 MiB every access is non-temporal: the bucket streams through once (6.8 TB/s at
+//     256 MiB; write-through stores 0.5-0.8 % slower there);
+//   * 32-256 MiB: non-temporal loads, write-through stores (64 MiB: 7.5 vs 6.6 TB/s all-nt;
+//     128 MiB: 6.9 vs 6.7);
+//   * below 32 MiB: plain loads — the operands of a small bucket are likely still in the
+//     Infinity Cache from whoever produced them — and write-through stores (16 MiB: 6.7 vs 6.4
+//     TB/s plain stores).
+constexpr size_t kNtMinBytes = 32u << 20, kNtStoreMinBytes = 256u << 20;
 int default_variant(size_t bytes) {
     static int v = [] {
         const char *e = std::getenv("DDL_REDUCE_VARIANT");
@@ -484,7 +507,9 @@ int default_variant(size_t bytes) {
         return (x >= 0 && x <= kVariantMask) ? x : -1;
     }();
     if (v >= 0) return v;
-    return bytes >= kNtMinBytes ? (kNtLoadA | kNtLoadB | kNtStore) : 0;
+    if (bytes >= kNtStoreMinBytes) return kNtLoadA | kNtLoadB | kNtStore;
+    if (bytes >= kNtMinBytes) return kNtLoadA | kNtLoadB | kWtStore;
+    return kWtStore;
 }
 
 // Ring reduce-scatter step: a = the rank's own gradient (read once: non-temporal), b = the slice

@@ -281,7 +281,8 @@ int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, in
                     void *hip_stream);
 /* Kernel variant selection for measurement (bit set; -1 = the engine's default):
  * 1 = non-temporal loads of a, 2 = non-temporal loads of b, 4 = non-temporal stores,
- * 8 = operand b staged through LDS by global_load_lds_dwordx4. */
+ * 8 = operand b staged through LDS by global_load_lds_dwordx4, 16 = write-through (sc0 sc1)
+ * stores of out (ignored with 8). */
 int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b,
                             size_t elements, int dtype, void *hip_stream);
 /* The direct schedule's fold: out[i] = a[i] + ins[0][i] + ... + ins[nb-1][i], 1 <= nb <= 15,

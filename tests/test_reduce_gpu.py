@@ -43,7 +43,7 @@ def test_reduce_local_in_place(lib, oracle, gpu, dt):
     assert from_dev(ta, a).tobytes() == oracle.sum2(dt, a, b).tobytes()
 
 
-@pytest.mark.parametrize('variant', [-1, 0, 1, 2, 3, 4, 7, 8, 9, 15])
+@pytest.mark.parametrize('variant', [-1, 0, 1, 2, 3, 4, 7, 8, 9, 15, 16, 19, 23, 24, 31])
 @pytest.mark.parametrize('dt', [DT_FLOAT, DT_HALF, DT_BFLOAT16, 3, 2], ids=lambda d: str(d))
 def test_variants_agree(lib, oracle, gpu, variant, dt):
     n = (1 << 20) + 77
