@@ -26,6 +26,7 @@
     } while (0)
 
 using f4 = float __attribute__((ext_vector_type(4)));
+using u4 = unsigned int __attribute__((ext_vector_type(4)));
 constexpr int K = 8;  // inputs (P = 8: own + 7 received)
 
 struct Ins {
@@ -38,8 +39,8 @@ __device__ __forceinline__ f4 ld(const f4 *p) {
     else return *p;
 }
 
-// POL bit 0: non-temporal loads, bit 1: non-temporal store. ILV: 0 = lane-contiguous vectors
-// (vector u of lane l at u*T + l), the loads of every input issued before the first add.
+// POL bit 0: non-temporal loads, bit 1: non-temporal store, bit 2: write-through store. Vector u
+// of lane l at u*T + l; the loads of every input issued before the first add.
 template <int T, int U, int POL>
 __global__ void __launch_bounds__(T) k_fold(f4 *o, Ins in, size_t nv) {
     const size_t base = (size_t)blockIdx.x * T * U + threadIdx.x;
@@ -58,8 +59,16 @@ __global__ void __launch_bounds__(T) k_fold(f4 *o, Ins in, size_t nv) {
         f4 s = r[0][u];
 #pragma unroll
         for (int k = 1; k < K; ++k) s += r[k][u];
-        if constexpr ((POL & 2) != 0) __builtin_nontemporal_store(s, o + i);
-        else o[i] = s;
+        if constexpr ((POL & 4) != 0) {  // write-through (sc0 sc1) raw buffer store
+            // one descriptor per workgroup (a per-lane base would make hipcc loop over lanes)
+            const size_t wg = (size_t)blockIdx.x * T * U;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(o + wg, 0, 0x7fffffff, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, s), rs, (int)((i - wg) * 16), 0, 17);
+        } else if constexpr ((POL & 2) != 0) {
+            __builtin_nontemporal_store(s, o + i);
+        } else {
+            o[i] = s;
+        }
     }
 }
 
@@ -120,6 +129,8 @@ int main(int argc, char **argv) {
         make<128, 4, 3>(""),
         make<256, 4, 1>("NT loads"),
         make<128, 2, 1>("NT loads"),
+        make<128, 1, 5>("NT loads, write-through store"),
+        make<128, 1, 4>("plain loads, write-through store"),
         Variant{"fold_serial T128 pol3",
                 [](f4 *o, Ins in, size_t nv, hipStream_t st) {
                     hipLaunchKernelGGL((k_fold_serial<128, 3>), dim3((unsigned)((nv + 127) / 128)), dim3(128), 0, st, o,
