@@ -305,6 +305,7 @@ def single_gpu(args):
         out['fusion_c5'] = fusion_c5(lib, Communicator.world(), dev, steps=5, forced=not args.no_forced_data_plane)
         if not args.no_host:
             out['keyed_host_c5'] = keyed_host_c5(lib, Communicator.world(), steps=3)
+            out['keyed_host_c5_pinned'] = keyed_host_c5(lib, Communicator.world(), steps=3, pinned=True)
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline()
         out['cpu_reduce_op_port'] = cpu_reduce_port(64 << 20, args.cpu_seconds)
@@ -455,12 +456,14 @@ def fusion_c5(lib, comm, dev, steps, k=4096, forced=True):
     return res
 
 
-def keyed_host_c5(lib, comm, steps, k=4096):
+def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
-    buffers) through the keyed path: negotiation, dtype groups, plans, then per plan pinned-chunk
-    staging — host pack -> H2D -> allreduce -> D2H -> host unpack (ddl_allreduce_submit_batch_mem,
-    DDL_MEMORY_HOST). At one rank the data plane is forced (one_rank_shortcut = 0). The rate is
-    PCIe-bound (2 x bytes cross the host link); it is never `value`."""
+    buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks —
+    pageable tensors: pinned-slot staging, host pack -> H2D -> allreduce -> D2H -> host unpack;
+    pinned tensors (`pinned`): zero copy, the pack / unpack kernels read and write the tensors
+    over PCIe (ddl_allreduce_submit_batch_mem, DDL_MEMORY_HOST). At one rank the data plane is
+    forced (one_rank_shortcut = 0). The rate is PCIe-bound (2 x bytes cross the host link); it is
+    never `value`."""
     import numpy as np
     import torch
     from ddl.torch.cpp_backend import DONE_FN, MEMORY_HOST, check
@@ -471,9 +474,10 @@ def keyed_host_c5(lib, comm, steps, k=4096):
     for i in order:
         half = rng.random() < 0.5
         n = int(sizes[i]) // (2 if half else 4)
-        tensors.append(torch.randn(n).to(torch.float16 if half else torch.float32))
+        t = torch.randn(n).to(torch.float16 if half else torch.float32)
+        tensors.append(t.pin_memory() if pinned else t)
         dts.append(19 if half else 1)
-        keys.append(f'hgrad_{i:05d}'.encode())
+        keys.append(f'{"p" if pinned else "h"}grad_{i:05d}'.encode())
     total = sum(t.numel() * t.element_size() for t in tensors)
     K, V = ctypes.c_char_p * k, ctypes.c_void_p * k
     ptrs = V(*[t.data_ptr() for t in tensors])
@@ -487,17 +491,22 @@ def keyed_host_c5(lib, comm, steps, k=4096):
             check(lib.ddl_allreduce_submit_batch_mem(comm.id, *args), 'ddl_allreduce_submit_batch_mem')
             check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
         step()
+        plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         dt = (time.perf_counter() - t0) / steps
+        zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
     finally:
         lib.ddl_set_config(b'one_rank_shortcut', old)
+    path = ('pinned host tensors -> keyed batch -> negotiation -> plans -> chunks: pack kernel reads the tensors '
+            'over PCIe, allreduce, unpack kernel writes them back (zero copy), in place' if pinned else
+            'pageable host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
+            'allreduce, D2H, host unpack), in place')
     return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3), 'bucket_GiBs': round(total / GiB / dt, 2),
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
-            'path': 'pageable host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
-                    'allreduce, D2H, host unpack), in place'}
+            'zero_copy_plans_per_step': zero_copy_plans / steps, 'path': path}
 
 
 def host_resident_rate(lib, comm, S, reps):

@@ -315,7 +315,8 @@ int ddl_set_config(const char *key, long long value) {
         } else if (k == "host_copy_threads") {
             DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
             c.host_copy_threads = value;
-        } else if (k == "tune") c.tune = value ? 1 : 0;
+        } else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
+        else if (k == "tune") c.tune = value ? 1 : 0;
         else if (k == "fusion_pipeline_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
             c.fusion_pipeline_bytes = value;
@@ -340,6 +341,8 @@ long long ddl_get_config(const char *key) {
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
     if (k == "tune") return c.tune;
     if (k == "host_copy_threads") return c.host_copy_threads;
+    if (k == "host_zero_copy") return c.host_zero_copy;
+    if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "reference_order") return c.reference_order;

@@ -584,31 +584,69 @@ void plan_slice(const Plan &p, size_t q, size_t n, size_t *b, size_t *e) {
 
 void RequestHandler::host_pieces_(const std::vector<HostSeg> &segs, const std::vector<size_t> &starts, size_t off,
                                   size_t len, char *pinned, bool pack, std::vector<CopyPool::Piece> &out) {
-    size_t i = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
-    size_t pos = off;
+    // segment i holds [starts[i], starts[i] + bytes) of the staged stream (padding between
+    // segments is neither packed nor unpacked)
     const size_t end = off + len;
-    for (; pos < end && i < segs.size(); ++i) {
-        const size_t so = pos - starts[i];
-        if (so >= segs[i].bytes) continue;  // empty segment
-        const size_t n = std::min(segs[i].bytes - so, end - pos);
-        if (pack) out.push_back(CopyPool::Piece{pinned + (pos - off), segs[i].src + so, n});
-        else out.push_back(CopyPool::Piece{segs[i].dst + so, pinned + (pos - off), n});
-        pos += n;
+    for (size_t i = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+         i < segs.size() && starts[i] < end; ++i) {
+        const size_t lo = std::max(off, starts[i]), hi = std::min(end, starts[i] + segs[i].bytes);
+        if (hi <= lo) continue;  // empty segment, or `off` past its data
+        if (pack) out.push_back(CopyPool::Piece{pinned + (lo - off), segs[i].src + (lo - starts[i]), hi - lo});
+        else out.push_back(CopyPool::Piece{segs[i].dst + (lo - starts[i]), pinned + (lo - off), hi - lo});
     }
 }
 
-void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
-                                  const std::function<void(void *, size_t)> &coll) {
-    std::vector<size_t> starts(segs.size());
+namespace {
+constexpr size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// Offsets of the segments in the staged stream: back to back, or 256-byte-rounded (padded).
+template <class Seg>
+size_t seg_starts(const std::vector<Seg> &segs, bool padded, std::vector<size_t> &starts) {
+    starts.resize(segs.size());
     size_t total = 0;
     for (size_t i = 0; i < segs.size(); ++i) {
         starts[i] = total;
-        total += segs[i].bytes;
+        total += padded ? round256(segs[i].bytes) : segs[i].bytes;
     }
-    if (total == 0) return;
+    return total;
+}
+
+// Host range [p, p + bytes) is pinned memory the device reaches at the same address, inside one
+// allocation, 16-byte aligned (the pack kernel's vector path). A failed query (pageable memory)
+// leaves no sticky error behind.
+bool mapped_host_range(const void *p, size_t bytes) {
+    if (bytes == 0) return true;
+    if (!p || (reinterpret_cast<uintptr_t>(p) & 15u) != 0) return false;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost || a.devicePointer != p) return false;
+    void *start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<void *>(p)) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, const_cast<void *>(p)) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(start), q = reinterpret_cast<uintptr_t>(p);
+    return start && q >= s0 && q + bytes <= s0 + size;
+}
+}  // namespace
+
+bool RequestHandler::mapped_host_segs_(const std::vector<HostSeg> &segs) {
+    for (const HostSeg &sg : segs) {
+        if (!mapped_host_range(sg.src, sg.bytes)) return false;
+        if (sg.dst != sg.src && !mapped_host_range(sg.dst, sg.bytes)) return false;
+    }
+    return true;
+}
+
+size_t RequestHandler::host_slots_(size_t total) {
     size_t chunk = (size_t)config().host_chunk_bytes.load() & ~size_t(255);  // a multiple of es
     if (chunk < 4096) chunk = 4096;
-    if (chunk > total) chunk = (total + 255) & ~size_t(255);
+    if (chunk > total) chunk = round256(total);
     if (host_slot_bytes_ < chunk) {
         for (hipStream_t st : {h2d_, d2h_, stream_})
             if (st) DDL_HIP(hipStreamSynchronize(st));
@@ -616,6 +654,7 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
             if (pin_[k]) DDL_HIP(hipHostFree(pin_[k]));
             if (dslot_[k]) DDL_HIP(hipFree(dslot_[k]));
             pin_[k] = dslot_[k] = nullptr;
+            slot_used_[k] = false;
         }
         host_slot_bytes_ = 0;
         for (int k = 0; k < kHostSlots; ++k) {
@@ -629,6 +668,15 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
         for (hipEvent_t &e : hev_) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    return chunk;
+}
+
+void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
+                                  const std::function<void(void *, size_t)> &coll, bool padded) {
+    std::vector<size_t> starts;
+    const size_t total = seg_starts(segs, padded, starts);
+    if (total == 0) return;
+    const size_t chunk = host_slots_(total);
     if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
     const size_t nchunks = (total + chunk - 1) / chunk;
     std::vector<CopyPool::Piece> pieces;
@@ -644,6 +692,8 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         const int k = (int)(i % kHostSlots);
         if (i >= (size_t)kHostSlots) unpack(i - kHostSlots);  // frees slot k (pinned and device)
         const size_t off = i * chunk, len = std::min(chunk, total - off);
+        // the device slot's last user may be a zero-copy plan still in flight
+        if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
         if (upload) {
             pieces.clear();
             host_pieces_(segs, starts, off, len, static_cast<char *>(pin_[k]), true, pieces);
@@ -657,8 +707,55 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
         DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], len, hipMemcpyDeviceToHost, d2h_));
         DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
+        slot_used_[k] = true;
     }
     for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) unpack(j);
+}
+
+void RequestHandler::host_zero_copy_(const std::vector<HostSeg> &segs, size_t es,
+                                     const std::function<void(void *, size_t)> &coll) {
+    std::vector<size_t> starts;
+    const size_t total = seg_starts(segs, true, starts);
+    if (total == 0) return;
+    const size_t chunk = host_slots_(total);
+    config().host_zero_copy_plans.fetch_add(1);
+    std::vector<void *> src, dst;
+    std::vector<size_t> len;
+    int last = 0;
+    for (size_t off = 0, i = 0; off < total; off += chunk, i++) {
+        const int k = (int)(i % kHostSlots);
+        const size_t end = std::min(total, off + chunk);
+        // the chunk's pieces; the pack kernel lays piece j at the rounded sum of the pieces
+        // before it, which is its offset in the padded stream (chunks start at multiples of 256,
+        // so a cut never falls inside a segment's padding)
+        src.clear();
+        dst.clear();
+        len.clear();
+        size_t flat = 0;
+        for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+             j < segs.size() && starts[j] < end; ++j) {
+            const size_t lo = std::max(off, starts[j]), hi = std::min(end, starts[j] + segs[j].bytes);
+            if (hi <= lo) continue;
+            DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "zero-copy chunk layout");
+            src.push_back(const_cast<char *>(segs[j].src) + (lo - starts[j]));
+            dst.push_back(segs[j].dst + (lo - starts[j]));
+            len.push_back(hi - lo);
+            flat += round256(hi - lo);
+        }
+        if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));  // slot free
+        copier_.run(0, dslot_[k], src.data(), len.data(), (int)src.size(), h2d_);
+        DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
+        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
+        coll(dslot_[k], (end - off) / es);
+        DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
+        DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
+        copier_.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
+        DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
+        slot_used_[k] = true;
+        last = k;
+    }
+    // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
+    DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * last + 2], 0));
 }
 
 // allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
@@ -703,9 +800,13 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
                     pool_->run(pieces);
                 } else {
-                    host_staged_(segs, es, true, [&](void *d, size_t elems) {
+                    // chunks of the padded stream either way, so ranks that differ in which
+                    // tensors are pinned still issue the same collectives
+                    auto coll = [&](void *d, size_t elems) {
                         data_->allreduce(d, d, elems, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
-                    });
+                    };
+                    if (config().host_zero_copy.load() && mapped_host_segs_(segs)) host_zero_copy_(segs, es, coll);
+                    else host_staged_(segs, es, true, coll, true);
                 }
             } else if (data_->size() == 1 && config().one_rank_shortcut.load()) {
                 // a one-rank world: the sum is the input; move bytes only where out != in

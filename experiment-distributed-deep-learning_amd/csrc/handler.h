@@ -184,10 +184,23 @@ private:
         char *dst;
         size_t bytes;
     };
+    // `padded`: segment i starts at the 256-byte-rounded running offset (the fusion kernels'
+    // layout), so a staged plan cuts the same chunks — and issues the same collectives — as a
+    // zero-copy one on another rank; otherwise back to back (broadcast, as the reference packs).
     void host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
-                      const std::function<void(void *dev, size_t elems)> &coll);
+                      const std::function<void(void *dev, size_t elems)> &coll, bool padded = false);
     void host_pieces_(const std::vector<HostSeg> &segs, const std::vector<size_t> &starts, size_t off, size_t len,
                       char *pinned, bool pack, std::vector<CopyPool::Piece> &out);
+    // Zero-copy form of host_staged_ (padded layout, same chunks) for segments that are all
+    // pinned host memory mapped on the device (mapped_host_segs_): per chunk the pack kernel
+    // reads the tensors over PCIe into a device slot (h2d_), `coll` runs on it (stream_), the
+    // unpack kernel writes the result back over PCIe (d2h_); no host copy, no host wait.
+    void host_zero_copy_(const std::vector<HostSeg> &segs, size_t es,
+                         const std::function<void(void *dev, size_t elems)> &coll);
+    // true when every segment's source and destination ranges are 16-byte-aligned pinned host
+    // memory that the device reaches at the same address, inside one allocation each
+    static bool mapped_host_segs_(const std::vector<HostSeg> &segs);
+    size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);
@@ -213,7 +226,8 @@ private:
     void *dslot_[kHostSlots] = {};  // device slots
     size_t host_slot_bytes_ = 0;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
-    hipEvent_t hev_[3 * kHostSlots] = {};
+    hipEvent_t hev_[3 * kHostSlots] = {};  // per slot: input landed, collective done, output landed
+    bool slot_used_[kHostSlots] = {};        // hev_[3k + 2] marks the slot's last device use
     std::unique_ptr<CopyPool> pool_;
     void *pin_gather_ = nullptr;  // host allgather staging
     size_t pin_gather_bytes_ = 0;

@@ -152,7 +152,11 @@ int ddl_is_initialized(void);
  * ncclAllGather then the rank-order fold, 4 direct-gather: the direct reduce-scatter then one
  * in-place ncclAllGather of the reduced chunks when they are equal), "slice_bytes", "rings", "max_slices",
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
- * "host_copy_threads" (memcpy workers of the keyed host staging),
+ * "host_copy_threads" (memcpy workers of the keyed host staging), "host_zero_copy" (1, default:
+ * a keyed host allreduce plan whose tensors are all pinned and mapped on the device — torch
+ * pin_memory, hipHostMalloc, hipHostRegister — is packed / unpacked by the fusion kernels
+ * straight over PCIe, no staging memcpy; 0: always stage through the pinned slots; the
+ * read-only "host_zero_copy_plans" counts the plans that took that path),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "reference_order" (1,

@@ -199,8 +199,10 @@ def check_keyed_host_requests(ctx):
     AllreduceOp.cc:68): fused per dtype, staged through pinned 64 KiB chunks (many chunks, the
     4 slots wrap), reduced on the GPU and unpacked back. Every element equals MPICH's order
     for the host group's message (ddlo_fold_ref_order with the group's bytes), bit for bit. A
-    device request of the same dtype in the same batch forms its own group. Then keyed host
-    broadcasts (mixed roots) and allgathers (per-rank first dims)."""
+    device request of the same dtype in the same batch forms its own group. Rounds 2 and 3 pin
+    the tensors — on even ranks only (zero-copy pack / unpack there, staging elsewhere: the
+    ranks must still cut the same chunks), then on every rank. Then keyed host broadcasts
+    (mixed roots) and allgathers (per-rank first dims)."""
     import _helpers as h
     torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
     from ddl.torch.tensor_communicate import allgather_async, allreduce_async_batch, broadcast_async
@@ -210,20 +212,27 @@ def check_keyed_host_requests(ctx):
     gb = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
     dev_x = [h.random_input(h.DT_FLOAT, 4099, 4000 + q) for q in range(P)]
     with h.config(lib, host_chunk_bytes=64 << 10, reference_order=1):
-        for rnd in range(2):
+        for rnd in range(4):
+            pin = rnd == 3 or (rnd == 2 and r % 2 == 0)
             ts = [torch.from_numpy(xs[i][r].copy()) for i in range(len(sizes))]
+            if pin:
+                ts = [t.pin_memory() for t in ts]
             order = np.random.default_rng(5 * rnd + r).permutation(len(sizes))
             tensors = [ts[i] for i in order] + [torch.from_numpy(dev_x[r]).cuda()]
             names = [f'host_{i}' for i in order] + ['dev_0']
-            outs = [t if (rnd == 1 and not t.is_cuda) else None for t in tensors]  # round 1: in place
+            outs = [t if (rnd % 2 == 1 and not t.is_cuda) else None for t in tensors]  # odd rounds: in place
+            plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
             hs = allreduce_async_batch(tensors, names, comm,
-                                       outputs=[o if o is not None else torch.empty_like(t) for o, t in zip(outs, tensors)])
+                                       outputs=[o if o is not None else torch.empty_like(t, pin_memory=pin and not t.is_cuda)
+                                                for o, t in zip(outs, tensors)])
             for hd, i in zip(hs, order):
                 got = hd.wait(timeout=120)
                 assert not got.is_cuda
                 want = ora.fold_ref_order(dts[i], xs[i], gb[dts[i]])
                 assert got.numpy().tobytes() == want.tobytes(), (rnd, i)
             assert hs[-1].wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, dev_x).tobytes()
+            # three host dtype groups, one plan each
+            assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == (3 if pin else 0), rnd
         hs, want = [], []
         for i in range(9):
             root, dt = i % P, [torch.float32, torch.int64, torch.float64][i % 3]
