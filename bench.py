@@ -458,10 +458,10 @@ def fusion_c5(lib, comm, dev, steps, k=4096, forced=True):
 
 def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
-    buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks —
-    pageable tensors: pinned-slot staging, host pack -> H2D -> allreduce -> D2H -> host unpack;
-    pinned tensors (`pinned`): zero copy, the pack / unpack kernels read and write the tensors
-    over PCIe (ddl_allreduce_submit_batch_mem, DDL_MEMORY_HOST). At one rank the data plane is
+    buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks
+    through pinned slots: host pack -> H2D -> allreduce -> D2H -> host unpack; with pinned tensors
+    (`pinned`) the unpack kernel writes the results into them over PCIe instead of D2H + host
+    unpack (ddl_allreduce_submit_batch_mem, DDL_MEMORY_HOST). At one rank the data plane is
     forced (one_rank_shortcut = 0). The rate is PCIe-bound (2 x bytes cross the host link); it is
     never `value`."""
     import numpy as np
@@ -499,14 +499,14 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
     finally:
         lib.ddl_set_config(b'one_rank_shortcut', old)
-    path = ('pinned host tensors -> keyed batch -> negotiation -> plans -> chunks: pack kernel reads the tensors '
-            'over PCIe, allreduce, unpack kernel writes them back (zero copy), in place' if pinned else
+    path = ('pinned host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
+            'allreduce), unpack kernel writes the results straight into the tensors over PCIe, in place' if pinned else
             'pageable host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
             'allreduce, D2H, host unpack), in place')
     return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3), 'bucket_GiBs': round(total / GiB / dt, 2),
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
-            'zero_copy_plans_per_step': zero_copy_plans / steps, 'path': path}
+            'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path}
 
 
 def host_resident_rate(lib, comm, S, reps):

@@ -38,12 +38,12 @@ struct Config {
     // memcpy workers of the keyed host-staging pipeline (pageable <-> pinned), besides the
     // engine thread itself
     std::atomic<long long> host_copy_threads{7};
-    // keyed host allreduce plans whose tensors are all pinned and mapped into the device's
-    // address space (torch pin_memory, hipHostMalloc, hipHostRegister): the pack / unpack kernels
-    // read and write them over PCIe in place of the pinned-slot memcpys (1 on, 0 always stage)
+    // keyed host allreduce plans whose outputs are all pinned and mapped into the device's
+    // address space (torch pin_memory, hipHostMalloc, hipHostRegister): the unpack kernel writes
+    // them over PCIe in place of the D2H copy and the host unpack memcpy (1 on, 0 always stage)
     std::atomic<long long> host_zero_copy{1};
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
-    // that took the zero-copy path in this process
+    // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set

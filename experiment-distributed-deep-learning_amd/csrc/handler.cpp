@@ -635,11 +635,9 @@ bool mapped_host_range(const void *p, size_t bytes) {
 }
 }  // namespace
 
-bool RequestHandler::mapped_host_segs_(const std::vector<HostSeg> &segs) {
-    for (const HostSeg &sg : segs) {
-        if (!mapped_host_range(sg.src, sg.bytes)) return false;
-        if (sg.dst != sg.src && !mapped_host_range(sg.dst, sg.bytes)) return false;
-    }
+bool RequestHandler::mapped_host_dsts_(const std::vector<HostSeg> &segs) {
+    for (const HostSeg &sg : segs)
+        if (!mapped_host_range(sg.dst, sg.bytes)) return false;
     return true;
 }
 
@@ -672,12 +670,13 @@ size_t RequestHandler::host_slots_(size_t total) {
 }
 
 void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
-                                  const std::function<void(void *, size_t)> &coll, bool padded) {
+                                  const std::function<void(void *, size_t)> &coll, bool padded, bool device_unpack) {
     std::vector<size_t> starts;
-    const size_t total = seg_starts(segs, padded, starts);
+    const size_t total = seg_starts(segs, padded || device_unpack, starts);
     if (total == 0) return;
     const size_t chunk = host_slots_(total);
     if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
+    if (device_unpack) config().host_zero_copy_plans.fetch_add(1);
     const size_t nchunks = (total + chunk - 1) / chunk;
     std::vector<CopyPool::Piece> pieces;
     auto unpack = [&](size_t j) {
@@ -688,74 +687,58 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         host_pieces_(segs, starts, off, std::min(chunk, total - off), static_cast<char *>(pin_[k]), false, pieces);
         pool_->run(pieces);
     };
+    std::vector<void *> dst;
+    std::vector<size_t> len;
     for (size_t i = 0; i < nchunks; ++i) {
         const int k = (int)(i % kHostSlots);
-        if (i >= (size_t)kHostSlots) unpack(i - kHostSlots);  // frees slot k (pinned and device)
-        const size_t off = i * chunk, len = std::min(chunk, total - off);
-        // the device slot's last user may be a zero-copy plan still in flight
+        if (i >= (size_t)kHostSlots && !device_unpack) unpack(i - kHostSlots);  // frees slot k (pinned and device)
+        const size_t off = i * chunk, n = std::min(chunk, total - off);
+        // the device slot's last user may still be in flight (a device unpack)
         if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
         if (upload) {
+            // the pinned slot's last upload must have left it (device-unpack plans do not wait
+            // for their D2H on the host)
+            if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
             pieces.clear();
-            host_pieces_(segs, starts, off, len, static_cast<char *>(pin_[k]), true, pieces);
+            host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
             pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
-            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], len, hipMemcpyHostToDevice, h2d_));
+            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
         }
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
-        coll(dslot_[k], len / es);
+        coll(dslot_[k], n / es);
         DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
         DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
-        DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], len, hipMemcpyDeviceToHost, d2h_));
+        if (device_unpack) {
+            // the unpack kernel writes the chunk's pieces straight into the pinned outputs over
+            // PCIe; it lays piece j at the rounded sum of the pieces before it, which is its
+            // offset in the padded stream (chunks start at multiples of 256, so a cut never
+            // falls inside a segment's padding)
+            dst.clear();
+            len.clear();
+            size_t flat = 0;
+            for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+                 j < segs.size() && starts[j] < off + n; ++j) {
+                const size_t lo = std::max(off, starts[j]), hi = std::min(off + n, starts[j] + segs[j].bytes);
+                if (hi <= lo) continue;
+                DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "device-unpack chunk layout");
+                dst.push_back(segs[j].dst + (lo - starts[j]));
+                len.push_back(hi - lo);
+                flat += round256(hi - lo);
+            }
+            copier_.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
+        } else {
+            DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
+        }
         DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
         slot_used_[k] = true;
+    }
+    if (device_unpack) {
+        // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
+        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * ((nchunks - 1) % kHostSlots) + 2], 0));
+        return;
     }
     for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) unpack(j);
-}
-
-void RequestHandler::host_zero_copy_(const std::vector<HostSeg> &segs, size_t es,
-                                     const std::function<void(void *, size_t)> &coll) {
-    std::vector<size_t> starts;
-    const size_t total = seg_starts(segs, true, starts);
-    if (total == 0) return;
-    const size_t chunk = host_slots_(total);
-    config().host_zero_copy_plans.fetch_add(1);
-    std::vector<void *> src, dst;
-    std::vector<size_t> len;
-    int last = 0;
-    for (size_t off = 0, i = 0; off < total; off += chunk, i++) {
-        const int k = (int)(i % kHostSlots);
-        const size_t end = std::min(total, off + chunk);
-        // the chunk's pieces; the pack kernel lays piece j at the rounded sum of the pieces
-        // before it, which is its offset in the padded stream (chunks start at multiples of 256,
-        // so a cut never falls inside a segment's padding)
-        src.clear();
-        dst.clear();
-        len.clear();
-        size_t flat = 0;
-        for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
-             j < segs.size() && starts[j] < end; ++j) {
-            const size_t lo = std::max(off, starts[j]), hi = std::min(end, starts[j] + segs[j].bytes);
-            if (hi <= lo) continue;
-            DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "zero-copy chunk layout");
-            src.push_back(const_cast<char *>(segs[j].src) + (lo - starts[j]));
-            dst.push_back(segs[j].dst + (lo - starts[j]));
-            len.push_back(hi - lo);
-            flat += round256(hi - lo);
-        }
-        if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));  // slot free
-        copier_.run(0, dslot_[k], src.data(), len.data(), (int)src.size(), h2d_);
-        DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
-        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
-        coll(dslot_[k], (end - off) / es);
-        DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
-        DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
-        copier_.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
-        DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
-        slot_used_[k] = true;
-        last = k;
-    }
-    // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
-    DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * last + 2], 0));
 }
 
 // allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
@@ -801,12 +784,12 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     pool_->run(pieces);
                 } else {
                     // chunks of the padded stream either way, so ranks that differ in which
-                    // tensors are pinned still issue the same collectives
+                    // outputs are pinned still issue the same collectives
                     auto coll = [&](void *d, size_t elems) {
                         data_->allreduce(d, d, elems, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
                     };
-                    if (config().host_zero_copy.load() && mapped_host_segs_(segs)) host_zero_copy_(segs, es, coll);
-                    else host_staged_(segs, es, true, coll, true);
+                    host_staged_(segs, es, true, coll, true,
+                                 config().host_zero_copy.load() && mapped_host_dsts_(segs));
                 }
             } else if (data_->size() == 1 && config().one_rank_shortcut.load()) {
                 // a one-rank world: the sum is the input; move bytes only where out != in

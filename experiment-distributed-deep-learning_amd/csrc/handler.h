@@ -179,27 +179,28 @@ private:
     // pinned slots in chunks — host pack (CopyPool) -> H2D -> `coll` on the device slot
     // (stream_) -> D2H -> host unpack — with kHostSlots chunks in flight so the copies overlap
     // the collective. `upload` false: nothing is packed (a broadcast's non-root ranks).
+    // `padded`: segment i starts at the 256-byte-rounded running offset (the fusion kernels'
+    // layout), so plans with and without `device_unpack` cut the same chunks — and issue the
+    // same collectives — on ranks that differ in which outputs are pinned; otherwise back to
+    // back (broadcast, as the reference packs).
+    // `device_unpack` (every destination pinned and mapped on the device, mapped_host_dsts_): the
+    // unpack kernel writes each chunk's result straight into the outputs over PCIe (d2h_), in
+    // place of the D2H copy and the host unpack; the host never waits for a chunk to come back
+    // (measured 43 GB/s each way with the uploads running, vs 32 when the pack kernel also
+    // reads the tensors over PCIe: profiles/r02/host/zero_copy_probe.jsonl).
     struct HostSeg {
         const char *src;
         char *dst;
         size_t bytes;
     };
-    // `padded`: segment i starts at the 256-byte-rounded running offset (the fusion kernels'
-    // layout), so a staged plan cuts the same chunks — and issues the same collectives — as a
-    // zero-copy one on another rank; otherwise back to back (broadcast, as the reference packs).
     void host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
-                      const std::function<void(void *dev, size_t elems)> &coll, bool padded = false);
+                      const std::function<void(void *dev, size_t elems)> &coll, bool padded = false,
+                      bool device_unpack = false);
     void host_pieces_(const std::vector<HostSeg> &segs, const std::vector<size_t> &starts, size_t off, size_t len,
                       char *pinned, bool pack, std::vector<CopyPool::Piece> &out);
-    // Zero-copy form of host_staged_ (padded layout, same chunks) for segments that are all
-    // pinned host memory mapped on the device (mapped_host_segs_): per chunk the pack kernel
-    // reads the tensors over PCIe into a device slot (h2d_), `coll` runs on it (stream_), the
-    // unpack kernel writes the result back over PCIe (d2h_); no host copy, no host wait.
-    void host_zero_copy_(const std::vector<HostSeg> &segs, size_t es,
-                         const std::function<void(void *dev, size_t elems)> &coll);
-    // true when every segment's source and destination ranges are 16-byte-aligned pinned host
-    // memory that the device reaches at the same address, inside one allocation each
-    static bool mapped_host_segs_(const std::vector<HostSeg> &segs);
+    // true when every segment's destination range is 16-byte-aligned pinned host memory that the
+    // device reaches at the same address, inside one allocation
+    static bool mapped_host_dsts_(const std::vector<HostSeg> &segs);
     size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);

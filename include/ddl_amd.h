@@ -153,9 +153,9 @@ int ddl_is_initialized(void);
  * in-place ncclAllGather of the reduced chunks when they are equal), "slice_bytes", "rings", "max_slices",
  * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
  * "host_copy_threads" (memcpy workers of the keyed host staging), "host_zero_copy" (1, default:
- * a keyed host allreduce plan whose tensors are all pinned and mapped on the device — torch
- * pin_memory, hipHostMalloc, hipHostRegister — is packed / unpacked by the fusion kernels
- * straight over PCIe, no staging memcpy; 0: always stage through the pinned slots; the
+ * a keyed host allreduce plan whose outputs are all pinned and mapped on the device — torch
+ * pin_memory, hipHostMalloc, hipHostRegister — is unpacked by the fusion kernel straight into
+ * them over PCIe, no D2H copy or host memcpy; 0: always stage through the pinned slots; the
  * read-only "host_zero_copy_plans" counts the plans that took that path),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a

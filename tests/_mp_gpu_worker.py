@@ -200,8 +200,8 @@ def check_keyed_host_requests(ctx):
     4 slots wrap), reduced on the GPU and unpacked back. Every element equals MPICH's order
     for the host group's message (ddlo_fold_ref_order with the group's bytes), bit for bit. A
     device request of the same dtype in the same batch forms its own group. Rounds 2 and 3 pin
-    the tensors — on even ranks only (zero-copy pack / unpack there, staging elsewhere: the
-    ranks must still cut the same chunks), then on every rank. Then keyed host broadcasts
+    the tensors — on even ranks only (the unpack kernel writes the outputs over PCIe there, D2H
+    and host unpack elsewhere: the ranks must still cut the same chunks), then on every rank. Then keyed host broadcasts
     (mixed roots) and allgathers (per-rank first dims)."""
     import _helpers as h
     torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']

@@ -273,16 +273,16 @@ def test_keyed_fusion_pipeline_large_segment(world, lib, data_plane_at_one_rank)
         assert torch.equal(h.wait(timeout=60), w)
 
 
-@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'mixed', 'pinned_misaligned'])
+@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'pinned_outputs', 'mixed', 'pinned_misaligned'])
 @pytest.mark.parametrize('chunk', [4096, 64 << 10, 32 << 20])
 def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     """Keyed requests on host tensors with the one-rank shortcut off: every plan goes through the
     host pipeline in chunks (4096 B chunks make hundreds of chunks over 4 slots), in and out of
     place, every dtype, plus a device request in the same batch; outputs equal the inputs bit for
-    bit (one rank). Pageable tensors are staged (host pack -> H2D -> allreduce -> D2H -> host
-    unpack); when every tensor of a plan is pinned the pack / unpack kernels read and write them
-    over PCIe (zero copy) — the plan counter says which path ran. A pinned tensor viewed at a
-    2-byte offset, or one pageable tensor in the dtype group, sends its plan back to staging."""
+    bit (one rank). Pageable outputs are staged back (D2H -> host unpack); when every output of a
+    plan is pinned the unpack kernel writes them over PCIe — the plan counter says which path
+    ran. A pinned output viewed at a 2-byte offset, or one pageable output in the dtype group,
+    sends its plan back to staging."""
     from ddl.torch.tensor_communicate import allreduce_async_batch, broadcast_async
     keys = (b'one_rank_shortcut', b'host_chunk_bytes')
     old = {k: lib.ddl_get_config(k) for k in keys}
@@ -293,12 +293,16 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
         dts = [torch.float32, torch.float64, torch.int32, torch.float16, torch.bfloat16, torch.int64]
         xs = [(torch.randn(n, generator=g) * 100).to(dts[i % 6]) for i, n in enumerate([1, 7, 1000, 65_537, 300_001,
                                                                                        5, 2_000_003, 4096])]
-        if memory != 'pageable':
-            xs = [x.pin_memory() if memory != 'mixed' or i != 2 else x for i, x in enumerate(xs)]
-        if memory == 'pinned_misaligned':  # fp16 tensor 3 seen from its second element: 2-byte offset
+        if memory in ('pinned', 'mixed', 'pinned_misaligned'):
+            xs = [x.pin_memory() for x in xs]
+        if memory == 'pinned_misaligned':  # fp16 tensor 3 (in place) seen from its second element: 2-byte offset
             xs[3] = xs[3][1:]
         keep = [x.clone() for x in xs]
-        outs = [x if i % 2 else torch.empty_like(x, pin_memory=memory != 'pageable') for i, x in enumerate(xs)]
+        # odd tensors in place, even ones into fresh outputs (int32 tensor 2: pageable when mixed)
+        outs = [x if i % 2 else torch.empty_like(x, pin_memory=memory != 'pageable' and (memory, i) != ('mixed', 2))
+                for i, x in enumerate(xs)]
+        if memory == 'pinned_outputs':  # pageable inputs, every output pinned
+            outs = [torch.empty_like(x, pin_memory=True) for x in xs]
         dev = torch.randn(1234, device='cuda')
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
         hs = allreduce_async_batch(xs + [dev], [f'hk_{i}' for i in range(len(xs))] + ['hk_dev'], world,
@@ -309,8 +313,9 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
         assert torch.equal(hs[-1].wait(timeout=60), dev)
         # one plan per host dtype group (6 dtypes); staged: the mixed int32 group and the
         # misaligned fp16 group
-        zero_copy = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
-        assert zero_copy == {'pageable': 0, 'pinned': 6, 'mixed': 5, 'pinned_misaligned': 5}[memory]
+        device_unpacked = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
+        assert device_unpacked == {'pageable': 0, 'pinned': 6, 'pinned_outputs': 6, 'mixed': 5,
+                                   'pinned_misaligned': 5}[memory]
         t = torch.arange(100_003, dtype=torch.float64)
         assert torch.equal(broadcast_async(t, 'hk_b', 0, world).wait(timeout=60), t)
     finally:

@@ -130,6 +130,52 @@ def main():
     emit({'probe': 'zero_copy_both_directions_c5', 'bytes_each_way': total, 'ms': round(t_both * 1e3, 3),
           'GBs_each_way': round(total / t_both / 1e9, 2)})
 
+    # DMA per tensor straight from / to the pinned tensors (no host memcpy): one hipMemcpyAsync
+    # per bucket, each direction alone and both at once, and mixed with the kernels
+    offs, o = [], 0
+    for b in nbytes:
+        offs.append(o)
+        o += (int(b) + 255) // 256 * 256
+    base, base2 = fused.data_ptr(), fused2.data_ptr()
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    sh1, sh2 = ctypes.c_void_p(s1.cuda_stream), ctypes.c_void_p(s2.cuda_stream)
+
+    def dma_h2d(dstbase=base):
+        for i in range(k):
+            hip.hipMemcpyAsync(dstbase + offs[i], ptrs[i], nbytes[i], 1, sh1)
+
+    def dma_d2h(srcbase=base2):
+        for i in range(k):
+            hip.hipMemcpyAsync(ptrs[i], srcbase + offs[i], nbytes[i], 2, sh2)
+
+    t0 = time.perf_counter()
+    dma_h2d()
+    t_enq = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    res = {'probe': 'dma_per_tensor_c5', 'enqueue_us_per_copy': round(t_enq / k * 1e6, 2)}
+    for name, fn in (('h2d', dma_h2d), ('d2h', dma_d2h), ('both', lambda: (dma_h2d(), dma_d2h())),
+                     ('kernel_h2d_dma_d2h', lambda: (check(lib.ddl_pack(base, ptrs, nbytes, k, s1.cuda_stream), 'p'),
+                                                     dma_d2h())),
+                     ('dma_h2d_kernel_d2h', lambda: (dma_h2d(), check(lib.ddl_unpack(ptrs, base2, nbytes, k,
+                                                                                    s2.cuda_stream), 'u')))):
+        t = timed(fn)
+        res[name + '_GBs_each_way'] = round(total / t / 1e9, 2)
+    emit(res)
+    if hasattr(hip, 'hipMemcpyBatchAsync'):
+        Vp = ctypes.c_void_p * k
+        dsts = Vp(*[base + x for x in offs])
+        fail = ctypes.c_size_t()
+        hip.hipMemcpyBatchAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        rcs = []
+
+        def batch():
+            rcs.append(hip.hipMemcpyBatchAsync(dsts, ptrs, nbytes, k, None, None, 0, ctypes.byref(fail), sh1))
+        t = timed(batch)
+        hip.hipGetLastError()
+        emit({'probe': 'hipMemcpyBatchAsync_h2d_c5', 'rc': rcs[-1], 'GBs': round(total / t / 1e9, 2)})
+
     # DMA reference: one pinned buffer of the same size, H2D, D2H, both at once
     big = torch.empty(total // 4, dtype=torch.float32, pin_memory=True)
     dbig, dbig2 = torch.empty(total // 4, device=dev), torch.empty(total // 4, device=dev)
@@ -148,6 +194,17 @@ def main():
         d2h()
     emit({'probe': 'dma_one_pinned_buffer', 'bytes': total, 'h2d_GBs': round(total / timed(h2d) / 1e9, 2),
           'd2h_GBs': round(total / timed(d2h) / 1e9, 2), 'both_GBs_each_way': round(total / timed(dma_both) / 1e9, 2)})
+
+    # hybrids: one direction by the kernel over PCIe, the other by one large DMA of a pinned slot
+    def kernel_pack_dma_d2h():
+        check(lib.ddl_pack(base, ptrs, nbytes, k, s1.cuda_stream), 'p')
+        d2h()
+
+    def dma_h2d_kernel_unpack():
+        h2d()
+        check(lib.ddl_unpack(ptrs, base2, nbytes, k, s2.cuda_stream), 'u')
+    emit({'probe': 'hybrid_c5', 'kernel_pack_with_large_d2h_GBs_each_way': round(total / timed(kernel_pack_dma_d2h) / 1e9, 2),
+          'large_h2d_with_kernel_unpack_GBs_each_way': round(total / timed(dma_h2d_kernel_unpack) / 1e9, 2)})
 
 
 if __name__ == '__main__':
