@@ -8,6 +8,12 @@ divided by the communicator size (allreduce_gradient, tensor_communicate.py:21-2
 gradient (torch sparse COO, TF's IndexedSlices) goes through allreduce_gradient's allgather
 branch (:26-30), as the reference's wrapper does for every grad. At size 1 nothing is
 communicated (the reference's `tf.cond(size > 1)`, :53-60).
+
+CPU models (the reference's deployment: its op is CPU-only, AllreduceOp.cc:68): with
+`pin_host_gradients` (default) each dense CPU gradient is moved once into pinned memory and
+kept there — zero_grad() zeroes it in place instead of dropping it, and autograd accumulates
+into it in place — so the engine's unpack kernel writes the reduced gradients straight into
+them over PCIe (no D2H copy, no host memcpy).
 """
 import torch
 
@@ -18,12 +24,21 @@ from ddl.torch.tensor_communicate import allreduce_async_batch, allreduce_gradie
 class DataParallelismDistributedOptimizer:
     """Mixin placed in front of the wrapped optimizer class (the reference's approach)."""
     communicator: Communicator = None
+    pin_host_gradients: bool = True
     _ddl_name = 'DataParallelismDistributedOptimizer'
+
+    def _pinning(self) -> bool:
+        return self.pin_host_gradients and torch.cuda.is_available()
+
+    @staticmethod
+    def _pinned_host_grad(g) -> bool:
+        return g is not None and not g.is_cuda and not g.is_sparse and g.is_pinned()
 
     def allreduce_gradients(self) -> None:
         comm = self.communicator or Communicator.world()
         if comm.size <= 1:
             return
+        pin = self._pinning()
         params, grads, keys, sparse = [], [], [], []
         for gi, group in enumerate(self.param_groups):
             for pi, p in enumerate(group['params']):
@@ -32,6 +47,8 @@ class DataParallelismDistributedOptimizer:
                 if p.grad.is_sparse:
                     sparse.append(p)
                     continue
+                if pin and not p.grad.is_cuda and p.grad.is_contiguous() and not p.grad.is_pinned():
+                    p.grad = p.grad.pin_memory()  # once: zero_grad keeps it (see below)
                 params.append(p)
                 grads.append(p.grad if p.grad.is_contiguous() else p.grad.contiguous())
                 keys.append(f'{self._ddl_name}/{type(self).__name__}/Allreduce/group{gi}/param{pi:05d}')
@@ -47,6 +64,20 @@ class DataParallelismDistributedOptimizer:
         for p in sparse:
             p.grad = allreduce_gradient(p.grad, comm)
 
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        # pinned host gradients survive zero_grad (zeroed in place), so the next backward
+        # accumulates into the same pinned buffers
+        keep = []
+        if self._pinning():
+            keep = [(p, p.grad) for group in self.param_groups for p in group['params']
+                    if self._pinned_host_grad(p.grad)]
+        super().zero_grad(set_to_none)
+        with torch.no_grad():
+            for p, g in keep:
+                if p.grad is None:
+                    g.zero_()
+                    p.grad = g
+
     @torch.no_grad()
     def step(self, closure=None):
         self.allreduce_gradients()
@@ -59,14 +90,17 @@ class DataParallelismDistributedOptimizer:
 
 def data_parallelism_distributed_optimizer_wrapper(
         optimizer: torch.optim.Optimizer,
-        communicator: Communicator = None) -> torch.optim.Optimizer:
+        communicator: Communicator = None,
+        pin_host_gradients: bool = True) -> torch.optim.Optimizer:
     """Return an optimizer of a subclass of `type(optimizer)` whose step() first averages the
     gradients across `communicator` (default: the world). Parameter groups and state are
-    shared with `optimizer`."""
+    shared with `optimizer`. `pin_host_gradients`: keep CPU gradients in pinned memory (module
+    docstring)."""
     opt_cls = optimizer.__class__
     assert issubclass(opt_cls, torch.optim.Optimizer)
     cls = type(opt_cls.__name__, (DataParallelismDistributedOptimizer, opt_cls), {})
     res = cls.__new__(cls)
     res.__dict__.update(optimizer.__dict__)
     res.communicator = communicator
+    res.pin_host_gradients = pin_host_gradients
     return res

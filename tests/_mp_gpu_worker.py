@@ -271,12 +271,18 @@ def check_dp_training_cpu_model(ctx):
     opt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(model.parameters(), lr=0.1), comm)
     ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
     g = torch.Generator().manual_seed(78)
+    lib = ctx['lib']
     for step in range(3):
         xb = [torch.randn(8, 16, generator=g, dtype=torch.float64) for _ in range(P)]
         yb = [torch.randn(8, 4, generator=g, dtype=torch.float64) for _ in range(P)]
         opt.zero_grad()
+        if step > 0:  # the gradients moved to pinned memory at step 0 survive zero_grad
+            assert all(p.grad is not None and p.grad.is_pinned() and not p.grad.any() for p in model.parameters())
         torch.nn.functional.mse_loss(model(xb[r]), yb[r]).backward()
+        plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
         opt.step()
+        if step > 0:  # one fp64 plan, unpacked by the kernel into the pinned gradients
+            assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == 1
         ref_opt.zero_grad()
         sum(torch.nn.functional.mse_loss(ref(xb[q]), yb[q]) for q in range(P)).div(P).backward()
         ref_opt.step()
