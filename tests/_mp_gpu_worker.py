@@ -5,6 +5,7 @@ carried differently: through gloo on host copies (ddl_init_test_transport), beca
 refuses two ranks on one device. Every check compares with the oracle or an exact sum; every
 rank runs the same checks in the same order (they are collectives) and reports
 (name, ok, detail). Test infrastructure only."""
+import contextlib
 import ctypes
 import os
 import sys
@@ -290,6 +291,44 @@ def check_dp_training_cpu_model(ctx):
         assert torch.allclose(p, q, rtol=1e-12, atol=1e-12)
 
 
+def check_dp_training_overlap(ctx):
+    """overlap_backward: every gradient's keyed allreduce is submitted from its backward hook
+    while autograd still runs; step() waits. Three steps equal one full-batch fp64 step each;
+    then gradient accumulation — the first micro-batch's backward inside no_sync(), the second
+    outside — equals the full-batch step over both micro-batches. GPU and CPU (pinned) models."""
+    torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
+    from ddl.torch.parallelism.data import InitialParametersBroadcast, data_parallelism_distributed_optimizer_wrapper
+    for dev in ('cuda', 'cpu'):
+        def model_fn(seed):
+            torch.manual_seed(seed)
+            return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 32), torch.nn.Tanh(),
+                                       torch.nn.Linear(32, 4)).double().to(dev)
+        model = model_fn(555 + r)
+        InitialParametersBroadcast(model, 0, communicator=comm).broadcast()
+        ref = model_fn(555)
+        opt = data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(model.parameters(), lr=0.05), comm,
+                                                             overlap_backward=True)
+        ref_opt = torch.optim.SGD(ref.parameters(), lr=0.05)
+        g = torch.Generator().manual_seed(91)
+        for step in range(4):
+            micro = 2 if step == 3 else 1
+            xb = [[torch.randn(8, 16, generator=g, dtype=torch.float64) for _ in range(P)] for _ in range(micro)]
+            yb = [[torch.randn(8, 4, generator=g, dtype=torch.float64) for _ in range(P)] for _ in range(micro)]
+            opt.zero_grad()
+            for m in range(micro):
+                ctxm = opt.no_sync() if m + 1 < micro else contextlib.nullcontext()
+                with ctxm:
+                    torch.nn.functional.mse_loss(model(xb[m][r].to(dev)), yb[m][r].to(dev)).backward()
+            assert len(opt._grad_handles) == len(list(model.parameters()))  # all submitted by the hooks
+            opt.step()
+            ref_opt.zero_grad()
+            for m in range(micro):
+                sum(torch.nn.functional.mse_loss(ref(xb[m][q].to(dev)), yb[m][q].to(dev)) for q in range(P)).div(P).backward()
+            ref_opt.step()
+        for p, q in zip(model.parameters(), ref.parameters()):
+            assert torch.allclose(p, q, rtol=1e-12, atol=1e-12), dev
+
+
 def check_keyed_broadcast_allgather(ctx):
     """Keyed broadcasts with mixed roots and dtypes, keyed allgathers with per-rank first dims."""
     torch, comm, P, r = ctx['torch'], ctx['comm'], ctx['P'], ctx['rank']
@@ -374,7 +413,8 @@ def check_dp_training(ctx):
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
           check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
-          check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model]
+          check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model,
+          check_dp_training_overlap]
 
 
 def worker(rank, world, port, q):

@@ -47,7 +47,7 @@ def test_engine_multiprocess_on_one_gpu(gpu, world):
                 p.join(timeout=10)
     assert sorted(res) == list(range(world)), f'ranks reported: {sorted(res)}'
     names = [n for n, _, _ in res[0]]
-    assert names and names[-1] == 'check_dp_training_cpu_model' or any(not ok for _, ok, _ in res[0]), names
+    assert names and names[-1] == _mp_gpu_worker.CHECKS[-1].__name__ or any(not ok for _, ok, _ in res[0]), names
     for rank, results in sorted(res.items()):
         for name, ok, detail in results:
             assert ok, f'rank {rank} {name}:\n{detail}'
