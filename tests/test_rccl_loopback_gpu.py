@@ -69,6 +69,22 @@ def test_rccl_loopback_reference_order(loop, oracle, gpu, P, dt, algo):
     assert _pairs(lib, P) > before  # the bytes really went through RCCL
 
 
+@pytest.mark.parametrize('P', [17, 20, 33])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE], ids=lambda d: NAME[d])
+@pytest.mark.parametrize('algo', [1, 2, 3])
+def test_rccl_loopback_reference_order_beyond_16(loop, oracle, gpu, P, dt, algo):
+    """More than 16 ranks over the RCCL transport: the fold is split into <= 16-input steps
+    through staging partials (plan_fold: MPICH's trees restricted to aligned blocks) and still
+    equals MPICH's order bit for bit on every rank — both sides of the 2048-byte switch."""
+    lib = loop
+    with config(lib, algo=algo, reference_order=1, tune=0, slice_bytes=64 << 10):
+        for n in (3, 300, 4099, 70_001):
+            xs = [random_input(dt, n, 31 * algo + 555 + 7919 * r + n) for r in range(P)]
+            want = oracle.fold_ref_order(dt, xs)
+            for r, o in enumerate(run_loop(lib, gpu, xs, dt)):
+                assert o.tobytes() == want.tobytes(), (n, r)
+
+
 @pytest.mark.parametrize('P', [3, 5, 8])
 @pytest.mark.parametrize('dt', [DT_FLOAT, DT_INT32, DT_HALF], ids=lambda d: NAME[d])
 def test_rccl_loopback_ring_order(loop, oracle, gpu, P, dt):
