@@ -771,6 +771,14 @@ def multi_gpu(args):
             out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['fusion_c5'] = repr(e)[:400]
+    # the deployment case at N ranks: C5's buckets as pinned host tensors through the keyed path
+    # (host pack -> H2D -> allreduce over xGMI -> unpack kernel into the tensors over PCIe)
+    state['leg'] = 'keyed_host_c5_pinned'
+    try:
+        if not args.no_fusion and not args.no_host:
+            out['keyed_host_c5_pinned'] = keyed_host_c5(lib, comm, steps=2, pinned=True)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['keyed_host_c5_pinned'] = repr(e)[:400]
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
     # size class) next to RCCL's own ncclAllReduce on the same buffers
     state['leg'] = 'size_sweep'
