@@ -271,6 +271,9 @@ def single_gpu(args):
         extra['fold_kernel'] = fold_roofline(lib, dev, sh, S)
         # the fold the reference-order direct schedule runs at P = 8 (MPICH's pre-fold + tree)
         extra['fold_kernel_reference_order'] = fold_roofline(lib, dev, sh, S, order=1)
+        # C4's fold: one 16 MiB fp16 bucket at P = 8 -> 2 MiB chunk, 7 received inputs (cache-resident
+        # operands, as RCCL has just written them)
+        extra['fold_kernel_fp16_c4'] = fold_roofline(lib, dev, sh, 16 << 20, half=True)
         extra['reduce_half_dtypes_achieved_GBs'] = half_dtypes(lib, dev, sh, S)
 
     traffic = pmc_traffic(f'reduce_fp32_{args.bucket_mib}MiB')
@@ -313,20 +316,23 @@ def single_gpu(args):
     emit(out)
 
 
-def fold_roofline(lib, dev, sh, S, nb=7, order=0):
+def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False):
     """k_sumN_tile<float, 7>: out = in + 7 received slices over one P=8 chunk (S/8 fp32), the
     direct schedule's reduce; algorithmic bytes (nb + 2) * chunk. order 0: left fold; 1: MPICH's
-    pre-fold + pairwise tree (reference_order at P = 8)."""
+    pre-fold + pairwise tree (reference_order at P = 8). `half`: the fp16 fold of C4 (inputs
+    widened to fp32, one rounding)."""
     import torch
     from ddl.torch.cpp_backend import check
-    n = S // 8 // 4
-    sets = [[torch.rand(n, device=dev) for _ in range(nb + 2)] for _ in range(2)]  # in, 7 inputs, out
+    es = 2 if half else 4
+    n = S // 8 // es
+    sets = [[torch.rand(n, device=dev).to(torch.float16 if half else torch.float32) for _ in range(nb + 2)]
+            for _ in range(2)]  # in, 7 inputs, out
     P = ctypes.c_void_p * nb
 
     def run(k):
         b = sets[k % 2]
         check(lib.ddl_reduce_fold_ordered(b[-1].data_ptr(), b[0].data_ptr(), P(*[t.data_ptr() for t in b[1:-1]]),
-                                          nb, n, DT_FLOAT, order, sh), 'ddl_reduce_fold_ordered')
+                                          nb, n, 19 if half else DT_FLOAT, order, sh), 'ddl_reduce_fold_ordered')
     for k in range(4):
         run(k)
     best = float('inf')
@@ -338,11 +344,12 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0):
         e1.record()
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
-    byts = (nb + 2) * n * 4
-    return {'kernel': f'k_sumN_tile<DDL_FLOAT,{nb},order {order}>', 'chunk_bytes': n * 4, 'us': round(best * 1e6, 1),
+    byts = (nb + 2) * n * es
+    return {'kernel': f'k_sumN_tile<{"DDL_HALF" if half else "DDL_FLOAT"},{nb},order {order}>', 'chunk_bytes': n * es,
+            'us': round(best * 1e6, 1),
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
             'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
-            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 and order == 0 else None}
+            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 and order == 0 and not half else None}
 
 
 def half_dtypes(lib, dev, sh, S):
