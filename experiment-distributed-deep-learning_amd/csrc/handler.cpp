@@ -612,8 +612,8 @@ size_t seg_starts(const std::vector<Seg> &segs, bool padded, std::vector<size_t>
 }
 
 // Host range [p, p + bytes) is pinned memory the device reaches at the same address, inside one
-// allocation, 16-byte aligned (the pack kernel's vector path). A failed query (pageable memory)
-// leaves no sticky error behind.
+// allocation, 16-byte aligned (the unpack kernel's vector path; byte stores over PCIe would
+// crawl). A failed query (pageable memory) leaves no sticky error behind.
 bool mapped_host_range(const void *p, size_t bytes) {
     if (bytes == 0) return true;
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15u) != 0) return false;
