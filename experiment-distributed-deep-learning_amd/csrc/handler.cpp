@@ -341,7 +341,7 @@ void RequestHandler::main_() {
                         if (kv.first.order == pending_.begin()->first.order) keys.push_back(kv.first);
                 }
                 if (P == 1) execute_(keys);
-                else root_round_();
+                else root_round_();  // negotiation lap times: DDL_LOG level 3 in root_round_
             } else {
                 Token t;
                 bool got = ch->recv(t, 50);
@@ -1131,6 +1131,10 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
 
 void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     if (ids.empty()) return;
+    // phase times of the round at log level 2 (take / enqueue / wait + done, microseconds)
+    using clk = std::chrono::steady_clock;
+    const bool timed = log_level() >= 2;
+    const clk::time_point t0 = timed ? clk::now() : clk::time_point();
     std::vector<Request> reqs;
     reqs.reserve(ids.size());
     {
@@ -1156,6 +1160,8 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     std::vector<Done> dones;
     size_t nplans = 0;
     int status = DDL_STATUS_OK;
+    const clk::time_point t1 = timed ? clk::now() : clk::time_point();
+    clk::time_point t2;
     try {
         for (const Request &r : reqs)
             DDL_REQUIRE(r.type == reqs[0].type, DDL_STATUS_COMM_ERROR, "agreed requests of mixed types");
@@ -1169,6 +1175,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
         DDL_LOG(0, "collective of agreed requests failed: " << e.msg);
         status = e.status;
     }
+    if (timed) t2 = clk::now();
     // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725)
     std::vector<char> fired(reqs.size(), 0);
     size_t synced = kNoPlan;  // dones are in plan order: wait for each plan's event once
@@ -1189,6 +1196,13 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
         inflight_ -= reqs.size();
     }
     idle_cv_.notify_all();
+    if (timed) {
+        auto us = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+        };
+        DDL_LOG(2, "round: " << reqs.size() << " requests, " << nplans << " plans; take " << us(t0, t1) << " us, enqueue "
+                             << us(t1, t2) << " us, wait + done " << us(t2, clk::now()) << " us");
+    }
     if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
 }
 
