@@ -7,16 +7,17 @@ autotuner's agreement (ncclAllReduce(MAX)) at size 1.
 
 Bar: bit-exact vs the oracle — MPICH 3.3.2's order (ddlo_fold_ref_order) with reference_order
 (default), the ring-order restatement with reference_order 0, MPI_Bcast / MPI_Allgatherv
-restatements for the data-movement collectives — at P = 3, 5, 8, fp32 / fp64 / int32, on both
-sides of MPICH's 2048-byte switch, in and out of place, every schedule."""
+restatements for the data-movement collectives — at P = 3, 5, 8, fp32 / fp64 / int32 / int64 /
+uint64, on both sides of MPICH's 2048-byte switch, in and out of place, every schedule; P = 17,
+20, 33 for the folds split beyond 16 inputs."""
 import ctypes
 
 import numpy as np
 import pytest
 import torch
 
-from _helpers import (DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, config, random_input, ring_perms,
-                      ring_shape)
+from _helpers import (DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, DT_INT64, DT_UINT64, NAME, config, random_input,
+                      ring_perms, ring_shape)
 
 pytestmark = pytest.mark.gpu
 
@@ -52,7 +53,7 @@ def _pairs(lib, P):
 
 
 @pytest.mark.parametrize('P', [3, 5, 8])
-@pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32], ids=lambda d: NAME[d])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_UINT64], ids=lambda d: NAME[d])
 @pytest.mark.parametrize('algo', [0, 1, 2, 3, 4])
 def test_rccl_loopback_reference_order(loop, oracle, gpu, P, dt, algo):
     """Default reference order over the RCCL transport: every rank equals MPICH's order bit for
