@@ -42,21 +42,40 @@ void CallbackTransport::allgather(const GatherOp &g, hipStream_t stream) {
     group(ops, stream);
 }
 
+CallbackTransport::~CallbackTransport() {
+    if (pinned_) (void)hipHostFree(pinned_);
+}
+
 void CallbackTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     if (ops.empty()) return;
-    DDL_HIP(hipStreamSynchronize(stream));  // the sends' data and the receive buffers are ready
-    std::vector<std::vector<char>> host(ops.size());
-    std::vector<ddl_p2p_op> v(ops.size());
-    for (size_t i = 0; i < ops.size(); ++i) {
-        host[i].resize(ops[i].bytes);
-        if (ops[i].send && ops[i].bytes)
-            DDL_HIP(hipMemcpy(host[i].data(), ops[i].ptr, ops[i].bytes, hipMemcpyDeviceToHost));
-        v[i] = ddl_p2p_op{ops[i].send ? 1 : 0, ops[i].peer, ops[i].tag, host[i].data(), ops[i].bytes};
+    // copies through pinned memory, ordered on `stream` only: a synchronous or pageable copy
+    // would also wait for what the caller's framework queued on the default stream (the rest
+    // of a backward pass, say)
+    size_t need = 0;
+    for (const P2POp &op : ops) need += (op.bytes + 255) & ~size_t(255);
+    if (need > pinned_bytes_) {
+        DDL_HIP(hipStreamSynchronize(stream));
+        if (pinned_) DDL_HIP(hipHostFree(pinned_));
+        pinned_ = nullptr;
+        pinned_bytes_ = 0;
+        DDL_HIP(hipHostMalloc(&pinned_, need, hipHostMallocDefault));
+        pinned_bytes_ = need;
     }
+    std::vector<ddl_p2p_op> v(ops.size());
+    std::vector<char *> host(ops.size());
+    for (size_t i = 0, off = 0; i < ops.size(); ++i) {
+        host[i] = pinned_ + off;
+        off += (ops[i].bytes + 255) & ~size_t(255);
+        if (ops[i].send && ops[i].bytes)
+            DDL_HIP(hipMemcpyAsync(host[i], ops[i].ptr, ops[i].bytes, hipMemcpyDeviceToHost, stream));
+        v[i] = ddl_p2p_op{ops[i].send ? 1 : 0, ops[i].peer, ops[i].tag, host[i], ops[i].bytes};
+    }
+    DDL_HIP(hipStreamSynchronize(stream));  // the sends' data is on the host, the receive buffers free
     host_group(v);
     for (size_t i = 0; i < ops.size(); ++i)
         if (!ops[i].send && ops[i].bytes)
-            DDL_HIP(hipMemcpy(ops[i].ptr, host[i].data(), ops[i].bytes, hipMemcpyHostToDevice));
+            DDL_HIP(hipMemcpyAsync(ops[i].ptr, host[i], ops[i].bytes, hipMemcpyHostToDevice, stream));
+    DDL_HIP(hipStreamSynchronize(stream));  // the pinned buffer is reused by the next group
 }
 
 void CallbackTransport::host_group(std::vector<ddl_p2p_op> &ops) {

@@ -57,8 +57,9 @@ struct TestHooks {
     std::atomic<long long> next_tag{1};  // communicator tags: 0 = world, then splits in order
 };
 
-// Synchronises the stream, stages the sends in host memory, runs the callback, copies the
-// received bytes to the device: the group is complete, in stream order, when group() returns.
+// Stages the sends in pinned host memory (copies ordered on the group's stream only),
+// synchronises that stream, runs the callback, copies the received bytes to the device: the
+// group is complete, in stream order, when group() returns.
 // Peers are ranks of the communicator; the callback sees world ranks (world_ranks[peer], or the
 // peer itself when world_ranks is empty).
 class CallbackTransport : public Transport {
@@ -72,12 +73,17 @@ public:
     bool capturable() const override { return false; }
     // One group of host-buffer operations straight to the callback (no device staging).
     void host_group(std::vector<ddl_p2p_op> &ops);
+    ~CallbackTransport() override;
+    CallbackTransport(const CallbackTransport &) = delete;
+    CallbackTransport &operator=(const CallbackTransport &) = delete;
 
 private:
     std::shared_ptr<TestHooks> hooks_;
     long long tag_;
     std::vector<int> world_ranks_;
     int rank_, size_;
+    char *pinned_ = nullptr;  // host side of a group's device buffers (pinned: truly async copies)
+    size_t pinned_bytes_ = 0;
 };
 
 // Streams, events and staging memory of one rank (reused across calls).

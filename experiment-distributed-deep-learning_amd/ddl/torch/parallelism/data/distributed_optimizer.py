@@ -19,8 +19,10 @@ Overlap with backward (`overlap_backward=True`): a post-accumulate-grad hook on 
 submits its keyed allreduce the moment autograd has finished its gradient, so the engine
 negotiates and reduces the late layers' gradients while the early layers' are still being
 computed (the reference's graph lets TF schedule each Allreduce op as soon as its input exists);
-step() only waits for them. Gradient accumulation over several backward passes: run all but the
-last inside `no_sync()`, as with torch DDP.
+step() only waits for them. The keys count backwards from the last parameter and the fusion
+plans are capped at `bucket_bytes`, so a round's plans run in backward order, each as soon as its
+own gradients are ready (DDP-style buckets). Gradient accumulation over several backward passes:
+run all but the last inside `no_sync()`, as with torch DDP.
 """
 import contextlib
 import functools
@@ -46,10 +48,16 @@ class DataParallelismDistributedOptimizer:
         return self.communicator or Communicator.world()
 
     def _register_overlap_hooks(self) -> None:
+        # keys numbered from the last parameter back: the engine runs a round's plans in key
+        # order, so the plans holding the gradients autograd produces first go first, each
+        # waiting only for its own gradients (a sequential model's backward runs in reverse
+        # parameter order)
         self._grad_handles = {}
-        self._hooks = [p.register_post_accumulate_grad_hook(functools.partial(self._grad_ready, self._key(gi, pi)))
-                       for gi, group in enumerate(self.param_groups)
-                       for pi, p in enumerate(group['params']) if p.requires_grad]
+        params = [p for group in self.param_groups for p in group['params'] if p.requires_grad]
+        self._hooks = [
+            p.register_post_accumulate_grad_hook(functools.partial(
+                self._grad_ready, f'{self._ddl_name}/{type(self).__name__}/Allreduce/backward{len(params) - 1 - i:05d}'))
+            for i, p in enumerate(params)]
 
     def _grad_ready(self, key: str, p: torch.Tensor) -> None:
         g = p.grad
@@ -146,12 +154,16 @@ def data_parallelism_distributed_optimizer_wrapper(
         optimizer: torch.optim.Optimizer,
         communicator: Communicator = None,
         pin_host_gradients: bool = True,
-        overlap_backward: bool = False) -> torch.optim.Optimizer:
+        overlap_backward: bool = False,
+        bucket_bytes: int = 32 << 20) -> torch.optim.Optimizer:
     """Return an optimizer of a subclass of `type(optimizer)` whose step() first averages the
     gradients across `communicator` (default: the world). Parameter groups and state are
     shared with `optimizer`. `pin_host_gradients`: keep CPU gradients in pinned memory;
     `overlap_backward`: submit each gradient's allreduce from a backward hook (module
-    docstring)."""
+    docstring) and cap the engine's fusion plans at `bucket_bytes` (the engine-wide
+    `fusion_threshold_bytes`, so every rank must build the wrapper the same way; None keeps the
+    configured cap): a round's gradients then reduce as several plans in backward order, each
+    starting once its own gradients exist."""
     opt_cls = optimizer.__class__
     assert issubclass(opt_cls, torch.optim.Optimizer)
     cls = type(opt_cls.__name__, (DataParallelismDistributedOptimizer, opt_cls), {})
@@ -160,5 +172,8 @@ def data_parallelism_distributed_optimizer_wrapper(
     res.communicator = communicator
     res.pin_host_gradients = pin_host_gradients
     if overlap_backward:
+        if bucket_bytes:
+            from ddl.torch import config
+            config.set('fusion_threshold_bytes', int(bucket_bytes))
         res._register_overlap_hooks()
     return res

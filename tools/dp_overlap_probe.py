@@ -3,8 +3,9 @@
 over the test-harness transport (point-to-point through gloo on host copies, tools/
 gloo_transport.py — not xGMI): a data-parallel MLP step (8 x Linear(1024, 1024), batch 16384,
 fp32) with the DP wrapper submitting every gradient at step() (overlap off) or from its backward
-hook (overlap on). Two identically initialised replicas, interleaved rounds; rank 0 prints the
-step times and checks both replicas stay equal.
+hook in 8 MiB buckets (overlap on; the cap applies to both replicas' fusion plans). Two
+identically initialised replicas, interleaved rounds; rank 0 prints the step times, the compute
+and the allreduce alone, and whether both replicas stay equal.
 
     python tools/dp_overlap_probe.py > gpurun_out/dp_overlap.json
 """
@@ -18,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), os.path.join(ROOT, 'tools')):
     sys.path.insert(0, p)
 
-WIDTH, LAYERS, BATCH, STEPS, ROUNDS = 1024, 8, 16384, 4, 3
+WIDTH, LAYERS, BATCH, STEPS, ROUNDS, BUCKET = 1024, 8, 16384, 4, 3, 8 << 20
 
 
 def worker(rank, world, port, q):
@@ -46,8 +47,10 @@ def worker(rank, world, port, q):
             layers += [torch.nn.Linear(WIDTH, WIDTH), torch.nn.ReLU()]
         return torch.nn.Sequential(*layers).cuda()
     models = {False: model_fn(), True: model_fn()}
+    # overlap on: 8 MiB buckets (two layers' gradients per plan), set before any step
     opts = {ov: data_parallelism_distributed_optimizer_wrapper(torch.optim.SGD(m.parameters(), lr=1e-4), comm,
-                                                               overlap_backward=ov) for ov, m in models.items()}
+                                                               overlap_backward=ov, bucket_bytes=BUCKET)
+            for ov, m in models.items()}
     g = torch.Generator(device='cuda').manual_seed(100 + rank)
     x = torch.randn(BATCH, WIDTH, device='cuda', generator=g)
     y = torch.randn(BATCH, WIDTH, device='cuda', generator=g)
@@ -57,10 +60,69 @@ def worker(rank, world, port, q):
         torch.nn.functional.mse_loss(models[ov](x), y).backward()
         opts[ov].step()
 
-    times = {False: [], True: []}
+    plain = model_fn()  # the same step without any communication (compute alone)
+    plain_opt = torch.optim.SGD(plain.parameters(), lr=1e-4)
+
+    def step_plain():
+        plain_opt.zero_grad()
+        torch.nn.functional.mse_loss(plain(x), y).backward()
+        plain_opt.step()
+
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    grads = [p.grad.clone() if p.grad is not None else torch.zeros_like(p) for p in models[False].parameters()]
+
+    def step_comm():  # the gradients' allreduce alone (one batch)
+        for h in allreduce_async_batch(grads, [f'comm_only/{i}' for i in range(len(grads))], comm, outputs=grads):
+            h.wait()
+
+    times = {False: [], True: [], 'compute_only': [], 'comm_only': []}
     for ov in (False, True):  # warm-up (tuning-free: tune = 0)
         step(ov)
+    step_plain()
+    step_comm()
     torch.cuda.synchronize()
+    lib.ddl_set_config(b'log_level', 2)  # the engine's round lines of one overlapped step
+    # host timeline of that step: when the hooks submit, when backward() returns, when the GPU
+    # has finished the backward (an event on the default stream), when step() returns
+    marks = []
+    hook_ts = []
+    orig = opts[True]._grad_ready
+    def stamped(key, p):
+        hook_ts.append(time.perf_counter())
+        orig(key, p)
+    opts[True]._grad_ready = stamped
+    for h in opts[True]._hooks:
+        h.remove()
+    opts[True]._register_overlap_hooks()
+    opts[True].zero_grad()
+    t0 = time.perf_counter()
+    loss = torch.nn.functional.mse_loss(models[True](x), y)
+    ev = torch.cuda.Event()
+    loss.backward()
+    marks.append(('backward_returned', time.perf_counter()))
+    ev.record()
+    opts[True].step()
+    marks.append(('step_returned', time.perf_counter()))
+    ev.synchronize()
+    marks.append(('gpu_backward_done_seen', time.perf_counter()))
+    torch.cuda.synchronize()
+    lib.ddl_set_config(b'log_level', 0)
+    opts[True]._grad_ready = orig
+    for h in opts[True]._hooks:
+        h.remove()
+    opts[True]._register_overlap_hooks()
+    timeline = {'first_hook_ms': round((hook_ts[0] - t0) * 1e3, 2), 'last_hook_ms': round((hook_ts[-1] - t0) * 1e3, 2),
+                'hooks': len(hook_ts)}
+    timeline.update({k: round((v - t0) * 1e3, 2) for k, v in marks})
+    for _ in range(ROUNDS):
+        for name, fn in (('compute_only', step_plain), ('comm_only', step_comm)):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(STEPS):
+                fn()
+            torch.cuda.synchronize()
+            times[name].append((time.perf_counter() - t0) / STEPS * 1e3)
     for _ in range(ROUNDS):
         for ov in (False, True):
             dist.barrier()
@@ -73,7 +135,7 @@ def worker(rank, world, port, q):
     same = all(torch.equal(a, b) for a, b in zip(models[False].parameters(), models[True].parameters()))
     dist.barrier()
     finalize()
-    q.put((rank, times, same))
+    q.put((rank, times, same, timeline))
 
 
 def main():
@@ -87,16 +149,18 @@ def main():
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (t, same)) for r, t, same in (q.get(timeout=600) for _ in range(world)))
+    res = dict((r, (t, same, tl)) for r, t, same, tl in (q.get(timeout=600) for _ in range(world)))
     for p in procs:
         p.join(timeout=30)
-    t, same = res[0]
+    t, same, tl = res[0]
     grad_mib = LAYERS * (WIDTH * WIDTH + WIDTH) * 4 / 2 ** 20
     print(json.dumps({'probe': 'dp_overlap_backward', 'ranks': world, 'transport': 'test harness: gloo over host copies',
                       'model': f'{LAYERS} x Linear({WIDTH},{WIDTH}) fp32, batch {BATCH}', 'grad_MiB': round(grad_mib, 1),
                       'ms_per_step_overlap_off': [round(v, 2) for v in t[False]],
                       'ms_per_step_overlap_on': [round(v, 2) for v in t[True]],
-                      'replicas_equal': same}), flush=True)
+                      'ms_compute_only': [round(v, 2) for v in t['compute_only']],
+                      'ms_allreduce_only': [round(v, 2) for v in t['comm_only']],
+                      'replicas_equal': same, 'rank0_timeline_ms': tl}), flush=True)
 
 
 if __name__ == '__main__':
