@@ -463,6 +463,44 @@ def fusion_c5(lib, comm, dev, steps, k=4096, forced=True):
     return res
 
 
+def keyed_bucket_stream(lib, comm, dev, steps, buckets=32, bucket_bytes=8 << 20):
+    """DDP-style gradient buckets through the keyed path: `buckets` fp32 buckets of
+    `bucket_bytes` (256 MiB in all, the C3 size), each submitted by its own call as a backward
+    pass would (so each is its own negotiated round), then one wait — with pipeline_rounds 1 (a
+    completion thread fires round n's done() while round n+1 negotiates and enqueues) and 0 (each
+    round waited for before the next is negotiated)."""
+    import torch
+    from ddl.torch.cpp_backend import DONE_FN, check
+    ts = [torch.randn(bucket_bytes // 4, device=dev) for _ in range(buckets)]
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    nodone = DONE_FN()
+
+    def step():
+        for i, t in enumerate(ts):
+            check(lib.ddl_allreduce_submit(comm.id, f'bucket_{i:03d}'.encode(), t.data_ptr(), t.data_ptr(), t.numel(),
+                                           1, 0, sh, nodone, None), 'ddl_allreduce_submit')
+        check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
+
+    res = {'buckets': buckets, 'bucket_bytes': bucket_bytes}
+    old = lib.ddl_get_config(b'pipeline_rounds')
+    try:
+        for pipelined in (1, 0):
+            check(lib.ddl_set_config(b'pipeline_rounds', pipelined), 'ddl_set_config')
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            dt = (time.perf_counter() - t0) / steps
+            tag = 'pipelined' if pipelined else 'unpipelined'
+            res[f'{tag}_ms'] = round(dt * 1e3, 3)
+            res[f'{tag}_algbw_GiBs'] = round(buckets * bucket_bytes / GiB / dt, 2)
+    finally:
+        lib.ddl_set_config(b'pipeline_rounds', old)
+    del ts
+    return res
+
+
 def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
     buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks
@@ -778,6 +816,12 @@ def multi_gpu(args):
             out['fusion_c5'] = fusion_c5(lib, comm, dev, steps=3)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['fusion_c5'] = repr(e)[:400]
+    state['leg'] = 'keyed_bucket_stream'
+    try:
+        if not args.no_fusion:
+            out['keyed_bucket_stream'] = keyed_bucket_stream(lib, comm, dev, steps=3)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['keyed_bucket_stream'] = repr(e)[:400]
     # the deployment case at N ranks: C5's buckets as pinned host tensors through the keyed path
     # (host pack -> H2D -> allreduce over xGMI -> unpack kernel into the tensors over PCIe)
     state['leg'] = 'keyed_host_c5_pinned'

@@ -321,6 +321,7 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
             c.fusion_pipeline_bytes = value;
         } else if (k == "one_rank_shortcut") c.one_rank_shortcut = value ? 1 : 0;
+        else if (k == "pipeline_rounds") c.pipeline_rounds = value ? 1 : 0;
         else if (k == "reference_order") c.reference_order = value ? 1 : 0;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
@@ -345,6 +346,7 @@ long long ddl_get_config(const char *key) {
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
+    if (k == "pipeline_rounds") return c.pipeline_rounds;
     if (k == "reference_order") return c.reference_order;
     return -1;
 }

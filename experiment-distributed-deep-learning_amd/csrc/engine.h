@@ -55,6 +55,11 @@ struct Config {
     // a one-rank world skips the keyed data plane (the sum is the input); 0 runs pack ->
     // allreduce -> unpack anyway (tests of the fusion path on one GPU)
     std::atomic<long long> one_rank_shortcut{1};
+    // keyed rounds: 1 — a completion thread waits for a round's data plane and fires its done()
+    // calls while the engine thread negotiates and enqueues the next round; 0 — the engine
+    // thread waits for each round before negotiating the next (as the reference's recv thread
+    // blocks in MPI_Allreduce)
+    std::atomic<long long> pipeline_rounds{1};
     // 1: every sum equals the reference's MPI_Allreduce (MPICH 3.3.2) bit for bit — direct /
     // one-shot folds in MPICH's order, the ring replaced by the direct schedule at P > 2
     // (RingConfig::ref_order); 0: ring order / left folds (error-bounded against the reference)

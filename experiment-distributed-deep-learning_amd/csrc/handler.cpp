@@ -191,6 +191,7 @@ RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
         data_ = owner_->shared_from_this();
     }
     DDL_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    done_thread_ = std::thread(&RequestHandler::completer_, this);
     thread_ = std::thread(&RequestHandler::main_, this);
 }
 
@@ -201,8 +202,14 @@ RequestHandler::~RequestHandler() {
     }
     cv_.notify_all();
     if (thread_.joinable()) thread_.join();
+    {  // the rounds already handed over complete (or fail) first, in order
+        std::lock_guard<std::mutex> g(done_mu_);
+        done_stop_ = true;
+    }
+    done_cv_.notify_all();
+    if (done_thread_.joinable()) done_thread_.join();
     fail_all_(DDL_STATUS_COMM_ERROR);
-    for (hipEvent_t e : plan_events_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     for (hipEvent_t e : pipe_events_) (void)hipEventDestroy(e);
     if (fusion_) (void)hipFree(fusion_);
     if (fusion2_) (void)hipFree(fusion2_);
@@ -330,7 +337,8 @@ void RequestHandler::main_() {
                 std::vector<ReqId> keys;
                 {
                     std::unique_lock<std::mutex> lk(mu_);
-                    cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
+                    cv_.wait(lk, [this] { return stop_ || failed_.load() || !pending_.empty(); });
+                    if (failed_.load()) fail(failed_.load(), "a keyed round failed on the device");
                     if (stop_) break;
                     // optional fusion window: let more registrations join this round
                     const long long cycle_us = config().cycle_time_us.load();
@@ -343,6 +351,7 @@ void RequestHandler::main_() {
                 if (P == 1) execute_(keys);
                 else root_round_();  // negotiation lap times: DDL_LOG level 3 in root_round_
             } else {
+                if (failed_.load()) fail(failed_.load(), "a keyed round failed on the device");
                 Token t;
                 bool got = ch->recv(t, 50);
                 if (!got) {
@@ -559,12 +568,17 @@ void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
 }
 
 size_t RequestHandler::record_plan_(size_t &nplans) {
-    if (plan_events_.size() <= nplans) {
-        hipEvent_t e;
-        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        plan_events_.push_back(e);
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(done_mu_);
+        if (!event_pool_.empty()) {
+            e = event_pool_.back();
+            event_pool_.pop_back();
+        }
     }
-    DDL_HIP(hipEventRecord(plan_events_[nplans], stream_));
+    if (!e) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    round_events_.push_back(e);
+    DDL_HIP(hipEventRecord(e, stream_));
     return nplans++;
 }
 
@@ -1161,7 +1175,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     size_t nplans = 0;
     int status = DDL_STATUS_OK;
     const clk::time_point t1 = timed ? clk::now() : clk::time_point();
-    clk::time_point t2;
+    round_events_.clear();
     try {
         for (const Request &r : reqs)
             DDL_REQUIRE(r.type == reqs[0].type, DDL_STATUS_COMM_ERROR, "agreed requests of mixed types");
@@ -1175,35 +1189,99 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
         DDL_LOG(0, "collective of agreed requests failed: " << e.msg);
         status = e.status;
     }
-    if (timed) t2 = clk::now();
-    // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725)
-    std::vector<char> fired(reqs.size(), 0);
+    Round rd;
+    rd.reqs = std::move(reqs);
+    rd.dones = std::move(dones);
+    rd.events.swap(round_events_);
+    rd.status = status;
+    rd.nplans = nplans;
+    rd.t0 = t0;
+    rd.t1 = t1;
+    if (timed) rd.t2 = clk::now();
+    unsigned long long seq;
+    {
+        std::lock_guard<std::mutex> g(done_mu_);
+        rounds_.push_back(std::move(rd));
+        seq = ++rounds_queued_;
+    }
+    done_cv_.notify_all();
+    // pipelined: back to negotiating while the device runs this round; otherwise (and after a
+    // failed enqueue, whose done() calls must have fired before the handler stops) wait for it
+    if (status != DDL_STATUS_OK || !config().pipeline_rounds.load()) {
+        std::unique_lock<std::mutex> lk(done_mu_);
+        done_cv_.wait(lk, [&] { return rounds_done_ >= seq; });
+    }
+    if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
+}
+
+// done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725).
+void RequestHandler::complete_(Round &rd) {
+    using clk = std::chrono::steady_clock;
+    int status = rd.status;
+    std::vector<char> fired(rd.reqs.size(), 0);
     size_t synced = kNoPlan;  // dones are in plan order: wait for each plan's event once
-    for (const Done &d : dones) {
+    for (const Done &d : rd.dones) {
         if (status == DDL_STATUS_OK && d.plan != kNoPlan && d.plan != synced) {
-            hipError_t he = hipEventSynchronize(plan_events_[d.plan]);
+            hipError_t he = hipEventSynchronize(rd.events[d.plan]);
             if (he != hipSuccess) status = DDL_STATUS_HIP_ERROR;
             synced = d.plan;
         }
-        const Request &r = reqs[d.req];
+        const Request &r = rd.reqs[d.req];
         fired[d.req] = 1;
         if (r.done) r.done(status == DDL_STATUS_OK ? d.status : status, r.user);
     }
-    for (size_t i = 0; i < reqs.size(); ++i)
-        if (!fired[i] && reqs[i].done) reqs[i].done(status == DDL_STATUS_OK ? DDL_STATUS_ERROR_UNKNOWN : status, reqs[i].user);
+    for (size_t i = 0; i < rd.reqs.size(); ++i)
+        if (!fired[i] && rd.reqs[i].done)
+            rd.reqs[i].done(status == DDL_STATUS_OK ? DDL_STATUS_ERROR_UNKNOWN : status, rd.reqs[i].user);
+    if (status == DDL_STATUS_OK) {  // waited for: safe to record again
+        std::lock_guard<std::mutex> g(done_mu_);
+        event_pool_.insert(event_pool_.end(), rd.events.begin(), rd.events.end());
+    } else {
+        for (hipEvent_t e : rd.events) (void)hipEventDestroy(e);
+        if (rd.status == DDL_STATUS_OK) {  // a device failure the engine thread has not seen
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                int expected = 0;
+                failed_.compare_exchange_strong(expected, status);
+            }
+            cv_.notify_all();
+        }
+    }
+    rd.events.clear();
+    const size_t n = rd.reqs.size();
+    rd.reqs.clear();  // the requests' input-ready events go with them
     {
         std::lock_guard<std::mutex> g(mu_);
-        inflight_ -= reqs.size();
+        inflight_ -= n;
     }
     idle_cv_.notify_all();
-    if (timed) {
+    if (log_level() >= 2 && rd.t0 != clk::time_point()) {
         auto us = [](clk::time_point a, clk::time_point b) {
             return std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
         };
-        DDL_LOG(2, "round: " << reqs.size() << " requests, " << nplans << " plans; take " << us(t0, t1) << " us, enqueue "
-                             << us(t1, t2) << " us, wait + done " << us(t2, clk::now()) << " us");
+        DDL_LOG(2, "round: " << n << " requests, " << rd.nplans << " plans; take " << us(rd.t0, rd.t1) << " us, enqueue "
+                             << us(rd.t1, rd.t2) << " us, wait + done " << us(rd.t2, clk::now()) << " us");
     }
-    if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
+}
+
+void RequestHandler::completer_() {
+    (void)hipSetDevice(owner_->device());
+    for (;;) {
+        Round rd;
+        {
+            std::unique_lock<std::mutex> lk(done_mu_);
+            done_cv_.wait(lk, [this] { return done_stop_ || !rounds_.empty(); });
+            if (rounds_.empty()) break;  // stopping, and every handed-over round has completed
+            rd = std::move(rounds_.front());
+            rounds_.pop_front();
+        }
+        complete_(rd);
+        {
+            std::lock_guard<std::mutex> g(done_mu_);
+            ++rounds_done_;
+        }
+        done_cv_.notify_all();
+    }
 }
 
 }  // namespace ddl

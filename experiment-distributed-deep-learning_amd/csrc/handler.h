@@ -17,7 +17,10 @@
 // runs on a private RCCL communicator so user-level ddl_allreduce calls never interleave.
 #pragma once
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -160,12 +163,28 @@ private:
     void forget_ids_();                                 // the id table was cleared
     void mark_cached_(const ReqId &id, Request &r);
     struct Done {
-        size_t plan;  // index into plan_events_ (kNoPlan: nothing to wait for)
+        size_t plan;  // index into the round's plan events (kNoPlan: nothing to wait for)
         size_t req;
         int status;
     };
     static constexpr size_t kNoPlan = (size_t)-1;
-    size_t record_plan_(size_t &nplans);  // records the next plan event on stream_
+    // One executed round: its requests, their done() order, the plan events they wait for.
+    // The engine thread enqueues the round's data plane and hands it to the completion thread,
+    // which waits for each plan's event and fires done() in plan order, rounds in FIFO order;
+    // meanwhile the engine thread negotiates the next round (pipeline_rounds = 1). The
+    // reference's recv thread blocks in MPI_Allreduce instead (MPIRingTokenCommunication.cc:
+    // 548-733); pipeline_rounds = 0 waits the same way.
+    struct Round {
+        std::vector<Request> reqs;
+        std::vector<Done> dones;
+        std::vector<hipEvent_t> events;
+        int status = 0;
+        size_t nplans = 0;
+        std::chrono::steady_clock::time_point t0, t1, t2;  // take / enqueue phase bounds (log)
+    };
+    size_t record_plan_(size_t &nplans);  // records the round's next plan event on stream_
+    void complete_(Round &rd);            // waits the plan events, fires done(), frees the events
+    void completer_();                    // the completion thread
     void wait_inputs_(const Request &r, std::vector<hipEvent_t> &waited);
     void *ensure_(void *&buf, size_t &cap, size_t need);
     void allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
@@ -221,7 +240,7 @@ private:
     void *dims_ = nullptr;    // allgather first-dim exchange
     size_t dims_bytes_ = 0;
     SegmentCopier copier_;
-    std::vector<hipEvent_t> plan_events_;
+    std::vector<hipEvent_t> round_events_;  // plan events of the round being enqueued (engine thread)
     static constexpr int kHostSlots = 4;
     void *pin_[kHostSlots] = {};    // pinned host staging slots
     void *dslot_[kHostSlots] = {};  // device slots
@@ -244,7 +263,17 @@ private:
     std::vector<uint8_t> pend_flag_;
     size_t inflight_ = 0;
     bool stop_ = false;
+    std::atomic<int> failed_{0};  // a completion failed: the engine thread stops with this status
     std::thread thread_;
+    // completion thread state (done_mu_): executed rounds waiting for their events, free plan
+    // events (returned once waited for, so none is re-recorded while still pending)
+    std::mutex done_mu_;
+    std::condition_variable done_cv_;
+    std::deque<Round> rounds_;
+    std::vector<hipEvent_t> event_pool_;
+    unsigned long long rounds_queued_ = 0, rounds_done_ = 0;
+    bool done_stop_ = false;
+    std::thread done_thread_;
 };
 
 }  // namespace ddl

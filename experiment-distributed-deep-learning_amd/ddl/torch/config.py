@@ -15,7 +15,8 @@ import contextlib
 from ddl.torch.cpp_backend import CPPBackend, check
 
 KEYS = ('algo', 'slice_bytes', 'rings', 'max_slices', 'fusion_threshold_bytes', 'log_level', 'cycle_time_us',
-        'host_chunk_bytes', 'host_copy_threads', 'host_zero_copy', 'tune', 'fusion_pipeline_bytes', 'one_rank_shortcut', 'reference_order')
+        'host_chunk_bytes', 'host_copy_threads', 'host_zero_copy', 'tune', 'fusion_pipeline_bytes', 'one_rank_shortcut', 'pipeline_rounds',
+        'reference_order')
 
 
 def set(key: str, value: int) -> None:  # noqa: A001 (mirrors ddl_set_config)

@@ -159,7 +159,9 @@ int ddl_is_initialized(void);
  * read-only "host_zero_copy_plans" counts the plans that took that path),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
- * one-rank world skips the keyed data plane; 0: runs it, for tests), "reference_order" (1,
+ * one-rank world skips the keyed data plane; 0: runs it, for tests), "pipeline_rounds" (1,
+ * default: a completion thread fires a keyed round's done() calls as its plans land while the
+ * engine thread negotiates the next round; 0: each round is waited for first), "reference_order" (1,
  * default: every allreduce sum equals the reference's MPI_Allreduce — MPICH 3.3.2 — bit for
  * bit: the direct and one-shot folds add the P inputs in rank order in MPICH's tree, picked by
  * the message size, and "algo" 0 runs as the direct schedule at P > 2; 0: ring order and left

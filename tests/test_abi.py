@@ -60,6 +60,8 @@ def test_config_roundtrip(lib):
     assert lib.ddl_set_config(b'fusion_threshold_bytes', 0) == 3
     # the product default: sums bit-equal to the reference's MPI_Allreduce
     assert lib.ddl_get_config(b'reference_order') == 1
+    # keyed rounds pipelined by default (done() fired by the completion thread)
+    assert lib.ddl_get_config(b'pipeline_rounds') == 1
 
 
 def test_product_does_not_reference_oracle():

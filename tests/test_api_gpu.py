@@ -184,6 +184,82 @@ def test_done_callbacks_fire_in_reference_order(world, lib):
     assert len(order) == len(specs)
 
 
+@pytest.mark.parametrize('pipelined', [1, 0])
+def test_keyed_rounds_pipelined(world, lib, data_plane_at_one_rank, pipelined):
+    """Rounds back to back with the data plane on: with pipeline_rounds = 1 the completion
+    thread fires round n's done() calls while the engine thread takes and enqueues round n+1
+    (its pack / allreduce / unpack queued behind round n's on the same streams). Every output
+    equals its input, every done() fires once with status 0, and done() order across rounds is
+    the submission order (batches keyed so their keys sort in submission order, one dtype)."""
+    from ddl.torch import cpp_backend as cb
+    from ddl.torch.util import ddl_dtype
+    assert lib.ddl_set_config(b'pipeline_rounds', pipelined) == 0
+    order, statuses = [], []
+
+    @cb.DONE_FN
+    def done(status, user):
+        order.append(user)
+        statuses.append(status)
+
+    api = cb.CPPBackend.c_api()
+    stream = torch.cuda.current_stream()
+    rng = np.random.default_rng(11 + pipelined)
+    keep, want, uid = [], {}, 0
+    try:
+        for b in range(24):
+            k = int(rng.integers(1, 40))
+            ts = [torch.randn(int(rng.integers(1, 200_000)), device='cuda') for _ in range(k)]
+            outs = [t if j % 2 else torch.zeros_like(t) for j, t in enumerate(ts)]
+            keys = [f'round{b:03d}_{j:03d}'.encode() for j in range(k)]
+            V = ctypes.c_void_p * k
+            st = api.ddl_allreduce_submit_batch(
+                world.id, k, (ctypes.c_char_p * k)(*keys), V(*[t.data_ptr() for t in ts]),
+                V(*[o.data_ptr() for o in outs]), (ctypes.c_size_t * k)(*[t.numel() for t in ts]),
+                (ctypes.c_int * k)(*[ddl_dtype(t) for t in ts]), 0, stream.cuda_stream, done, None)
+            assert st == 0
+            # the batch's user pointers are None: identify by key order instead (one done per key)
+            for j in range(k):
+                want[uid] = (ts[j].clone(), outs[j])
+                uid += 1
+            keep.append((ts, outs))
+        assert api.ddl_wait_all(world.id) == 0
+    finally:
+        lib.ddl_set_config(b'pipeline_rounds', 1)
+    assert len(order) == uid and all(s == 0 for s in statuses)
+    torch.cuda.synchronize()
+    for w, o in want.values():
+        assert torch.equal(o, w)
+
+
+def test_keyed_rounds_pipelined_done_order(world, lib, data_plane_at_one_rank):
+    """done() across pipelined rounds in submission order: single-request submits, each its own
+    user value, keys sorting in submission order; batches of requests registered while earlier
+    rounds are still on the device."""
+    from ddl.torch import cpp_backend as cb
+    from ddl.torch.util import ddl_dtype
+    order, statuses = [], []
+
+    @cb.DONE_FN
+    def done(status, user):
+        statuses.append(status)
+        order.append(user)
+
+    api = cb.CPPBackend.c_api()
+    stream = torch.cuda.current_stream()
+    keep = []
+    n = 400
+    for i in range(n):
+        t = torch.full((int(1 + (i * 7919) % 300_000),), float(i), device='cuda')
+        keep.append(t)
+        assert api.ddl_allreduce_submit(world.id, f'ord{i:05d}'.encode(), t.data_ptr(), t.data_ptr(), t.numel(),
+                                        ddl_dtype(t), 0, stream.cuda_stream, done, i + 1) == 0
+    assert api.ddl_wait_all(world.id) == 0
+    assert order == list(range(1, n + 1)) and set(statuses) == {0}
+    torch.cuda.synchronize()
+    for i, t in enumerate(keep):
+        assert bool((t == float(i)).all())
+
+
 def test_dp_optimizer_wrapper_size1(world):
     from ddl.torch.parallelism.data import data_parallelism_distributed_optimizer_wrapper
     torch.manual_seed(0)

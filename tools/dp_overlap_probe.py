@@ -111,6 +111,7 @@ def worker(rank, world, port, q):
     for h in opts[True]._hooks:
         h.remove()
     opts[True]._register_overlap_hooks()
+    step(False)  # the other replica takes the same number of steps
     timeline = {'first_hook_ms': round((hook_ts[0] - t0) * 1e3, 2), 'last_hook_ms': round((hook_ts[-1] - t0) * 1e3, 2),
                 'hooks': len(hook_ts)}
     timeline.update({k: round((v - t0) * 1e3, 2) for k, v in marks})
