@@ -483,16 +483,26 @@ def keyed_bucket_stream(lib, comm, dev, steps, buckets=32, bucket_bytes=8 << 20)
 
     res = {'buckets': buckets, 'bucket_bytes': bucket_bytes}
     old = lib.ddl_get_config(b'pipeline_rounds')
+    sr, cr = ctypes.c_longlong(), ctypes.c_longlong()
+
+    def rounds():  # negotiation rounds of the world's token ring so far (N > 1)
+        check(lib.ddl_control_stats(ctypes.byref(sr), ctypes.byref(cr)), 'ddl_control_stats')
+        return sr.value + cr.value
+
     try:
         for pipelined in (1, 0):
             check(lib.ddl_set_config(b'pipeline_rounds', pipelined), 'ddl_set_config')
             step()
             torch.cuda.synchronize()
+            r0 = rounds()
             t0 = time.perf_counter()
             for _ in range(steps):
                 step()
             dt = (time.perf_counter() - t0) / steps
             tag = 'pipelined' if pipelined else 'unpipelined'
+            # buckets submitted while a round runs join the next one: fewer, larger rounds when
+            # the engine waits for each round
+            res[f'{tag}_rounds_per_step'] = round((rounds() - r0) / steps, 2)
             res[f'{tag}_ms'] = round(dt * 1e3, 3)
             res[f'{tag}_algbw_GiBs'] = round(buckets * bucket_bytes / GiB / dt, 2)
     finally:
