@@ -61,15 +61,24 @@ ControlChannel::~ControlChannel() { close_all(); }
 
 void ControlChannel::close_all() {
     cache.clear();
-    for (int *fd : {&listen_fd_, &send_fd_, &recv_fd_}) {
-        if (*fd >= 0) ::close(*fd);
-        *fd = -1;
-    }
+    if (listen_fd_ >= 0) ::close(listen_fd_);
+    listen_fd_ = -1;
+    for (int fd : fd_)
+        if (fd >= 0) ::close(fd);
+    fd_.clear();
+}
+
+bool ControlChannel::connected() const {
+    if (size_ <= 1 || fd_.empty()) return false;
+    if (rank_ != 0) return fd_[0] >= 0;
+    for (int r = 1; r < size_; ++r)
+        if (fd_[r] < 0) return false;
+    return true;
 }
 
 std::string ControlChannel::listen() {
     DDL_REQUIRE(listen_fd_ < 0, DDL_STATUS_INVALID_ARGUMENT, "control channel already listening");
-    // The token ring is a single-node, same-host channel: it binds to loopback. A deployment
+    // The token channel is a single-node, same-host channel: it binds to loopback. A deployment
     // that spans hosts opts in by naming the interface address in $DDL_CONTROL_HOST.
     const char *env = std::getenv("DDL_CONTROL_HOST");
     const std::string host = env && *env ? env : "127.0.0.1";
@@ -82,7 +91,7 @@ std::string ControlChannel::listen() {
     DDL_REQUIRE(listen_fd_ >= 0, DDL_STATUS_COMM_ERROR, "socket: " << std::strerror(errno));
     DDL_REQUIRE(::bind(listen_fd_, (sockaddr *)&a, sizeof a) == 0, DDL_STATUS_COMM_ERROR,
                 "bind " << host << ": " << std::strerror(errno));
-    DDL_REQUIRE(::listen(listen_fd_, 16) == 0, DDL_STATUS_COMM_ERROR, "listen: " << std::strerror(errno));
+    DDL_REQUIRE(::listen(listen_fd_, 128) == 0, DDL_STATUS_COMM_ERROR, "listen: " << std::strerror(errno));
     socklen_t len = sizeof a;
     getsockname(listen_fd_, (sockaddr *)&a, &len);
     return host + ":" + std::to_string(ntohs(a.sin_port));
@@ -96,82 +105,111 @@ void ControlChannel::connect(int rank, int size, const std::vector<std::string> 
     cache.clear();
     if (size == 1) return;
     DDL_REQUIRE(listen_fd_ >= 0, DDL_STATUS_INVALID_ARGUMENT, "ddl_control_listen must come first");
+    for (int fd : fd_)
+        if (fd >= 0) ::close(fd);
+    fd_.assign(rank == 0 ? size : 1, -1);
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
-    // 1) connect to the successor (its listener may not be accepting yet: retry)
-    std::string host;
-    int port = 0;
-    split_endpoint(eps[(rank + 1) % size], host, port);
-    for (;;) {
-        int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-        DDL_REQUIRE(fd >= 0, DDL_STATUS_COMM_ERROR, "socket: " << std::strerror(errno));
-        sockaddr_in a{};
-        a.sin_family = AF_INET;
-        a.sin_port = htons((uint16_t)port);
-        DDL_REQUIRE(inet_pton(AF_INET, host.c_str(), &a.sin_addr) == 1, DDL_STATUS_INVALID_ARGUMENT,
-                    "bad control host '" << host << "'");
-        if (::connect(fd, (sockaddr *)&a, sizeof a) == 0) {
-            tune(fd);
-            int32_t me = rank;
-            write_all(fd, &me, sizeof me);
-            send_fd_ = fd;
-            break;
-        }
-        ::close(fd);
-        DDL_REQUIRE(std::chrono::steady_clock::now() < deadline, DDL_STATUS_COMM_ERROR,
-                    "control connect to " << eps[(rank + 1) % size] << " timed out");
-        std::this_thread::sleep_for(std::chrono::milliseconds(5));
-    }
-    // 2) accept the predecessor (a connection announcing any other rank is dropped)
-    const int pred = (rank + size - 1) % size;
-    while (recv_fd_ < 0) {
-        pollfd p{listen_fd_, POLLIN, 0};
-        int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
-                       deadline - std::chrono::steady_clock::now()).count();
-        DDL_REQUIRE(left > 0, DDL_STATUS_COMM_ERROR, "control accept from rank " << pred << " timed out");
-        if (::poll(&p, 1, left) <= 0) continue;
-        int fd = ::accept(listen_fd_, nullptr, nullptr);
-        if (fd < 0) continue;
-        int32_t who = -1;
-        read_all(fd, &who, sizeof who);
-        if (who == pred) {
-            tune(fd);
-            recv_fd_ = fd;
-        } else {
+    if (rank != 0) {
+        // connect to rank 0 (its listener may not be accepting yet: retry)
+        std::string host;
+        int port = 0;
+        split_endpoint(eps[0], host, port);
+        for (;;) {
+            int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            DDL_REQUIRE(fd >= 0, DDL_STATUS_COMM_ERROR, "socket: " << std::strerror(errno));
+            sockaddr_in a{};
+            a.sin_family = AF_INET;
+            a.sin_port = htons((uint16_t)port);
+            DDL_REQUIRE(inet_pton(AF_INET, host.c_str(), &a.sin_addr) == 1, DDL_STATUS_INVALID_ARGUMENT,
+                        "bad control host '" << host << "'");
+            if (::connect(fd, (sockaddr *)&a, sizeof a) == 0) {
+                tune(fd);
+                int32_t me = rank;
+                write_all(fd, &me, sizeof me);
+                fd_[0] = fd;
+                break;
+            }
             ::close(fd);
+            DDL_REQUIRE(std::chrono::steady_clock::now() < deadline, DDL_STATUS_COMM_ERROR,
+                        "control connect to " << eps[0] << " timed out");
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        }
+    } else {
+        // accept every member (a connection announcing an unknown or repeated rank is dropped)
+        int missing = size - 1;
+        while (missing > 0) {
+            pollfd p{listen_fd_, POLLIN, 0};
+            int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                           deadline - std::chrono::steady_clock::now()).count();
+            DDL_REQUIRE(left > 0, DDL_STATUS_COMM_ERROR, "control accept: " << missing << " rank(s) missing");
+            if (::poll(&p, 1, left) <= 0) continue;
+            int fd = ::accept(listen_fd_, nullptr, nullptr);
+            if (fd < 0) continue;
+            int32_t who = -1;
+            read_all(fd, &who, sizeof who);
+            if (who >= 1 && who < size && fd_[who] < 0) {
+                tune(fd);
+                fd_[who] = fd;
+                --missing;
+            } else {
+                ::close(fd);
+            }
         }
     }
-    // the ring is complete: no further connections are accepted
+    // the star is complete: no further connections are accepted
     ::close(listen_fd_);
     listen_fd_ = -1;
 }
 
-void ControlChannel::send(const Token &t) {
+namespace {
+void send_token(int fd, const Token &t) {
     unsigned char hdr[10];
     uint64_t len = t.msg.size();
     hdr[0] = t.type;
     hdr[1] = t.request;
     std::memcpy(hdr + 2, &len, 8);  // host byte order, as the reference's MPI_Pack of size_t
-    write_all(send_fd_, hdr, sizeof hdr);
-    if (len) write_all(send_fd_, t.msg.data(), len);
+    write_all(fd, hdr, sizeof hdr);
+    if (len) write_all(fd, t.msg.data(), len);
 }
 
-bool ControlChannel::recv(Token &t, int timeout_ms) {
+bool recv_token(int fd, Token &t, int timeout_ms) {
     if (timeout_ms >= 0) {
-        pollfd p{recv_fd_, POLLIN, 0};
+        pollfd p{fd, POLLIN, 0};
         int r = ::poll(&p, 1, timeout_ms);
         if (r == 0) return false;
         DDL_REQUIRE(r > 0, DDL_STATUS_COMM_ERROR, "control poll: " << std::strerror(errno));
     }
     unsigned char hdr[10];
-    read_all(recv_fd_, hdr, sizeof hdr);
+    read_all(fd, hdr, sizeof hdr);
     uint64_t len;
     std::memcpy(&len, hdr + 2, 8);
     DDL_REQUIRE(len < (1ull << 32), DDL_STATUS_COMM_ERROR, "control token too long: " << len);
     t.type = hdr[0];
     t.request = hdr[1];
     t.msg.assign(len, '\0');
-    if (len) read_all(recv_fd_, &t.msg[0], len);
+    if (len) read_all(fd, &t.msg[0], len);
     return true;
+}
+}  // namespace
+
+void ControlChannel::send(const Token &t) {
+    DDL_REQUIRE(connected(), DDL_STATUS_NOT_INITIALIZED, "control channel not connected");
+    if (rank_ != 0) {
+        send_token(fd_[0], t);
+        return;
+    }
+    for (int r = 1; r < size_; ++r) send_token(fd_[r], t);
+}
+
+bool ControlChannel::recv(Token &t, int timeout_ms) {
+    DDL_REQUIRE(rank_ != 0 && connected(), DDL_STATUS_NOT_INITIALIZED, "control recv: not a connected member");
+    return recv_token(fd_[0], t, timeout_ms);
+}
+
+bool ControlChannel::recv_from(int from, Token &t, int timeout_ms) {
+    DDL_REQUIRE(rank_ == 0 && from >= 1 && from < size_ && connected(), DDL_STATUS_INVALID_ARGUMENT,
+                "control recv_from(" << from << ") on rank " << rank_);
+    return recv_token(fd_[from], t, timeout_ms);
 }
 
 bool IdCache::lookup(const std::string &id, uint32_t *idx) const {

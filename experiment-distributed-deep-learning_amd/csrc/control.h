@@ -1,10 +1,14 @@
-// control.h — host control channel: a ring of TCP links carrying negotiation tokens.
+// control.h — host control channel: TCP links carrying negotiation tokens.
 //
 // Replaces the reference's token transport over MPI point-to-point
-// (communicate/tensor/collective/controller/rtc/mpi/MPIRingTokenCommunication.cc:29-102):
-// every rank sends to rank+1 and receives from rank-1; a token on the wire is the same
-// packed header the reference sends with MPI_Pack — {u8 type, u8 request type, u64 length}
-// (10 bytes, :25,44-53) — followed by `length` bytes of key list.
+// (communicate/tensor/collective/controller/rtc/mpi/MPIRingTokenCommunication.cc:29-102). The
+// reference passes the token around a ring (rank -> rank+1), so a round's two laps cost 2P
+// hops. Here the links form a star around rank 0: rank 0 sends the proposal to every member,
+// each member answers with its intersection, rank 0 intersects the answers and sends the
+// agreed set to every member — 3 hops at any P, the members' hops in parallel (a single-key
+// round at P = 8 on 8 cores: 0.35 ms as a ring). A token on the wire is the same packed header
+// the reference sends with MPI_Pack — {u8 type, u8 request type, u64 length} (10 bytes,
+// :25,44-53) — followed by `length` bytes of key list.
 #pragma once
 
 #include <cstdint>
@@ -60,13 +64,18 @@ public:
     // Opens the listening socket; returns "host:port" (host from $DDL_CONTROL_HOST, default
     // 127.0.0.1 — one node).
     std::string listen();
-    // Connects to rank+1's endpoint and accepts rank-1's connection.
+    // Rank 0 accepts one connection from every other rank; the others connect to rank 0's
+    // endpoint (their own listeners are closed unused).
     void connect(int rank, int size, const std::vector<std::string> &endpoints, int timeout_ms);
-    bool connected() const { return send_fd_ >= 0 && recv_fd_ >= 0; }
+    bool connected() const;
 
+    // Member: to rank 0. Rank 0: to every member, in rank order.
     void send(const Token &t);
-    // Blocks until a token arrives, or returns false after timeout_ms (< 0: forever).
+    // Member: the next token from rank 0. Blocks until one arrives, or returns false after
+    // timeout_ms (< 0: forever).
     bool recv(Token &t, int timeout_ms);
+    // Rank 0: the next token from member `from` (1 .. size-1).
+    bool recv_from(int from, Token &t, int timeout_ms);
     int rank() const { return rank_; }
     int size() const { return size_; }
     void close_all();
@@ -76,7 +85,8 @@ public:
     long long cached_rounds = 0;
 
 private:
-    int listen_fd_ = -1, send_fd_ = -1, recv_fd_ = -1;
+    int listen_fd_ = -1;
+    std::vector<int> fd_;  // rank 0: fd_[r] links member r (fd_[0] unused); member: fd_[0] links rank 0
     int rank_ = 0, size_ = 1;
 };
 

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <iterator>
 #include <set>
 #include <tuple>
 
@@ -357,7 +358,7 @@ void RequestHandler::main_() {
                 if (!got) {
                     std::lock_guard<std::mutex> g(mu_);
                     if (stop_ && pending_.empty()) {
-                        // rank 0 shuts the ring down; keep listening a little for it
+                        // rank 0 shuts the channel down; keep listening a little for it
                         Token s;
                         if (ch->recv(s, 5000) && s.type == TOKEN_SHUT_DOWN) ch->send(s);
                         break;
@@ -365,20 +366,25 @@ void RequestHandler::main_() {
                     continue;
                 }
                 if (t.type == TOKEN_SHUT_DOWN) {
-                    ch->send(t);
+                    ch->send(t);  // the acknowledgement
                     break;
                 }
                 member_round_(t);
             }
         }
-        if (P > 1 && rank == 0) {  // SHUT_DOWN lap (RingTokenCommunicateHandler.cc:34-48)
-            Token s;
+        if (P > 1 && rank == 0) {  // SHUT_DOWN to every member, then their acknowledgements
+            Token s;                // (the reference's SHUT_DOWN lap, RingTokenCommunicateHandler.cc:34-48)
             s.type = TOKEN_SHUT_DOWN;
             s.request = TOKEN_REQUEST_SHUTDOWN;
             s.msg = "shut down";
             ch->send(s);
-            Token back;
-            while (ch->recv(back, 5000) && back.type != TOKEN_SHUT_DOWN) {
+            for (int r = 1; r < P; ++r) {
+                Token back;
+                try {
+                    while (ch->recv_from(r, back, 5000) && back.type != TOKEN_SHUT_DOWN) {
+                    }
+                } catch (const Error &) {  // a member that already left closed its link
+                }
             }
         }
     } catch (const Error &e) {
@@ -392,40 +398,72 @@ void RequestHandler::main_() {
     idle_cv_.notify_all();
 }
 
+namespace {
+// Rank 0's view of one round: the agreed set is the proposal's entries that every member kept.
+// String rounds: each answer is a subsequence of the proposal (members walk it in order).
+// Cached rounds: index sets.
+Agreed decide(bool cached, const std::vector<uint32_t> &idx, const std::vector<std::string> &strs,
+              const std::vector<Token> &answers, ControlChannel &ch) {
+    Agreed a;
+    a.cached = cached;
+    if (cached) {
+        std::vector<uint32_t> agreed(idx);
+        std::sort(agreed.begin(), agreed.end());
+        for (const Token &t : answers) {
+            std::vector<uint32_t> theirs = ch.cache.decode(t.msg);
+            std::sort(theirs.begin(), theirs.end());
+            std::vector<uint32_t> both;
+            std::set_intersection(agreed.begin(), agreed.end(), theirs.begin(), theirs.end(), std::back_inserter(both));
+            agreed.swap(both);
+        }
+        a.idx = std::move(agreed);
+        return a;
+    }
+    std::vector<int> kept(strs.size(), 0);
+    for (const Token &t : answers) {
+        size_t j = 0;
+        for (const std::string &k : decode_keys(t.msg)) {
+            while (j < strs.size() && strs[j] != k) ++j;
+            DDL_REQUIRE(j < strs.size(), DDL_STATUS_COMM_ERROR, "token protocol: answer '" << k << "' not proposed");
+            ++kept[j++];
+        }
+    }
+    for (size_t j = 0; j < strs.size(); ++j)
+        if (kept[j] == (int)answers.size()) a.wire.push_back(strs[j]);
+    return a;
+}
+}  // namespace
+
 Agreed negotiate_root(ControlChannel &ch, bool cached, const std::vector<uint32_t> &idx,
                       const std::vector<std::string> &strs, int request_type) {
     Token t;
     t.type = cached ? TOKEN_SYNC_CACHED : TOKEN_SYNC;
     t.request = (uint8_t)request_type;
     t.msg = cached ? ch.cache.encode(idx) : encode_keys(strs);
-    ch.send(t);
-    Token back;
-    ch.recv(back, -1);
-    DDL_REQUIRE(back.type == t.type, DDL_STATUS_COMM_ERROR, "token protocol: expected SYNC, got " << (int)back.type);
+    ch.send(t);  // the proposal to every member
+    std::vector<Token> answers(ch.size() - 1);
+    for (int r = 1; r < ch.size(); ++r) {
+        ch.recv_from(r, answers[r - 1], -1);
+        DDL_REQUIRE(answers[r - 1].type == t.type, DDL_STATUS_COMM_ERROR,
+                    "token protocol: expected SYNC from rank " << r << ", got " << (int)answers[r - 1].type);
+    }
+    Agreed a = decide(cached, idx, strs, answers, ch);
     Token c;
     c.type = cached ? TOKEN_COMMUNICATE_CACHED : TOKEN_COMMUNICATE;
     c.request = (uint8_t)request_type;
-    c.msg = back.msg;
-    ch.send(c);
-    Agreed a;
-    a.cached = cached;
+    c.msg = cached ? ch.cache.encode(a.idx) : encode_keys(a.wire);
+    ch.send(c);  // the agreed set to every member
     if (cached) {
-        a.idx = ch.cache.decode(back.msg);
         ++ch.cached_rounds;
     } else {
-        a.wire = decode_keys(back.msg);
         std::sort(a.wire.begin(), a.wire.end());
         ++ch.string_rounds;
     }
     return a;
 }
 
-void negotiate_root_finish(ControlChannel &ch) {
-    Token drain;
-    ch.recv(drain, -1);
-    DDL_REQUIRE(drain.type == TOKEN_COMMUNICATE || drain.type == TOKEN_COMMUNICATE_CACHED, DDL_STATUS_COMM_ERROR,
-                "token protocol: expected COMMUNICATE, got " << (int)drain.type);
-}
+// Nothing to drain in the star (the ring's COMMUNICATE lap came back to rank 0 here).
+void negotiate_root_finish(ControlChannel &) {}
 
 Agreed negotiate_member(ControlChannel &ch, const Token &sync,
                         const std::function<std::vector<std::string>(const std::vector<std::string> &)> &by_string,
@@ -437,12 +475,11 @@ Agreed negotiate_member(ControlChannel &ch, const Token &sync,
     s.type = sync.type;
     s.request = sync.request;
     s.msg = cached ? ch.cache.encode(by_index(ch.cache.decode(sync.msg))) : encode_keys(by_string(decode_keys(sync.msg)));
-    ch.send(s);
+    ch.send(s);  // this rank's intersection with the proposal
     Token c;
     ch.recv(c, -1);
     DDL_REQUIRE(c.type == (cached ? TOKEN_COMMUNICATE_CACHED : TOKEN_COMMUNICATE), DDL_STATUS_COMM_ERROR,
                 "token protocol: expected COMMUNICATE, got " << (int)c.type);
-    ch.send(c);  // forward first, then communicate (RingTokenCommunicateHandler.cc:302-310)
     Agreed a;
     a.cached = cached;
     if (cached) {
@@ -496,8 +533,8 @@ std::vector<ReqId> RequestHandler::agreed_ids_(const Agreed &a) {
     return ids;
 }
 
-// Rank 0: propose every registered id of one type (lap 1, SYNC — each rank intersects), then
-// announce the agreed set (lap 2, COMMUNICATE) and run it.
+// Rank 0: propose every registered id of one type (SYNC to every member — each intersects and
+// answers), then announce the agreed set (COMMUNICATE) and run it.
 void RequestHandler::root_round_() {
     ControlChannel &ch = *ch_;
     // one request type per round (the token carries one RequestType): the type of the first
@@ -524,9 +561,9 @@ void RequestHandler::root_round_() {
     negotiate_root_finish(ch);
 }
 
-// Other ranks: join the SYNC lap once the first proposed id is registered here (the reference
-// parks the READY token the same way, RingTokenCommunicateHandler.cc:225-250), forward the
-// intersection, then forward COMMUNICATE and run the agreed set (:302-310).
+// Other ranks: answer the SYNC once the first proposed id is registered here (the reference
+// parks the READY token the same way, RingTokenCommunicateHandler.cc:225-250) with the
+// intersection, then take COMMUNICATE and run the agreed set (:302-310).
 void RequestHandler::member_round_(Token &t) {
     const Agreed a = negotiate_member(
         *ch_, t,

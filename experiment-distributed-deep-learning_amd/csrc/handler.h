@@ -10,8 +10,9 @@
 //     495-749): dtype classification (ascending enum), plans capped at the fusion threshold,
 //     memcpy in -> MPI_Allreduce -> memcpy out, done() as each tensor's last element lands.
 //
-// MI355X-first changes: the token makes 2 laps instead of 3 (READY+SYNC merged: a rank joins
-// the lap once it has the first key of the proposed set, then intersects); one-request plans
+// MI355X-first changes: a round is 3 hops over a star around rank 0 instead of 3 laps of a ring
+// (READY+SYNC merged: a member answers the proposal once it has the proposal's first key, with
+// its intersection; rank 0 intersects the answers and announces the result); one-request plans
 // run the ring directly on the tensor (no staging copy); multi-request plans are packed by
 // one gather kernel into an HBM fusion buffer and scattered by one kernel; the data plane
 // runs on a private RCCL communicator so user-level ddl_allreduce calls never interleave.
@@ -125,11 +126,12 @@ std::vector<Plan> make_plans(const std::vector<size_t> &elements, const std::vec
 // ddl_control_connect_ranked keeps it for ddl_control_negotiate (tools, CPU tests).
 std::shared_ptr<ControlChannel> &standalone_control();
 
-// One negotiation round of the 2-lap token protocol.
-//   root:   SYNC(proposal) -> ... -> SYNC(intersection) back; COMMUNICATE(agreed) sent.
-//           After running the agreed set, negotiate_root_finish() drains COMMUNICATE.
+// One negotiation round over the star (control.h).
+//   root:   SYNC(proposal) to every member; every member's SYNC(intersection) back; the
+//           proposal's ids every member kept go out as COMMUNICATE(agreed). (negotiate_root_finish
+//           is a no-op kept for the ring's call sites.)
 //   member: receives SYNC, intersects with what it holds (may block until the first proposed
-//           id is registered), forwards, then receives and forwards COMMUNICATE.
+//           id is registered), answers rank 0, then receives COMMUNICATE.
 // A proposal made only of ids agreed in earlier rounds travels as indices into the channel's
 // IdCache (TOKEN_*_CACHED) and is intersected by index; otherwise as "Type::key" strings.
 struct Agreed {

@@ -2,7 +2,7 @@
 ddl_control_negotiate with the same 4096 gradient keys (the C5 / training-step case). Round 1
 ships the ids as strings; later rounds ship them as indices into the shared id table.
 
-    python tools/negotiation_bench.py [P ...]
+    python tools/negotiation_bench.py [P ...]        (NEG_KEYS=1 NEG_ROUNDS=200: one-key rounds)
 """
 import ctypes
 import json
@@ -15,8 +15,8 @@ import multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
 
-KEYS = [f'grad_{i:05d}' for i in range(4096)]
-ROUNDS = 20
+KEYS = [f'grad_{i:05d}' for i in range(int(os.environ.get('NEG_KEYS', 4096)))]
+ROUNDS = int(os.environ.get('NEG_ROUNDS', 20))
 
 
 def worker(rank, world, eps_q, go_q, out_q):
