@@ -511,6 +511,33 @@ def keyed_bucket_stream(lib, comm, dev, steps, buckets=32, bucket_bytes=8 << 20)
     return res
 
 
+def keyed_c1_latency(lib, comm, dev, reps=200):
+    """C1 through the keyed path at this N: one fp32[1024] tensor, x_r = rank, one
+    keyed submit + wait per iteration (negotiation over the star, then the allreduce) — the
+    reference's per-request latency case (0.73 ms at P = 2 on its CPU+MPI path).
+    Reports the median and best round trip and checks the sum."""
+    import torch
+    from ddl.torch.cpp_backend import DONE_FN, check
+    x = torch.full((1024,), float(comm.rank), device=dev)
+    y = torch.empty_like(x)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    nodone = DONE_FN()
+    ts = []
+    for i in range(reps + 10):
+        t0 = time.perf_counter()
+        check(lib.ddl_allreduce_submit(comm.id, b'C1', x.data_ptr(), y.data_ptr(), 1024, 1, 0, sh, nodone, None),
+              'ddl_allreduce_submit')
+        check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
+        if i >= 10:
+            ts.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    want = comm.size * (comm.size - 1) / 2
+    ts.sort()
+    return {'elements': 1024, 'dtype': 'f32', 'reps': reps, 'median_us': round(ts[len(ts) // 2] * 1e6, 1),
+            'best_us': round(ts[0] * 1e6, 1), 'sum_ok': bool((y == want).all().item()),
+            'path': 'keyed submit -> star negotiation -> allreduce in place on the tensor -> done'}
+
+
 def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
     buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks
@@ -832,6 +859,11 @@ def multi_gpu(args):
             out['keyed_bucket_stream'] = keyed_bucket_stream(lib, comm, dev, steps=3)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['keyed_bucket_stream'] = repr(e)[:400]
+    state['leg'] = 'keyed_c1_latency'
+    try:
+        out['keyed_c1_latency'] = keyed_c1_latency(lib, comm, dev)
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['keyed_c1_latency'] = repr(e)[:400]
     # the deployment case at N ranks: C5's buckets as pinned host tensors through the keyed path
     # (host pack -> H2D -> allreduce over xGMI -> unpack kernel into the tensors over PCIe)
     state['leg'] = 'keyed_host_c5_pinned'

@@ -146,8 +146,10 @@ def _control_worker(rank, world, keysets, eps_q, go_q, out_q):
         out_q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('world', [2, 3, 5, 9])
 def test_token_ring_negotiation(world):
+    """Agreed set per round = the lexicographic intersection of every rank's keys (the star: rank
+    0's proposal, each member's intersection, rank 0's intersection of the answers)."""
     # per rank, per round: registered keys (unsorted, overlapping, some missing on some ranks)
     rng = np.random.default_rng(world)
     universe = [f'grad_{i:04d}' for i in range(60)] + ['Grad_X', 'grad_é', 'a', 'a::b']
@@ -207,7 +209,7 @@ def _run_control(world, keysets):
     return res
 
 
-@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('world', [2, 3, 6])
 def test_token_ring_cached_ids(world):
     """Rounds whose proposal holds only ids agreed before travel as indices into the shared id
     table (TOKEN_SYNC_CACHED); the agreed sets must be exactly the string protocol's."""
