@@ -6,6 +6,7 @@
 #include <cstring>
 #include <iterator>
 #include <set>
+#include <thread>
 #include <tuple>
 
 namespace ddl {
@@ -1251,6 +1252,23 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
 }
 
+namespace {
+// Waits for a plan's event without holding a core for a whole long round: queries with yields
+// for the first 200 us (a plan about to land — small rounds keep their latency), then sleeps
+// between queries (each sleep ~20-70 us with the kernel's timer slack), so the completion thread
+// does not spin beside the engine thread, the host copies and the framework's own threads.
+hipError_t wait_plan(hipEvent_t e) {
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q != hipErrorNotReady) return q;
+        if (clk::now() - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+}  // namespace
+
 // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725).
 void RequestHandler::complete_(Round &rd) {
     using clk = std::chrono::steady_clock;
@@ -1259,7 +1277,7 @@ void RequestHandler::complete_(Round &rd) {
     size_t synced = kNoPlan;  // dones are in plan order: wait for each plan's event once
     for (const Done &d : rd.dones) {
         if (status == DDL_STATUS_OK && d.plan != kNoPlan && d.plan != synced) {
-            hipError_t he = hipEventSynchronize(rd.events[d.plan]);
+            hipError_t he = wait_plan(rd.events[d.plan]);
             if (he != hipSuccess) status = DDL_STATUS_HIP_ERROR;
             synced = d.plan;
         }
