@@ -442,6 +442,9 @@ def worker(rank, world, port, q):
         # the configured schedule unless a check turns the tuner on (check_tuned_exact): tuning
         # every new size class through gloo host copies is what makes these runs slow at P = 8
         check(lib.ddl_set_config(b'tune', 0), 'ddl_set_config')
+        # keyed rounds waited for one by one (the reference's behaviour) when the test asks
+        check(lib.ddl_set_config(b'pipeline_rounds', int(os.environ.get('DDL_MP_PIPELINE_ROUNDS', 1))),
+              'ddl_set_config')
         ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
                'oracle': h.Oracle()}
         import time

@@ -22,9 +22,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize('world', [2, 3, 4, 5, 8])
-def test_engine_multiprocess_on_one_gpu(gpu, world):
+@pytest.mark.parametrize('world,pipelined', [(2, 1), (3, 1), (4, 1), (5, 1), (8, 1), (4, 0)])
+def test_engine_multiprocess_on_one_gpu(gpu, world, pipelined, monkeypatch):
+    """Every check at P ranks; keyed rounds pipelined (default) and, at P = 4, waited for one by
+    one (pipeline_rounds = 0, the spawned workers read DDL_MP_PIPELINE_ROUNDS)."""
     import torch.multiprocessing as mp
+    monkeypatch.setenv('DDL_MP_PIPELINE_ROUNDS', str(pipelined))
 
     import _mp_gpu_worker
     ctx = mp.get_context('spawn')
