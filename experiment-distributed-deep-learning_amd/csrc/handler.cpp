@@ -1236,6 +1236,22 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     rd.t0 = t0;
     rd.t1 = t1;
     if (timed) rd.t2 = clk::now();
+    const bool pipelined = config().pipeline_rounds.load() != 0;
+    size_t bytes = 0;
+    for (const Request &r : rd.reqs) bytes += r.n * dtype_size(r.dtype);
+    bool idle;
+    {
+        std::lock_guard<std::mutex> g(done_mu_);
+        idle = rounds_queued_ == rounds_done_;  // no earlier round waiting or completing
+    }
+    // nothing earlier in flight and the round is to be waited for anyway (unpipelined, failed)
+    // or small (its data plane takes microseconds): complete it here — done() order holds and
+    // the hand-off to the completion thread (a thread wake-up each way) is saved
+    if (idle && (!pipelined || status != DDL_STATUS_OK || bytes <= kInlineRoundBytes)) {
+        complete_(rd);
+        if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
+        return;
+    }
     unsigned long long seq;
     {
         std::lock_guard<std::mutex> g(done_mu_);
@@ -1245,7 +1261,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     done_cv_.notify_all();
     // pipelined: back to negotiating while the device runs this round; otherwise (and after a
     // failed enqueue, whose done() calls must have fired before the handler stops) wait for it
-    if (status != DDL_STATUS_OK || !config().pipeline_rounds.load()) {
+    if (status != DDL_STATUS_OK || !pipelined) {
         std::unique_lock<std::mutex> lk(done_mu_);
         done_cv_.wait(lk, [&] { return rounds_done_ >= seq; });
     }

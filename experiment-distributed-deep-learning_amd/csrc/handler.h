@@ -184,6 +184,9 @@ private:
         size_t nplans = 0;
         std::chrono::steady_clock::time_point t0, t1, t2;  // take / enqueue phase bounds (log)
     };
+    // a round of at most this many bytes, with no earlier round in flight, completes on the
+    // engine thread even when pipelined (its data plane is microseconds: the hand-off costs more)
+    static constexpr size_t kInlineRoundBytes = 256u << 10;
     size_t record_plan_(size_t &nplans);  // records the round's next plan event on stream_
     void complete_(Round &rd);            // waits the plan events, fires done(), frees the events
     void completer_();                    // the completion thread
