@@ -641,6 +641,10 @@ def multi_gpu(args):
     dog = threading.Timer(args.watchdog_s, hung)
     dog.daemon = True
     dog.start()
+    if not args.rehearse and torch.cuda.device_count() < world:  # counting does not initialise the GPU
+        sys.stderr.write(f'[bench rank {rank}] {world} ranks need {world} GPUs, this box has '
+                         f'{torch.cuda.device_count()} (use --rehearse to run the N>1 legs on one GPU)\n')
+        sys.exit(2)
     torch.cuda.set_device(local)
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29533')
@@ -651,6 +655,13 @@ def multi_gpu(args):
         import gloo_transport
         state['callbacks'] = gloo_transport.init_world(lib, dist, torch, rank, world, device=local)
     comm = Communicator.world()
+    kind, tranks = ctypes.c_int(), ctypes.c_int()
+    check(lib.ddl_comm_transport(comm.id, ctypes.byref(kind), ctypes.byref(tranks)), 'ddl_comm_transport')
+    transport = {'kind': ('none', 'rccl', 'test_transport_gloo')[kind.value], 'ranks': tranks.value,
+                 'rccl_ranks': tranks.value if kind.value == 1 else None}
+    if tranks.value != world:
+        sys.stderr.write(f'[bench rank {rank}] the transport sees {tranks.value} ranks, the launcher {world}\n')
+        sys.exit(2)
     dev = torch.device('cuda', local)
     S = args.bucket_mib << 20
     n = S // 4
@@ -739,6 +750,7 @@ def multi_gpu(args):
                    'bucket_bytes': S, 'parallelism': f'dp{world}',
                    'reference_order': lib.ddl_get_config(b'reference_order')},
         'value_is': 'allreduce algbw: bucket bytes / max-over-ranks time per allreduce (GiB/s)',
+        'transport': transport,
         'algbw_GiBs': round(algbw, 2),
         'busbw_GBs': round(busbw_gbs, 2),
         'link_roofline': (None if ceiling is None else
@@ -1043,13 +1055,73 @@ def emit(obj):
     os.write(fd, line)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` with no launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, as torch.distributed.run would) and exit with the first failing
+    rank's code. The parent never imports torch or touches HIP (no GPU initialised here, so no
+    exec hazards); rank 0's JSON line reaches this process's stdout directly."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                   DDL_BENCH_SPAWNED='1')
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    deadline = time.time() + args.watchdog_s + 120
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    sys.stderr.write(f'[bench] rank {procs.index(p)} exited with {code}; stopping the others\n')
+                    for q in live:
+                        os.killpg(q.pid, signal.SIGTERM)
+            if time.time() > deadline:
+                sys.stderr.write('[bench] ranks still running past the watchdog; killing them\n')
+                for q in live:
+                    os.killpg(q.pid, signal.SIGKILL)
+                rc = rc or 124
+                deadline = float('inf')
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+                q.wait()
+    return rc
+
+
 def main():
     global _REAL_STDOUT
+    args = parse()
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        sys.stdout.flush()
+        sys.exit(spawn_ranks(args))
     sys.stdout.flush()
     _REAL_STDOUT = os.dup(1)
     os.dup2(2, 1)  # native and Python chatter -> stderr
-    args = parse()
-    world = int(os.environ.get('WORLD_SIZE', args.gpus))
+    world = int(env_world) if env_world is not None else 1
+    if world != args.gpus and not (args.force_multi and world == 1):
+        sys.stderr.write(f'[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to print a line for a '
+                         f'different world\n')
+        sys.exit(2)
     if world <= 1 and not args.force_multi:
         single_gpu(args)
     else:

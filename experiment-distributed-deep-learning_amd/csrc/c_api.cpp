@@ -1,6 +1,7 @@
 // c_api.cpp — extern "C" boundary (include/ddl_amd.h). Every entry point converts internal
 // errors into a status code; no C++ exception crosses the ABI.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -137,6 +138,9 @@ void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len)
         agreed = a.wire;
         ch.cache.learn(agreed);
     }
+    DDL_REQUIRE(a.cfg_ok, DDL_STATUS_CONFIG_MISMATCH,
+                "negotiation refused: the ranks' shared tunables differ (config hash here " << std::hex
+                                                                                           << config().shared_hash() << ")");
     std::string res;
     for (const auto &k : agreed) res.append(k.substr(k.find("::") + 2)).append("\n");
     DDL_REQUIRE(res.size() < len, DDL_STATUS_INVALID_ARGUMENT, "output buffer too small");
@@ -195,6 +199,10 @@ int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn gr
     return guarded([&] {
         DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && group, DDL_STATUS_INVALID_ARGUMENT,
                     "bad test transport arguments");
+        const char *allow = std::getenv("DDL_ALLOW_TEST_TRANSPORT");
+        DDL_REQUIRE(allow && std::string(allow) == "1", DDL_STATUS_INVALID_ARGUMENT,
+                    "ddl_init_test_transport is a test harness (host-synchronised groups, no RCCL): set "
+                    "DDL_ALLOW_TEST_TRANSPORT=1 to use it; deployments call ddl_init");
         DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
         DDL_HIP(hipSetDevice(device));
         auto hooks = std::make_shared<TestHooks>();
@@ -323,6 +331,7 @@ int ddl_set_config(const char *key, long long value) {
         } else if (k == "one_rank_shortcut") c.one_rank_shortcut = value ? 1 : 0;
         else if (k == "pipeline_rounds") c.pipeline_rounds = value ? 1 : 0;
         else if (k == "reference_order") c.reference_order = value ? 1 : 0;
+        else if (k == "capture_forked") c.capture_forked = value ? 1 : 0;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
     });
@@ -348,6 +357,7 @@ long long ddl_get_config(const char *key) {
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;
     if (k == "reference_order") return c.reference_order;
+    if (k == "capture_forked") return c.capture_forked;
     return -1;
 }
 
@@ -435,24 +445,45 @@ int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, 
         }
         DDL_REQUIRE(variant == 1, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
         DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM");
-        DeviceGuard g(c->device());
-        if (c->size() == 1) {
-            if (send != recv) DDL_HIP(hipMemcpyAsync(recv, send, elements * dtype_size(dtype), hipMemcpyDeviceToDevice, as_stream(hip_stream)));
-            return;
+        c->rccl_allreduce(send, recv, elements, dtype, as_stream(hip_stream));
+    });
+}
+
+int ddl_comm_transport(ddl_communicator_id id, int *kind, int *ranks) {
+    return guarded([&] {
+        DDL_REQUIRE(kind && ranks, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        Registry::get().find(id)->transport(kind, ranks);
+    });
+}
+
+int ddl_testing_round_log(ddl_communicator_id id, long long *user_collectives, long long *releases, int max_releases,
+                          int *count) {
+    return guarded([&] {
+        DDL_REQUIRE(user_collectives && count, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        auto c = Registry::get().find(id);
+        *user_collectives = c->user_collectives();
+        std::vector<long long> log = c->round_log();
+        *count = (int)log.size();
+        for (int i = 0; i < (int)log.size() && i < max_releases && releases; ++i) releases[i] = log[i];
+    });
+}
+
+int ddl_testing_agree_config(int rank, int size, ddl_test_group_fn group, void *user) {
+    return guarded([&] {
+        DDL_REQUIRE(size >= 1 && rank >= 0 && rank < size && group, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad agreement arguments");
+        std::vector<uint64_t> all(size, 0);
+        all[rank] = config().shared_hash();
+        std::vector<ddl_p2p_op> ops;
+        for (int d = 1; d < size; ++d) {
+            const int to = (rank + d) % size, from = (rank + size - d) % size;
+            ops.push_back(ddl_p2p_op{1, to, 4002, &all[rank], sizeof(uint64_t)});
+            ops.push_back(ddl_p2p_op{0, from, 4002, &all[from], sizeof(uint64_t)});
         }
-        DDL_REQUIRE(c->nccl() != nullptr, DDL_STATUS_INVALID_ARGUMENT, "no RCCL communicator (test transport)");
-        ncclDataType_t t;
-        switch (dtype) {
-            case DDL_FLOAT: t = ncclFloat32; break;
-            case DDL_DOUBLE: t = ncclFloat64; break;
-            case DDL_INT32: t = ncclInt32; break;
-            case DDL_INT64: t = ncclInt64; break;
-            case DDL_UINT64: t = ncclUint64; break;
-            case DDL_HALF: t = ncclFloat16; break;
-            case DDL_BFLOAT16: t = ncclBfloat16; break;
-            default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
-        }
-        rccl_check(rccl().AllReduce(send, recv, elements, t, ncclSum, c->nccl(), as_stream(hip_stream)), "ncclAllReduce");
+        if (!ops.empty())
+            DDL_REQUIRE(group(0, ops.data(), (int)ops.size(), user) == 0, DDL_STATUS_COMM_ERROR,
+                        "agreement exchange failed");
+        check_config_agreement(rank, all);
     });
 }
 

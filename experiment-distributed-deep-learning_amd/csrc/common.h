@@ -12,7 +12,7 @@
 #include <sstream>
 #include <vector>
 
-#include "ddl_amd.h"
+#include "ddl_amd_testing.h"
 
 namespace ddl {
 

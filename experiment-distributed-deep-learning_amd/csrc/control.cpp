@@ -163,11 +163,13 @@ void ControlChannel::connect(int rank, int size, const std::vector<std::string> 
 
 namespace {
 void send_token(int fd, const Token &t) {
-    unsigned char hdr[10];
+    unsigned char hdr[26];
     uint64_t len = t.msg.size();
     hdr[0] = t.type;
     hdr[1] = t.request;
     std::memcpy(hdr + 2, &len, 8);  // host byte order, as the reference's MPI_Pack of size_t
+    std::memcpy(hdr + 10, &t.cfg, 8);  // the engine's extension
+    std::memcpy(hdr + 18, &t.seq, 8);
     write_all(fd, hdr, sizeof hdr);
     if (len) write_all(fd, t.msg.data(), len);
 }
@@ -179,10 +181,12 @@ bool recv_token(int fd, Token &t, int timeout_ms) {
         if (r == 0) return false;
         DDL_REQUIRE(r > 0, DDL_STATUS_COMM_ERROR, "control poll: " << std::strerror(errno));
     }
-    unsigned char hdr[10];
+    unsigned char hdr[26];
     read_all(fd, hdr, sizeof hdr);
     uint64_t len;
     std::memcpy(&len, hdr + 2, 8);
+    std::memcpy(&t.cfg, hdr + 10, 8);
+    std::memcpy(&t.seq, hdr + 18, 8);
     DDL_REQUIRE(len < (1ull << 32), DDL_STATUS_COMM_ERROR, "control token too long: " << len);
     t.type = hdr[0];
     t.request = hdr[1];

@@ -8,7 +8,9 @@
 // agreed set to every member — 3 hops at any P, the members' hops in parallel (a single-key
 // round at P = 8 on 8 cores: 0.35 ms as a ring). A token on the wire is the same packed header
 // the reference sends with MPI_Pack — {u8 type, u8 request type, u64 length} (10 bytes,
-// :25,44-53) — followed by `length` bytes of key list.
+// :25,44-53) — then a 16-byte engine extension {u64 config hash, i64 user-collective count}
+// (the round's config agreement and its place among the communicator's user collectives, see
+// handler.h), then `length` bytes of key list.
 #pragma once
 
 #include <cstdint>
@@ -28,8 +30,11 @@ enum TokenRequest : uint8_t { TOKEN_REQUEST_SHUTDOWN = 0, TOKEN_REQUEST_ALLREDUC
 struct Token {
     uint8_t type = TOKEN_READY;
     uint8_t request = TOKEN_REQUEST_ALLREDUCE;
+    uint64_t cfg = 0;  // sender's shared-config hash (kCfgMismatch in a COMMUNICATE: ranks disagree)
+    int64_t seq = -1;  // user collectives issued (SYNC answers) / the round's release point (COMMUNICATE)
     std::string msg;
 };
+constexpr uint64_t kCfgMismatch = ~0ull;
 
 // Request ids agreed in earlier rounds, in agreement order. Every rank appends the same agreed
 // lists in the same order, so the tables are identical across ranks and a proposal made only

@@ -36,7 +36,22 @@ Config &config() {
     return *c;
 }
 
+uint64_t Config::shared_hash() const {
+    const long long v[] = {algo.load(), slice_bytes.load(), rings.load(), max_slices.load(),
+                           fusion_threshold_bytes.load(), tune.load(), fusion_pipeline_bytes.load(),
+                           reference_order.load(), host_chunk_bytes.load()};
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the values' bytes
+    for (long long x : v)
+        for (int b = 0; b < 8; ++b) {
+            h ^= (uint64_t)((unsigned long long)x >> (8 * b)) & 0xff;
+            h *= 1099511628211ull;
+        }
+    h |= 1;  // never 0 ("no agreement yet")
+    return h == kCfgMismatch ? h - 2 : h;
+}
+
 int log_level() { return (int)config().log_level.load(); }
+bool config_capture_forked() { return config().capture_forked.load() != 0; }
 
 void log_line(int level, const std::string &msg) {
     static std::mutex mu;
@@ -81,9 +96,126 @@ Communicator::~Communicator() {
     exec_.reset();
     for (void *s : slots_)
         if (s) (void)hipFree(s);
-    for (hipStream_t s : {h2d_, ring_, d2h_})
+    for (hipStream_t s : {h2d_, ring_, d2h_, ctl_stream_})
         if (s) (void)hipStreamDestroy(s);
     if (nccl_) (void)rccl().CommDestroy(nccl_);
+}
+
+// One user collective on a communicator with a token ring: waits while a keyed round is being
+// placed at or before this collective's number (round_freeze / round_release), then counts itself
+// as entered; on leaving (enqueued, or failed on every rank alike) as done. The gate's mutex is
+// held only for those two steps: a collective that synchronises with the other ranks (tuning,
+// the config agreement, the test transport) never blocks the handler's placement of a round —
+// which counts it already (entered), so every rank runs it before the round.
+class Communicator::UserCollective {
+public:
+    explicit UserCollective(Communicator &c) : c_(c) {
+        if (c_.size_ <= 1 || !c_.keyed_data_) return;
+        std::unique_lock<std::mutex> lk(c_.gate_mu_);
+        c_.gate_cv_.wait(lk, [&] { return !c_.frozen_ || c_.user_seq_ < c_.release_; });
+        ++c_.user_seq_;
+        active_ = true;
+    }
+    ~UserCollective() {
+        if (!active_) return;
+        {
+            std::lock_guard<std::mutex> g(c_.gate_mu_);
+            ++c_.user_done_;
+        }
+        c_.gate_cv_.notify_all();
+    }
+
+private:
+    Communicator &c_;
+    bool active_ = false;
+};
+
+long long Communicator::round_freeze() {
+    std::lock_guard<std::mutex> g(gate_mu_);
+    frozen_ = true;
+    release_ = user_seq_;
+    return user_seq_;
+}
+
+void Communicator::round_release(long long at) {
+    {
+        std::lock_guard<std::mutex> g(gate_mu_);
+        DDL_REQUIRE(at >= user_seq_, DDL_STATUS_COMM_ERROR,
+                    "keyed round placed after user collective " << at << " but " << user_seq_ << " have started");
+        release_ = at;
+        round_log_.push_back(at);
+        if (round_log_.size() > 4096) round_log_.erase(round_log_.begin(), round_log_.begin() + 2048);
+    }
+    gate_cv_.notify_all();
+}
+
+void Communicator::round_enter(long long at) {
+    std::unique_lock<std::mutex> g(gate_mu_);
+    gate_cv_.wait(g, [&] { return user_done_ >= at; });
+    DDL_REQUIRE(user_seq_ == at && user_done_ == at, DDL_STATUS_COMM_ERROR,
+                "keyed round placed after user collective " << at << " but " << user_seq_ << " have started");
+}
+
+void Communicator::round_unfreeze() {
+    {
+        std::lock_guard<std::mutex> g(gate_mu_);
+        frozen_ = false;
+    }
+    gate_cv_.notify_all();
+}
+
+long long Communicator::user_collectives() const {
+    std::lock_guard<std::mutex> g(const_cast<std::mutex &>(gate_mu_));
+    return user_seq_;
+}
+
+std::vector<long long> Communicator::round_log() const {
+    std::lock_guard<std::mutex> g(const_cast<std::mutex &>(gate_mu_));
+    return round_log_;
+}
+
+void Communicator::transport(int *kind, int *ranks) const {
+    *kind = size_ <= 1 ? 0 : (hooks_ ? 2 : 1);
+    *ranks = size_;
+    if (*kind == 1) rccl_check(rccl().CommCount(nccl_, ranks), "ncclCommCount");
+}
+
+void check_config_agreement(int rank, const std::vector<uint64_t> &hashes) {
+    bool same = true;
+    for (uint64_t h : hashes) same = same && h == hashes[0];
+    if (same) return;
+    std::ostringstream os;
+    os << "shared tunables differ between ranks (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, "
+          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes must be set alike on every rank); "
+          "config hash per rank:";
+    for (size_t q = 0; q < hashes.size(); ++q)
+        os << " " << q << (q == (size_t)rank ? "*" : "") << "=" << std::hex << hashes[q] << std::dec;
+    fail(DDL_STATUS_CONFIG_MISMATCH, os.str());
+}
+
+void Communicator::agree_config(hipStream_t stream) {
+    if (size_ <= 1) return;
+    const uint64_t mine = config().shared_hash();
+    if (mine == agreed_hash_) return;
+    DDL_REQUIRE(!stream_capturing(stream), DDL_STATUS_INVALID_ARGUMENT,
+                "the shared tunables changed (or this is the communicator's first collective): the ranks must "
+                "agree on them outside a graph capture — run one collective before capturing");
+    std::vector<uint64_t> all(size_, 0);
+    all[rank_] = mine;
+    if (hooks_) {
+        std::vector<ddl_p2p_op> ops;
+        for (int d = 1; d < size_; ++d) {
+            const int to = (rank_ + d) % size_, from = (rank_ + size_ - d) % size_;
+            ops.push_back(ddl_p2p_op{1, to, 4002, &all[rank_], sizeof(uint64_t)});
+            ops.push_back(ddl_p2p_op{0, from, 4002, &all[from], sizeof(uint64_t)});
+        }
+        cb_->host_group(ops);
+    } else {
+        if (!ctl_stream_) DDL_HIP(hipStreamCreateWithFlags(&ctl_stream_, hipStreamNonBlocking));
+        rccl_allgather_u64(nccl_, all.data(), size_, rank_, ctl_stream_);
+    }
+    check_config_agreement(rank_, all);
+    agreed_hash_ = mine;
 }
 
 void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, int op, hipStream_t stream,
@@ -91,11 +223,36 @@ void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, 
     DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported (op " << op << ")");
     DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
     DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    UserCollective uc(*this);
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
     RingConfig cfg = ring_config(n, dtype, stream);
     cfg.order_bytes = order_bytes;
     exec_->allreduce(send, recv, n, dtype, stream, cfg);
+}
+
+void Communicator::rccl_allreduce(const void *send, void *recv, size_t n, int dtype, hipStream_t stream) {
+    UserCollective uc(*this);
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    if (size_ == 1) {
+        if (send != recv && n) DDL_HIP(hipMemcpyAsync(recv, send, n * dtype_size(dtype), hipMemcpyDeviceToDevice, stream));
+        return;
+    }
+    DDL_REQUIRE(nccl_ != nullptr, DDL_STATUS_INVALID_ARGUMENT, "no RCCL communicator (test transport)");
+    ncclDataType_t t;
+    switch (dtype) {
+        case DDL_FLOAT: t = ncclFloat32; break;
+        case DDL_DOUBLE: t = ncclFloat64; break;
+        case DDL_INT32: t = ncclInt32; break;
+        case DDL_INT64: t = ncclInt64; break;
+        case DDL_UINT64: t = ncclUint64; break;
+        case DDL_HALF: t = ncclFloat16; break;
+        case DDL_BFLOAT16: t = ncclBfloat16; break;
+        default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
+    }
+    agree_config(stream);
+    rccl_check(rccl().AllReduce(send, recv, n, t, ncclSum, nccl_, stream), "ncclAllReduce");
 }
 
 namespace {
@@ -233,11 +390,12 @@ TuneResult Communicator::tune_(size_t n, int dtype, hipStream_t stream, const Ri
 
 RingConfig Communicator::ring_config(size_t n, int dtype, hipStream_t stream) {
     const RingConfig base = config().ring();
-    if (size_ <= 1 || n == 0 || !config().tune.load()) return base;
-    const long long ep = config().epoch.load();
-    if (ep != tuned_epoch_) {
+    if (size_ <= 1 || n == 0) return base;
+    agree_config(stream);
+    if (!config().tune.load()) return base;
+    if (agreed_hash_ != tuned_hash_) {  // the shared tunables changed: tune again
         tuned_.clear();
-        tuned_epoch_ = ep;
+        tuned_hash_ = agreed_hash_;
     }
     const int cls = size_class(n * dtype_size(dtype));
     auto it = tuned_.find(cls);
@@ -253,7 +411,7 @@ RingConfig Communicator::ring_config(size_t n, int dtype, hipStream_t stream) {
 TuneResult Communicator::tune_result(size_t bytes) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = tuned_.find(size_class(bytes));
-    if (it == tuned_.end() || tuned_epoch_ != config().epoch.load()) return TuneResult{};
+    if (it == tuned_.end() || tuned_hash_ != config().shared_hash()) return TuneResult{};
     return it->second;
 }
 
@@ -261,8 +419,10 @@ void Communicator::broadcast(void *buf, size_t n, int dtype, int root, hipStream
     DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
     DDL_REQUIRE(root >= 0 && root < size_, DDL_STATUS_INVALID_ARGUMENT, "root " << root << " outside [0, " << size_ << ")");
     DDL_REQUIRE(n == 0 || buf, DDL_STATUS_INVALID_ARGUMENT, "null buffer");
+    UserCollective uc(*this);
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
+    if (n) agree_config(stream);
     exec_->broadcast(buf, n, dtype, root, stream, config().ring());
 }
 
@@ -274,8 +434,10 @@ void Communicator::allgatherv(const void *send, void *recv, const size_t *counts
     size_t total = 0;
     for (int q = 0; q < size_; ++q) total += counts[q];
     DDL_REQUIRE(total == 0 || recv, DDL_STATUS_INVALID_ARGUMENT, "null recv buffer");
+    UserCollective uc(*this);
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
+    if (total) agree_config(stream);
     exec_->allgatherv(send, recv, counts, displs, dtype, stream);
 }
 
@@ -315,6 +477,7 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
     DDL_REQUIRE(n == 0 || (send && recv), DDL_STATUS_INVALID_ARGUMENT, "null buffer");
     const size_t total = n * es;
     if (total == 0) return;
+    UserCollective uc(*this);
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
     size_t chunk = (size_t)config().host_chunk_bytes.load();
@@ -405,6 +568,7 @@ static_assert(sizeof(SplitRecord) == 64, "split record is 8 int64 on the wire");
 }  // namespace
 
 std::shared_ptr<Communicator> Communicator::split(int color, int key, bool keyed) {
+    UserCollective uc(*this);
     std::lock_guard<std::mutex> g(mu_);
     DeviceGuard dg(device_);
     // 1) every rank's record, in rank order, over this communicator's data plane (an allgather,
@@ -525,6 +689,22 @@ void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stre
         DDL_HIP(hipMemcpyAsync(d, values, sizeof(float) * count, hipMemcpyHostToDevice, stream));
         rccl_check(rccl().AllReduce(d, d, count, ncclFloat32, ncclMax, comm, stream), "ncclAllReduce(max)");
         DDL_HIP(hipMemcpyAsync(values, d, sizeof(float) * count, hipMemcpyDeviceToHost, stream));
+        DDL_HIP(hipStreamSynchronize(stream));
+    } catch (...) {
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(d);
+        throw;
+    }
+    DDL_HIP(hipFree(d));
+}
+
+void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, hipStream_t stream) {
+    uint64_t *d = nullptr;
+    DDL_HIP(hipMalloc(&d, sizeof(uint64_t) * size));
+    try {
+        DDL_HIP(hipMemcpyAsync(d + rank, values + rank, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+        rccl_check(rccl().AllGather(d + rank, d, sizeof(uint64_t), ncclInt8, comm, stream), "ncclAllGather(config)");
+        DDL_HIP(hipMemcpyAsync(values, d, sizeof(uint64_t) * size, hipMemcpyDeviceToHost, stream));
         DDL_HIP(hipStreamSynchronize(stream));
     } catch (...) {
         (void)hipStreamSynchronize(stream);

@@ -8,6 +8,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <map>
 #include <memory>
@@ -64,8 +65,18 @@ struct Config {
     // one-shot folds in MPICH's order, the ring replaced by the direct schedule at P > 2
     // (RingConfig::ref_order); 0: ring order / left folds (error-bounded against the reference)
     std::atomic<long long> reference_order{1};
-    // bumped by every ddl_set_config: tuned choices are dropped when the tunables change
+    // inside a hipGraph capture: 1 — the program forks onto the comm / compute streams as it does
+    // eagerly (recv / reduce / send overlap kept in the graph); 0 — posted serially on the
+    // captured stream
+    std::atomic<long long> capture_forked{0};
+    // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
+    // Hash of the tunables every rank of a communicator must share (they shape the collectives'
+    // programs, the fusion plans and the host chunks): algo, slice_bytes, rings, max_slices,
+    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes.
+    // Never 0 or kCfgMismatch. Local tunables (log_level, cycle_time_us, host_copy_threads,
+    // host_zero_copy, pipeline_rounds, one_rank_shortcut) are not in it.
+    uint64_t shared_hash() const;
     RingConfig ring() const {
         RingConfig c;
         c.algo = (int)algo.load();
@@ -150,8 +161,50 @@ public:
     std::shared_ptr<Communicator> keyed_data() const { return keyed_data_; }
     RingExecutor &executor() { return *exec_; }
     std::mutex &mutex() { return mu_; }
+    // RCCL's own ncclAllReduce on this communicator (bench comparator), as a user collective.
+    void rccl_allreduce(const void *send, void *recv, size_t n, int dtype, hipStream_t stream);
+    // How the ranks of this communicator are connected: kind 0 none (one rank), 1 RCCL
+    // (*ranks = ncclCommCount), 2 the test transport (*ranks = size).
+    void transport(int *kind, int *ranks) const;
+
+    // ---- order between user collectives and keyed rounds (a communicator with a token ring) ----
+    // The keyed handler reduces on a private RCCL communicator; the user's collectives run on this
+    // one. Two RCCL communicators must see their operations in the same order on every rank
+    // (their kernels can share a hardware queue), which the reference gets from
+    // MPI_THREAD_MULTIPLE (MPIBackend.cc:77-86). So every keyed round is placed after exactly U*
+    // user collectives on every rank: each rank reports how many it has issued when it joins the
+    // round (and issues no more until the round's place is known), rank 0 announces the maximum,
+    // and each rank enqueues the round's data plane once its user collectives reach U* — never
+    // before, never after. With no keyed round under way a user collective only takes a mutex.
+    long long round_freeze();            // handler: user collectives entered here; no more enter
+    void round_release(long long at);    // handler: the round goes after user collective `at`
+    void round_enter(long long at);      // handler: waits until `at` user collectives are enqueued
+    void round_unfreeze();               // handler: the round is enqueued (or failed)
+    long long user_collectives() const;  // issued so far (tests)
+    // The round release points this rank used, most recent last (bounded log; tests compare
+    // them across ranks).
+    std::vector<long long> round_log() const;
+
+    // Shared-config agreement of the direct path (ddl_allreduce & co.): at the first collective,
+    // and whenever this rank's shared tunables changed since the last agreement, every rank's
+    // Config::shared_hash() is allgathered over the data plane; a mismatch fails the collective on
+    // every rank with DDL_STATUS_CONFIG_MISMATCH before any program is built (different slice
+    // sizes would otherwise build different programs and hang RCCL). Keyed rounds carry the hash
+    // in their tokens instead (every round).
+    void agree_config(hipStream_t stream);
 
 private:
+    class UserCollective;  // scope of one user collective (the order gate above)
+    std::mutex gate_mu_;
+    std::condition_variable gate_cv_;
+    long long user_seq_ = 0;    // user collectives entered
+    long long user_done_ = 0;   // user collectives enqueued (or failed)
+    bool frozen_ = false;       // a keyed round is being placed
+    long long release_ = 0;     // while frozen: user collectives may run while user_seq_ < release_
+    std::vector<long long> round_log_;
+    uint64_t agreed_hash_ = 0;  // last shared-config hash all ranks agreed on (0: none yet)
+    uint64_t tuned_hash_ = 0;   // the shared config the tuned choices were made under
+    hipStream_t ctl_stream_ = nullptr;  // the config agreement's exchange
     // elementwise max of host floats over the ranks (the autotuner's agreement)
     void agree_max_(float *values, int count, hipStream_t stream);
 
@@ -168,7 +221,6 @@ private:
     std::unique_ptr<RequestHandler> handler_;
     std::mutex handler_mu_;
     std::map<int, TuneResult> tuned_;  // by floor(log2(bucket bytes)); guarded by mu_
-    long long tuned_epoch_ = -1;
     TuneResult tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base);
     // host pipeline resources (lazily created)
     hipStream_t h2d_ = nullptr, ring_ = nullptr, d2h_ = nullptr;
@@ -215,6 +267,10 @@ ncclComm_t rccl_split(ncclComm_t parent, int color, int key, int *rank, int *siz
 // Elementwise max over the communicator's ranks of `count` host floats (the autotuner's
 // agreement step: one ncclAllReduce(MAX) on `stream`, host-synchronising).
 void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stream);
+// values[rank] of every rank into values[0 .. size) (one ncclAllGather, host-synchronising).
+void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, hipStream_t stream);
+// Fails with DDL_STATUS_CONFIG_MISMATCH (naming every rank's hash) unless all hashes are equal.
+void check_config_agreement(int rank, const std::vector<uint64_t> &hashes);
 
 // One-rank RCCL communicator driving P virtual ranks' programs through RcclTransport (self
 // send/recv pairs) — test / diagnostic path (ddl_rccl_loopback_*), never used by ddl_init.

@@ -94,6 +94,7 @@ RankResources::RankResources(int dev) : device(dev) {
     DDL_HIP(hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));
     DDL_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     DDL_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+    DDL_HIP(hipEventCreateWithFlags(&join_cp_ev, hipEventDisableTiming));
 }
 
 RankResources::~RankResources() {
@@ -102,9 +103,11 @@ RankResources::~RankResources() {
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
     if (join_ev) (void)hipEventDestroy(join_ev);
+    if (join_cp_ev) (void)hipEventDestroy(join_cp_ev);
     if (comm) (void)hipStreamDestroy(comm);
     if (compute) (void)hipStreamDestroy(compute);
     if (staging_) (void)hipFree(staging_);
+    for (void *p : retired_) (void)hipFree(p);
 }
 
 void RankResources::ensure_events(size_t ticks) {
@@ -122,7 +125,12 @@ void *RankResources::ensure_staging(size_t bytes, bool capturing) {
         DDL_REQUIRE(!capturing, DDL_STATUS_INVALID_ARGUMENT,
                     "the staging buffer would grow (to " << bytes << " B) inside a stream capture: run this "
                     "collective once before capturing it");
-        if (staging_) {
+        if (staging_ && staging_captured_) {
+            // a captured graph may replay with this address at any time: keep it allocated
+            retired_.push_back(staging_);
+            staging_ = nullptr;
+            staging_captured_ = false;
+        } else if (staging_) {
             // a previous call may still read it on the device
             DDL_HIP(hipStreamSynchronize(comm));
             DDL_HIP(hipStreamSynchronize(compute));
@@ -133,6 +141,7 @@ void *RankResources::ensure_staging(size_t bytes, bool capturing) {
         DDL_HIP(hipMalloc(&staging_, sz));
         staging_bytes_ = sz;
     }
+    if (capturing) staging_captured_ = true;
     return staging_;
 }
 
@@ -224,10 +233,11 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     // in the HIP runtime torch loads (7.0.2; tools/graph_probe.py), although every fork / join
     // shape it uses passes alone (tools/capture_patterns.hip) — DESIGN §9. A graph is for
     // latency-bound buckets, where the reduce / exchange overlap inside one call buys little.
-    const bool serial = stream_capturing(user);
-    DDL_REQUIRE(!serial || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
+    const bool capturing = stream_capturing(user);
+    const bool serial = capturing && !config_capture_forked();
+    DDL_REQUIRE(!capturing || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
                 "this communicator's transport synchronises the host and cannot be captured into a graph");
-    const bool timing = timing_ && !serial;
+    const bool timing = timing_ && !capturing;
     hipStream_t comm = serial ? user : res_.comm, compute = serial ? user : res_.compute;
     res_.ensure_events(prog_.ticks.size());
     if (!serial) {
@@ -274,10 +284,13 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
         }
     }
     if (serial) return;
-    // the last tick waited for the last reduce (allreduce) or there is none, so the comm
-    // stream's tail covers everything
+    // join both forked streams back into the caller's: every stream a capture forked must be
+    // joined before it ends (the compute stream of a program with no reduce — broadcast,
+    // allgatherv — only waited on the fork)
     DDL_HIP(hipEventRecord(res_.join_ev, comm));
+    DDL_HIP(hipEventRecord(res_.join_cp_ev, compute));
     DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
+    DDL_HIP(hipStreamWaitEvent(user, res_.join_cp_ev, 0));
 }
 
 LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks) {
@@ -286,11 +299,13 @@ LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks)
     if (loopback) {
         loop_.reset(new RcclTransport(loopback));
         DDL_HIP(hipStreamCreateWithFlags(&loop_stream_, hipStreamNonBlocking));
+        DDL_HIP(hipEventCreateWithFlags(&loop_join_, hipEventDisableTiming));
     }
 }
 
 LocalWorld::~LocalWorld() {
     for (hipEvent_t e : loop_ev_) (void)hipEventDestroy(e);
+    if (loop_join_) (void)hipEventDestroy(loop_join_);
     if (loop_stream_) (void)hipStreamDestroy(loop_stream_);
 }
 
@@ -351,7 +366,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
     }
     // under a graph capture every rank's work goes on the captured stream in posting order
     // (as RingExecutor::run_ does): event waits are then implied by stream order
-    const bool serial = stream_capturing(user);
+    const bool serial = stream_capturing(user) && !config_capture_forked();
     auto comm = [&](int r) { return serial ? user : res_[r]->comm; };
     auto compute = [&](int r) { return serial ? user : res_[r]->compute; };
     auto loop_stream = [&] { return serial ? user : loop_stream_; };
@@ -468,7 +483,13 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
     }
     for (int r = 0; r < P_; ++r) {
         record(res_[r]->join_ev, comm(r));
+        record(res_[r]->join_cp_ev, compute(r));
         wait(user, res_[r]->join_ev);
+        wait(user, res_[r]->join_cp_ev);
+    }
+    if (loop_) {  // the transport stream too (its groups are joined through the comm streams already)
+        record(loop_join_, loop_stream());
+        wait(user, loop_join_);
     }
 }
 

@@ -36,6 +36,9 @@ public:
 // autotuning — the calls that need those must run once outside the capture first (the same
 // warm-up rule as for any captured workload).
 bool stream_capturing(hipStream_t s);
+// Config "capture_forked": inside a capture, post the program on the forked comm / compute
+// streams as eagerly (1) or serially on the captured stream (0).
+bool config_capture_forked();
 
 class RcclTransport : public Transport {
 public:
@@ -96,16 +99,22 @@ public:
 
     void ensure_events(size_t ticks);
     // Staging of at least `bytes`; growing it is refused while the caller's stream is captured.
+    // Once a capture has used the staging buffer, a graph may hold its address for as long as
+    // the graph lives: a later (eager) growth retires the buffer instead of freeing it — it stays
+    // allocated until these resources are destroyed, so replaying the graph stays valid.
     void *ensure_staging(size_t bytes, bool capturing = false);
+    size_t retired_staging() const { return retired_.size(); }
 
     int device;
     hipStream_t comm = nullptr, compute = nullptr;
     std::vector<hipEvent_t> comm_ev, red_ev, pre_ev, post_ev;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr, join_cp_ev = nullptr;
 
 private:
     void *staging_ = nullptr;
     size_t staging_bytes_ = 0;
+    bool staging_captured_ = false;  // a graph capture has used staging_
+    std::vector<void *> retired_;    // captured staging buffers replaced by a larger one
 };
 
 // Optional timing of the reduce kernels on the compute stream (bench.py's roofline leg):
@@ -177,6 +186,7 @@ private:
     std::unique_ptr<RcclTransport> loop_;
     hipStream_t loop_stream_ = nullptr;
     std::vector<hipEvent_t> loop_ev_;
+    hipEvent_t loop_join_ = nullptr;
     long long loop_pairs_ = 0;
 };
 

@@ -436,22 +436,43 @@ Agreed decide(bool cached, const std::vector<uint32_t> &idx, const std::vector<s
 }  // namespace
 
 Agreed negotiate_root(ControlChannel &ch, bool cached, const std::vector<uint32_t> &idx,
-                      const std::vector<std::string> &strs, int request_type) {
+                      const std::vector<std::string> &strs, int request_type,
+                      const std::function<long long()> &snapshot) {
+    const uint64_t cfg = config().shared_hash();
     Token t;
     t.type = cached ? TOKEN_SYNC_CACHED : TOKEN_SYNC;
     t.request = (uint8_t)request_type;
+    t.cfg = cfg;
     t.msg = cached ? ch.cache.encode(idx) : encode_keys(strs);
     ch.send(t);  // the proposal to every member
     std::vector<Token> answers(ch.size() - 1);
+    bool cfg_ok = true;
+    long long release = -1;
+    std::vector<uint64_t> hashes(ch.size(), cfg);
     for (int r = 1; r < ch.size(); ++r) {
         ch.recv_from(r, answers[r - 1], -1);
         DDL_REQUIRE(answers[r - 1].type == t.type, DDL_STATUS_COMM_ERROR,
                     "token protocol: expected SYNC from rank " << r << ", got " << (int)answers[r - 1].type);
+        hashes[r] = answers[r - 1].cfg;
+        cfg_ok = cfg_ok && answers[r - 1].cfg == cfg;
+        release = std::max<long long>(release, answers[r - 1].seq);
     }
+    if (snapshot) release = std::max(release, snapshot());
     Agreed a = decide(cached, idx, strs, answers, ch);
+    a.cfg_ok = cfg_ok;
+    a.release = release;
+    if (!cfg_ok) {
+        try {
+            check_config_agreement(0, hashes);
+        } catch (const Error &e) {
+            DDL_LOG(0, "keyed round refused: " << e.msg);
+        }
+    }
     Token c;
     c.type = cached ? TOKEN_COMMUNICATE_CACHED : TOKEN_COMMUNICATE;
     c.request = (uint8_t)request_type;
+    c.cfg = cfg_ok ? cfg : kCfgMismatch;
+    c.seq = release;
     c.msg = cached ? ch.cache.encode(a.idx) : encode_keys(a.wire);
     ch.send(c);  // the agreed set to every member
     if (cached) {
@@ -468,14 +489,17 @@ void negotiate_root_finish(ControlChannel &) {}
 
 Agreed negotiate_member(ControlChannel &ch, const Token &sync,
                         const std::function<std::vector<std::string>(const std::vector<std::string> &)> &by_string,
-                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index) {
+                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index,
+                        const std::function<long long()> &snapshot) {
     DDL_REQUIRE(sync.type == TOKEN_SYNC || sync.type == TOKEN_SYNC_CACHED, DDL_STATUS_COMM_ERROR,
                 "token protocol: expected SYNC, got " << (int)sync.type);
     const bool cached = sync.type == TOKEN_SYNC_CACHED;
     Token s;
     s.type = sync.type;
     s.request = sync.request;
+    s.cfg = config().shared_hash();
     s.msg = cached ? ch.cache.encode(by_index(ch.cache.decode(sync.msg))) : encode_keys(by_string(decode_keys(sync.msg)));
+    s.seq = snapshot ? snapshot() : -1;
     ch.send(s);  // this rank's intersection with the proposal
     Token c;
     ch.recv(c, -1);
@@ -483,6 +507,11 @@ Agreed negotiate_member(ControlChannel &ch, const Token &sync,
                 "token protocol: expected COMMUNICATE, got " << (int)c.type);
     Agreed a;
     a.cached = cached;
+    a.cfg_ok = c.cfg != kCfgMismatch;
+    a.release = c.seq;
+    if (!a.cfg_ok)
+        DDL_LOG(0, "keyed round refused: the ranks' shared tunables differ (this rank's config hash " << std::hex
+                                                                                                   << s.cfg << std::dec << ")");
     if (cached) {
         a.idx = ch.cache.decode(c.msg);
         ++ch.cached_rounds;
@@ -557,9 +586,20 @@ void RequestHandler::root_round_() {
                 if (kv.second.type == type) strs.push_back(wire_id(kv.first));
         cached = cached && !idx.empty();
     }
-    const Agreed a = negotiate_root(ch, cached, idx, strs, type);
-    execute_(agreed_ids_(a));
+    const Agreed a = negotiate_root(ch, cached, idx, strs, type, [this] { return owner_->round_freeze(); });
     negotiate_root_finish(ch);
+    run_agreed_(a);
+}
+
+void RequestHandler::run_agreed_(const Agreed &a) {
+    struct Unfreeze {  // user collectives go on whatever happens to the round
+        Communicator *c;
+        ~Unfreeze() { c->round_unfreeze(); }
+    } unfreeze{owner_};
+    owner_->round_release(a.release);
+    std::vector<ReqId> ids = agreed_ids_(a);
+    owner_->round_enter(a.release);
+    execute_(ids, a.cfg_ok ? DDL_STATUS_OK : DDL_STATUS_CONFIG_MISMATCH);
 }
 
 // Other ranks: answer the SYNC once the first proposed id is registered here (the reference
@@ -586,8 +626,9 @@ void RequestHandler::member_round_(Token &t) {
             for (uint32_t i : proposed)
                 if (held(i)) mine.push_back(i);
             return mine;
-        });
-    execute_(agreed_ids_(a));
+        },
+        [this] { return owner_->round_freeze(); });
+    run_agreed_(a);
 }
 
 void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
@@ -1181,7 +1222,7 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
     }
 }
 
-void RequestHandler::execute_(const std::vector<ReqId> &ids) {
+void RequestHandler::execute_(const std::vector<ReqId> &ids, int forced) {
     if (ids.empty()) return;
     // phase times of the round at log level 2 (take / enqueue / wait + done, microseconds)
     using clk = std::chrono::steady_clock;
@@ -1211,10 +1252,10 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     }
     std::vector<Done> dones;
     size_t nplans = 0;
-    int status = DDL_STATUS_OK;
+    int status = forced;
     const clk::time_point t1 = timed ? clk::now() : clk::time_point();
     round_events_.clear();
-    try {
+    if (forced == DDL_STATUS_OK) try {
         for (const Request &r : reqs)
             DDL_REQUIRE(r.type == reqs[0].type, DDL_STATUS_COMM_ERROR, "agreed requests of mixed types");
         switch (reqs[0].type) {
@@ -1249,7 +1290,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
     // the hand-off to the completion thread (a thread wake-up each way) is saved
     if (idle && (!pipelined || status != DDL_STATUS_OK || bytes <= kInlineRoundBytes)) {
         complete_(rd);
-        if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
+        if (status != DDL_STATUS_OK && status != forced) fail(status, "keyed collective failed");
         return;
     }
     unsigned long long seq;
@@ -1265,7 +1306,7 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids) {
         std::unique_lock<std::mutex> lk(done_mu_);
         done_cv_.wait(lk, [&] { return rounds_done_ >= seq; });
     }
-    if (status != DDL_STATUS_OK) fail(status, "keyed collective failed");
+    if (status != DDL_STATUS_OK && status != forced) fail(status, "keyed collective failed");
 }
 
 namespace {

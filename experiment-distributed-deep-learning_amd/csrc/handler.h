@@ -134,17 +134,29 @@ std::shared_ptr<ControlChannel> &standalone_control();
 //           id is registered), answers rank 0, then receives COMMUNICATE.
 // A proposal made only of ids agreed in earlier rounds travels as indices into the channel's
 // IdCache (TOKEN_*_CACHED) and is intersected by index; otherwise as "Type::key" strings.
+// Every token also carries the sender's Config::shared_hash(): rank 0 compares the members'
+// with its own and the COMMUNICATE says whether they all agree (cfg_ok); a round whose ranks
+// disagree takes its agreed requests out on every rank and fails them with
+// DDL_STATUS_CONFIG_MISMATCH instead of running them. `snapshot` (optional) freezes the rank's
+// user collectives and returns how many it has issued (Communicator::round_freeze): members
+// call it right before answering, rank 0 once every answer is in; the COMMUNICATE carries the
+// maximum (release: the round goes after that many user collectives on every rank, -1 without
+// snapshots).
 struct Agreed {
     bool cached = false;
     std::vector<uint32_t> idx;      // cached round: indices into ch.cache
     std::vector<std::string> wire;  // string round: ids, sorted (their (type, key) order)
+    bool cfg_ok = true;
+    long long release = -1;
 };
 Agreed negotiate_root(ControlChannel &ch, bool cached, const std::vector<uint32_t> &idx,
-                      const std::vector<std::string> &strs, int request_type = kReqAllreduce);
+                      const std::vector<std::string> &strs, int request_type = kReqAllreduce,
+                      const std::function<long long()> &snapshot = nullptr);
 void negotiate_root_finish(ControlChannel &ch);
 Agreed negotiate_member(ControlChannel &ch, const Token &sync,
                         const std::function<std::vector<std::string>(const std::vector<std::string> &)> &by_string,
-                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index);
+                        const std::function<std::vector<uint32_t>(const std::vector<uint32_t> &)> &by_index,
+                        const std::function<long long()> &snapshot = nullptr);
 
 class RequestHandler {
 public:
@@ -160,7 +172,12 @@ private:
     void main_();
     void root_round_();
     void member_round_(Token &first);
-    void execute_(const std::vector<ReqId> &ids);
+    // Runs the agreed requests; `forced` != OK takes them out and fails them with that status
+    // (a round whose ranks' shared tunables differ) without stopping the handler.
+    void execute_(const std::vector<ReqId> &ids, int forced = DDL_STATUS_OK);
+    // root_round_ / member_round_ after the agreement: places the round among the user collectives
+    // (Communicator::round_release / round_enter), executes it, lifts the freeze
+    void run_agreed_(const Agreed &a);
     std::vector<ReqId> agreed_ids_(const Agreed &a);  // learns new ids (string rounds)
     void forget_ids_();                                 // the id table was cleared
     void mark_cached_(const ReqId &id, Request &r);

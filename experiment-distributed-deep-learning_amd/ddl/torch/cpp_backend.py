@@ -17,7 +17,9 @@ DEFAULT_LIB = os.path.join(_PKG_ROOT, 'lib', 'libddl_amd.so')
 DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_BFLOAT16, DT_HALF, DT_UINT64 = 1, 2, 3, 9, 14, 19, 23
 STATUS_OK = 0
 STATUS_NAMES = {0: 'OK', 1: 'COMM_ERROR', 2: 'ERROR_UNKNOWN', 3: 'INVALID_ARGUMENT',
-                4: 'UNSUPPORTED_DTYPE', 5: 'HIP_ERROR', 6: 'NOT_INITIALIZED', 7: 'DUPLICATE_KEY'}
+                4: 'UNSUPPORTED_DTYPE', 5: 'HIP_ERROR', 6: 'NOT_INITIALIZED', 7: 'DUPLICATE_KEY',
+                8: 'CONFIG_MISMATCH'}
+STATUS_CONFIG_MISMATCH = 8
 OP_SUM = 0
 MEMORY_DEVICE, MEMORY_HOST = 0, 1  # enum ddl_memory
 
@@ -70,6 +72,9 @@ class CPPBackend:
         sig('ddl_control_negotiate', ci, ctypes.c_char_p, ctypes.c_char_p, sz)
         sig('ddl_control_stats', ci, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong))
         sig('ddl_allreduce_variant', ci, cid, vp, vp, sz, ci, ci, vp, ci)
+        sig('ddl_comm_transport', ci, cid, ctypes.POINTER(ci), ctypes.POINTER(ci))
+        sig('ddl_testing_round_log', ci, cid, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong), ci,
+            ctypes.POINTER(ci))
         sig('ddl_allreduce_host', ci, cid, vp, vp, sz, ci, ci)
         sig('ddl_ring_program', ci, ci, ci, sz, ci, ctypes.POINTER(ctypes.c_longlong), sz, ctypes.POINTER(sz))
         sig('ddl_finalize', ci)

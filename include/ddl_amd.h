@@ -60,7 +60,9 @@ enum ddl_status {
     DDL_STATUS_UNSUPPORTED_DTYPE = 4,
     DDL_STATUS_HIP_ERROR = 5,
     DDL_STATUS_NOT_INITIALIZED = 6,
-    DDL_STATUS_DUPLICATE_KEY = 7 /* TensorCommunicateRequest.h:21: one pending request per key */
+    DDL_STATUS_DUPLICATE_KEY = 7, /* TensorCommunicateRequest.h:21: one pending request per key */
+    DDL_STATUS_CONFIG_MISMATCH = 8 /* the ranks' shared tunables differ (see ddl_set_config): the
+                                      collective or keyed round fails on every rank, nothing runs */
 };
 
 /* Where a keyed request's buffers live: SURVEY §8(b)'s device_ptr_flag. The reference's op is
@@ -98,28 +100,6 @@ int ddl_get_unique_id(void *out, size_t len);
 /* Creates the world communicator for this process (one process per GPU). */
 int ddl_init(int rank, int size, int device, const void *unique_id, size_t len);
 
-/* TEST HARNESS ONLY (not a product path): a world communicator whose point-to-point groups and
- * the autotuner's max-reduce go through host callbacks instead of RCCL, so the multi-process
- * engine — control channel, keyed handler, fusion, schedules, streams, kernels — can run as
- * several processes sharing one GPU (RCCL refuses two ranks on one device). `comm_tag` names
- * the communicator (0 = world; splits agree on theirs), so the callbacks can keep concurrent
- * communicators apart. The engine synchronises the group's stream, stages every
- * send into host memory, calls the group callback — which must complete the whole exchange on
- * the host buffers before it returns, 0 = success — and copies the received host buffers to
- * the device. `peer` is a world rank (splits map their ranks); `comm_tag` differs between any two
- * communicators that share a pair of ranks. `max` is no longer called (the autotuner agrees
- * through `group`); it may be NULL. */
-typedef struct ddl_p2p_op {
-    int send;     /* 1 send, 0 receive */
-    int peer;     /* world rank of the peer */
-    int tag;      /* matches a send with its receive inside one group (posting order per tag) */
-    void *ptr;    /* host staging buffer of `bytes` */
-    size_t bytes;
-} ddl_p2p_op;
-typedef int (*ddl_test_group_fn)(long long comm_tag, const ddl_p2p_op *ops, int count, void *user);
-typedef int (*ddl_test_max_fn)(long long comm_tag, float *values, int count, void *user);
-int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn group, ddl_test_max_fn max,
-                            void *user);
 /* Same, for a single-process world (size 1); no RCCL involved. */
 int ddl_init_single(int device);
 /* Optional control channel for keyed requests at size > 1 (ring of TCP links, replaces the
@@ -128,23 +108,9 @@ int ddl_init_single(int device);
  * separated by ';', in rank order. */
 int ddl_control_listen(char *endpoint_out, size_t len);
 int ddl_control_connect(const char *endpoints);
-/* Control channel without a world communicator (tools / CPU tests of the token protocol). */
-int ddl_control_connect_ranked(int rank, int size, const char *endpoints);
-/* One negotiation round over the control channel with a fixed key set ('\n'-separated):
- * writes the agreed keys ('\n'-separated, lexicographic) to out. Same protocol as the
- * keyed-request handler, without the data plane. */
-int ddl_control_negotiate(const char *keys, char *out, size_t len);
 /* Negotiation rounds so far by token form: ids as strings, or as indices into the table of ids
  * agreed in earlier rounds (a repeated key set, e.g. every training step's gradients). */
 int ddl_control_stats(long long *string_rounds, long long *cached_rounds);
-/* Several independent token rings in one process (tools, CPU tests of per-communicator rings):
- * _open listens and returns a handle (0 on failure) and "ip:port"; _connect joins the ring of
- * `size` ranks; _negotiate is ddl_control_negotiate on that ring. Every communicator of size > 1
- * made by split_communicator owns such a ring (RingTokenCommunicateController.cc:53-79). */
-long long ddl_control_channel_open(char *endpoint_out, size_t len);
-int ddl_control_channel_connect(long long channel, int rank, int size, const char *endpoints);
-int ddl_control_channel_negotiate(long long channel, const char *keys, char *out, size_t len);
-int ddl_control_channel_close(long long channel);
 int ddl_finalize(void);
 int ddl_is_initialized(void);
 
@@ -169,9 +135,19 @@ int ddl_is_initialized(void);
  * With "tune" = 1 (default) a communicator of P > 1 ranks picks the schedule (algo, rings,
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
- * Every rank must set the same tunables; any ddl_set_config drops the tuned choices. */
+ * The shared tunables (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, tune,
+ * fusion_pipeline_bytes, reference_order, host_chunk_bytes) must be equal on every rank of a
+ * communicator: the ranks agree on a hash of them at a communicator's first collective and
+ * whenever this rank's values changed since (change them on every rank between the same two
+ * collectives), and every keyed round carries the hash; on a mismatch the collective or round
+ * fails on every rank with DDL_STATUS_CONFIG_MISMATCH instead of building different programs.
+ * A change of the shared tunables drops the tuned choices; the other keys are per process. */
 int ddl_set_config(const char *key, long long value);
 long long ddl_get_config(const char *key);
+
+/* How the ranks of communicator `id` are connected: *kind 0 = one rank (no transport), 1 = RCCL
+ * (*ranks = ncclCommCount of its RCCL communicator), 2 = the test transport (*ranks = size). */
+int ddl_comm_transport(ddl_communicator_id id, int *kind, int *ranks);
 
 /* ---- reference c_api.h surface ----------------------------------------------------- */
 int communicator_rank(ddl_communicator_id id);
@@ -210,22 +186,18 @@ int ddl_allgather(ddl_communicator_id id, const void *send, size_t send_elements
 int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, size_t elements,
                        int dtype, int op);
 
-/* Comparator entry for measurement: variant 0 = the engine's ring (= ddl_allreduce),
- * variant 1 = RCCL's built-in ncclAllReduce on the same communicator. */
-int ddl_allreduce_variant(ddl_communicator_id id, const void *send, void *recv, size_t elements,
-                          int dtype, int op, void *hip_stream, int variant);
-
 /* Autotuner record for the size class of `bucket_bytes` on communicator `id`: *chosen = index
  * of the schedule in use (-1 = class not tuned yet), *count = candidates; for the first
  * max_candidates of them configs[4i..4i+3] = {algo, rings, slice_bytes, max_slices} and
  * ms[i] = mean time per allreduce (max over ranks). configs/ms may be NULL. */
 int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, int *count,
                     long long *configs, float *ms, int max_candidates);
-/* The same tuning procedure on ddl_local_ring_allreduce's P virtual ranks (one GPU, copies
- * for the transport; no cross-rank agreement needed): a test/diagnostic entry. */
-int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
-                   long long *configs, float *ms, int max_candidates);
-
+/* Order between the two (the reference's MPI_THREAD_MULTIPLE, MPIBackend.cc:77-86): a
+ * communicator with a token ring reduces its keyed rounds on a private RCCL communicator, and
+ * every round is placed after the same number of the communicator's direct collectives
+ * (ddl_allreduce, ddl_broadcast, ddl_allgather[v], ddl_allreduce_host, split_communicator) on
+ * every rank, so both RCCL communicators see their work in one order everywhere. A direct
+ * collective issued while a round is being placed waits for the placement (one negotiation). */
 /* Keyed asynchronous request (TF op Allreduce semantics): registered under `key`,
  * negotiated across ranks, fused by dtype in lexicographic key order, then `done` fires.
  * `in`/`out` must stay valid until `done`. Work is ordered after `hip_stream`'s current
@@ -278,103 +250,6 @@ int ddl_wait_all(ddl_communicator_id id);
  * (3 * elements * sizeof(T) per launch) and summed kernel milliseconds, then resets. */
 int ddl_kernel_timing(ddl_communicator_id id, int on);
 int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes, double *ms);
-
-/* ---- HIP kernels exposed for measurement and tests ----------------------------------- */
-/* acc[i] = acc[i] + in[i]  (the per-hop reduce of the ring). */
-int ddl_reduce_local(void *acc, const void *in, size_t elements, int dtype, void *hip_stream);
-/* out[i] = a[i] + b[i]; out may alias a or b. */
-int ddl_reduce_sum2(void *out, const void *a, const void *b, size_t elements, int dtype,
-                    void *hip_stream);
-/* Kernel variant selection for measurement (bit set; -1 = the engine's default):
- * 1 = non-temporal loads of a, 2 = non-temporal loads of b, 4 = non-temporal stores,
- * 8 = operand b staged through LDS by global_load_lds_dwordx4, 16 = write-through (sc0 sc1)
- * stores of out (ignored with 8). */
-int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b,
-                            size_t elements, int dtype, void *hip_stream);
-/* The direct schedule's fold: out[i] = a[i] + ins[0][i] + ... + ins[nb-1][i], 1 <= nb <= 15,
- * left to right; fp16/bf16 accumulate in fp32 and round once. out may alias a. */
-int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
-                    void *hip_stream);
-/* The same fold in a given order of the inputs x_0 = a, x_1 = ins[0], ...: order 0 left to right,
- * 1 MPICH 3.3.2's MPI_Allreduce order above 2048 bytes (the first 2*rem inputs folded in pairs,
- * then a pairwise tree over the pof2 leaves), 2 its order up to 2048 bytes (binomial tree).
- * fp16/bf16 fold left in fp32 whatever the order. The reference-order schedules launch this. */
-int ddl_reduce_fold_ordered(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
-                            int order, void *hip_stream);
-
-/* Fusion pack/unpack (device): gathers `count` segments into one contiguous buffer and
- * scatters it back (executeCommunicatePlan_'s memcpy in/out, MPIRingTokenCommunication.cc:548-733). */
-int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream);
-int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int count,
-               void *hip_stream);
-
-/* ---- single-GPU rehearsal of the ring schedule --------------------------------------- */
-/* Runs the exact per-rank ring schedule for `nranks` virtual ranks inside this process on
- * the current device, with device-to-device copies standing in for RCCL send/recv.
- * sends[r]/recvs[r] are rank r's buffers. Stream-ordered on hip_stream. */
-int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *recvs,
-                             size_t elements, int dtype, int op, void *hip_stream);
-
-/* Broadcast / allgatherv of P virtual ranks on one GPU (as ddl_local_ring_allreduce). */
-int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream);
-int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
-                         const size_t *displs, int dtype, void *hip_stream);
-
-/* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
- * A one-rank RCCL communicator (ncclGetUniqueId + ncclCommInitRank, the calls ddl_init makes at
- * size > 1) carries the matched send/recv pairs of P virtual ranks' programs as self-send /
- * self-recv pairs, posted through the engine's RcclTransport::group in matching order — the
- * data path that replaces MPI_Allreduce (MPICommunicator.cc:14-28) with RCCL doing the moves.
- * _split runs ncclCommSplit (MPICommunicator.cc:92-101) on the current loopback communicator;
- * the split becomes current (color < 0: *rank = -1, *size = 0, nothing changes). _max is the
- * autotuner's cross-rank agreement (ncclAllReduce(MAX)); _tune runs the autotuner with the
- * candidates over RCCL and that agreement. _stats: self pairs posted so far for P ranks. */
-int ddl_rccl_loopback_init(int device);
-int ddl_rccl_loopback_split(int color, int key, int *rank, int *size);
-int ddl_rccl_loopback_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements,
-                                int dtype, void *hip_stream);
-int ddl_rccl_loopback_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
-                                void *hip_stream);
-int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
-                                 const size_t *displs, int dtype, void *hip_stream);
-/* RcclTransport::allgather (ncclAllGather, the gather-fold schedule's transport) on the one-rank
- * loopback communicator: recv[0..bytes) = send. */
-int ddl_rccl_loopback_allgather(const void *send, void *recv, size_t bytes, void *hip_stream);
-int ddl_rccl_loopback_max(float *values, int count, void *hip_stream);
-int ddl_rccl_loopback_tune(int nranks, size_t elements, int dtype, void *hip_stream, int *chosen, int *count,
-                           long long *configs, float *ms, int max_candidates);
-int ddl_rccl_loopback_stats(int nranks, long long *pairs);
-int ddl_rccl_loopback_finalize(void);
-
-/* ---- schedule introspection (host only, no GPU needed) -------------------------------- */
-int ddl_ring_count(int nranks, int max_rings);
-/* perm_out[p] = rank at ring position p (length nranks). */
-int ddl_ring_perm(int nranks, int max_rings, int ring, int *perm_out);
-/* Element range [begin, end) of (ring, chunk) in a bucket of `elements` of `dtype`. */
-int ddl_chunk_range(size_t elements, int dtype, int nranks, int rings, int ring, int chunk,
-                    size_t *begin, size_t *end);
-/* Rings and reduce-scatter slices the schedule uses for a bucket under the current config. */
-int ddl_ring_shape(size_t elements, int dtype, int nranks, int *rings, int *slices);
-/* Rank `rank`'s ring program as rows of 8 int64:
- *   send/recv: {tick, 0=send|1=recv, peer, ring, buffer(0 in, 1 out, 2 staging), offset, count, wait_tick}
- *   reduce:    {tick, 2, -1, segment, 1 (out), offset, count, staging offset}  (out = in + staging)
- *   fold:      {tick, 3, nb, input i, 1 (out), offset, count, staging offset of input i}
- *              (direct schedule: out = in + input 0 + ... + input nb-1, fp16/bf16 in fp32)
- * Offsets and counts in elements. Host only. */
-int ddl_ring_program(int rank, int nranks, size_t elements, int dtype, long long *ops_out,
-                     size_t max_ops, size_t *nops);
-/* Broadcast program of `rank` (buffer 1 = the broadcast buffer) and allgatherv program
- * (buffer 0 = send, 1 = recv), same row format; copy rows: {tick, 4, -1, -1, 1, dst offset,
- * count, src offset in buffer 0}. */
-int ddl_broadcast_program(int rank, int nranks, int root, size_t elements, int dtype, long long *ops_out,
-                          size_t max_ops, size_t *nops);
-int ddl_allgather_program(int rank, int nranks, const size_t *counts, const size_t *displs, int dtype,
-                          long long *ops_out, size_t max_ops, size_t *nops);
-/* Fusion plans (requestBegin, elementBegin, requestEnd, elementEnd) over `count` requests of
- * one dtype group, capped at `limit` bytes (makeCollectiveCommunicatePlan,
- * MPIRingTokenCommunication.cc:495-546). plans_out holds 4*max_plans entries. */
-int ddl_make_plans(const size_t *elements, const size_t *esizes, size_t count, size_t limit,
-                   size_t *plans_out, size_t max_plans, size_t *nplans);
 
 #ifdef __cplusplus
 }

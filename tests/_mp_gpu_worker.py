@@ -411,10 +411,97 @@ def check_dp_training(ctx):
     assert logs == {'loss': (P - 1) / 2, 'acc': float(P - 1)}
 
 
+def check_config_mismatch(ctx):
+    """VERDICT r2 next #4(b) on the real engine: every rank changes a shared tunable at the same
+    point, the last rank to a different value than the others — the next ddl_allreduce returns
+    DDL_STATUS_CONFIG_MISMATCH on EVERY rank (the agreement runs before any program is built), a
+    keyed request completes with that status on every rank (its round's tokens carry the hash),
+    and once the values agree again both work."""
+    import threading
+
+    import _helpers as h
+    from ddl.torch.cpp_backend import DONE_FN
+    torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
+    s = torch.cuda.current_stream().cuda_stream
+    x = torch.full((4099,), float(r), device='cuda')
+    slice_bytes = (96 << 10) if r == P - 1 else (64 << 10)
+    with h.config(lib, slice_bytes=slice_bytes):
+        st = lib.ddl_allreduce(comm.id, x.data_ptr(), x.data_ptr(), x.numel(), h.DT_FLOAT, 0, s)
+        assert st == 8, (st, lib.ddl_last_error())
+        assert b'slice_bytes' in lib.ddl_last_error()
+        got, ev = [], threading.Event()
+
+        @DONE_FN
+        def done(status, user):
+            got.append(status)
+            ev.set()
+        y = torch.full((300,), float(r), device='cuda')
+        assert lib.ddl_allreduce_submit(comm.id, b'cfg_mismatch', y.data_ptr(), y.data_ptr(), 300, h.DT_FLOAT, 0, s,
+                                        done, None) == 0
+        assert ev.wait(60) and got == [8], got
+        assert lib.ddl_wait_all(comm.id) == 0
+    # agreed again (every rank back to the same values): both paths work
+    assert lib.ddl_allreduce(comm.id, x.data_ptr(), x.data_ptr(), x.numel(), h.DT_FLOAT, 0, s) == 0, lib.ddl_last_error()
+    assert torch.equal(x, torch.full_like(x, float(P * (P - 1) // 2)))
+    from ddl.torch.tensor_communicate import allreduce_async
+    z = torch.full((300,), float(r), device='cuda')
+    assert torch.equal(allreduce_async(z, 'cfg_ok', comm).wait(timeout=60), torch.full_like(z, float(P * (P - 1) // 2)))
+
+
+def check_keyed_round_order(ctx):
+    """keyed rounds (on the handler's private communicator) and direct
+    ddl_allreduce calls (on the world) issued concurrently from two threads, with per-rank random
+    pacing: every rank places every round after the same number of direct collectives (identical
+    round logs), and every result is exact."""
+    import random
+    import threading
+    import time
+
+    import _helpers as h
+    torch, lib, comm, P, r, dist = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['dist']
+    from ddl.torch.tensor_communicate import allreduce_async
+    n_keyed, n_user = 24, 24
+    rnd = random.Random(1000 + r)
+    keyed = [torch.full((1000 + i,), float(r + i), device='cuda') for i in range(n_keyed)]
+    errs = []
+
+    def submitter():
+        try:
+            hs = []
+            for i, t in enumerate(keyed):
+                time.sleep(rnd.random() * 0.004)
+                hs.append(allreduce_async(t, f'order_{i:02d}', comm))
+            for i, hd in enumerate(hs):
+                want = float(P * (P - 1) // 2 + P * i)
+                assert torch.equal(hd.wait(timeout=120), torch.full_like(keyed[i], want)), i
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+    th = threading.Thread(target=submitter)
+    th.start()
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        for j in range(n_user):
+            time.sleep(rnd.random() * 0.004)
+            u = torch.full((4099,), float(r * j), device='cuda')
+            assert lib.ddl_allreduce(comm.id, u.data_ptr(), u.data_ptr(), u.numel(), h.DT_FLOAT, 0,
+                                     stream.cuda_stream) == 0, lib.ddl_last_error()
+            assert torch.equal(u, torch.full_like(u, float(j * P * (P - 1) // 2))), j
+    th.join(timeout=180)
+    assert not th.is_alive() and not errs, errs
+    users, cnt = ctypes.c_longlong(), ctypes.c_int()
+    rel = (ctypes.c_longlong * 4096)()
+    assert lib.ddl_testing_round_log(comm.id, ctypes.byref(users), rel, 4096, ctypes.byref(cnt)) == 0
+    mine = (users.value, list(rel[:min(cnt.value, 4096)]))
+    everyone = [None] * P
+    dist.all_gather_object(everyone, mine)
+    assert all(e == mine for e in everyone), everyone
+    assert mine[1] and mine[1] == sorted(mine[1]), mine
+
+
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
           check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
           check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model,
-          check_dp_training_overlap]
+          check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]
 
 
 def worker(rank, world, port, q):

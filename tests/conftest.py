@@ -24,7 +24,7 @@ def source_hash():
     csrc = os.path.join(PKG, 'csrc')
     names = sorted(os.path.basename(f) for pat in ('*.h', '*.cpp', '*.hip') for f in glob.glob(os.path.join(csrc, pat)))
     h = hashlib.sha1()
-    for f in [os.path.join(csrc, n) for n in names] + [os.path.join(ROOT, 'include', 'ddl_amd.h')]:
+    for f in [os.path.join(csrc, n) for n in names] + [os.path.join(ROOT, 'include', h) for h in ('ddl_amd.h', 'ddl_amd_testing.h')]:
         with open(f, 'rb') as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

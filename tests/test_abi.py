@@ -10,11 +10,27 @@ import pytest
 from conftest import PKG, ROOT
 
 HEADER = os.path.join(ROOT, 'include', 'ddl_amd.h')
+TESTING_HEADER = os.path.join(ROOT, 'include', 'ddl_amd_testing.h')
 LIB = os.path.join(PKG, 'lib', 'libddl_amd.so')
 
+# reference src/cpp/c_api.h:15-41 (the ctypes surface, cpp_backend.py:47-78)
+REFERENCE_C_API = {'communicator_rank', 'communicator_size', 'world_communicator', 'split_communicator',
+                   'detach_communicator', 'py_info', 'py_debug', 'py_error'}
+# what a framework binding needs: lifecycle, tunables, the data plane, keyed requests, and the
+# measurement hooks on a live communicator
+DEPLOYMENT = {
+    'ddl_version', 'ddl_build_info', 'ddl_last_error', 'ddl_dtype_name', 'ddl_dtype_size',
+    'ddl_get_unique_id', 'ddl_init', 'ddl_init_single', 'ddl_control_listen', 'ddl_control_connect',
+    'ddl_control_stats', 'ddl_finalize', 'ddl_is_initialized', 'ddl_set_config', 'ddl_get_config',
+    'ddl_comm_transport', 'ddl_allreduce', 'ddl_broadcast', 'ddl_allgatherv', 'ddl_allgather',
+    'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit',
+    'ddl_allgather_submit', 'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem',
+    'ddl_allreduce_submit_batch_mem', 'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all',
+    'ddl_kernel_timing', 'ddl_kernel_stats'}
 
-def declared_functions():
-    text = open(HEADER).read()
+
+def declared_functions(header=HEADER):
+    text = open(header).read()
     text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
     text = '\n'.join(line for line in text.splitlines() if not line.lstrip().startswith('typedef'))
     names = re.findall(r'^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(', text, flags=re.M)
@@ -23,18 +39,46 @@ def declared_functions():
 
 def test_header_declares_reference_c_api_names():
     names = declared_functions()
-    # reference src/cpp/c_api.h:15-41 (the ctypes surface, cpp_backend.py:47-78)
-    for n in ('communicator_rank', 'communicator_size', 'world_communicator', 'split_communicator',
-              'detach_communicator', 'py_info', 'py_debug', 'py_error'):
-        assert n in names
+    assert REFERENCE_C_API <= set(names)
     assert 'ddl_allreduce' in names and 'ddl_allreduce_submit' in names
+
+
+def test_deployment_header_is_only_the_deployment_surface():
+    """include/ddl_amd.h declares the deployment surface plus the reference's
+    c_api.h names and nothing else; the test transport, virtual-rank worlds, the RCCL loopback,
+    raw kernels and introspection live in include/ddl_amd_testing.h."""
+    names = set(declared_functions())
+    assert names == DEPLOYMENT | REFERENCE_C_API, (sorted(names - DEPLOYMENT - REFERENCE_C_API),
+                                                   sorted(DEPLOYMENT | REFERENCE_C_API - names))
+    testing = set(declared_functions(TESTING_HEADER))
+    assert not testing & names
+    for n in ('ddl_init_test_transport', 'ddl_local_ring_allreduce', 'ddl_rccl_loopback_init', 'ddl_ring_program',
+              'ddl_reduce_local', 'ddl_allreduce_variant', 'ddl_control_channel_open'):
+        assert n in testing, n
 
 
 def test_every_declared_symbol_is_exported():
     out = subprocess.run(['nm', '-D', '--defined-only', LIB], capture_output=True, text=True, check=True).stdout
     exported = set(line.split()[-1] for line in out.splitlines() if ' T ' in line)
-    missing = [n for n in declared_functions() if n not in exported]
+    declared = declared_functions() + declared_functions(TESTING_HEADER)
+    missing = [n for n in declared if n not in exported]
     assert not missing, f'declared but not exported: {missing}'
+
+
+def test_test_transport_refused_without_opt_in(lib):
+    """ddl_init_test_transport (host-synchronised groups, no RCCL) refuses unless the process
+    opts in with DDL_ALLOW_TEST_TRANSPORT=1, so a binding cannot pick it up by mistake."""
+    fn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p)(
+        lambda *a: 0)
+    lib.ddl_init_test_transport.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, type(fn), ctypes.c_void_p,
+                                            ctypes.c_void_p]
+    old = os.environ.pop('DDL_ALLOW_TEST_TRANSPORT', None)
+    try:
+        assert lib.ddl_init_test_transport(0, 2, 0, fn, None, None) == 3
+        assert b'DDL_ALLOW_TEST_TRANSPORT' in lib.ddl_last_error()
+    finally:
+        if old is not None:
+            os.environ['DDL_ALLOW_TEST_TRANSPORT'] = old
 
 
 def test_library_loads_via_ctypes_and_reports(lib):

@@ -147,3 +147,39 @@ def test_capture_refuses_to_grow_staging(loop, gpu):
         with torch.cuda.stream(s):
             assert _loop_allreduce(lib, ins, outs, n, DT_FLOAT, s.cuda_stream) == 0, lib.ddl_last_error()
         torch.cuda.synchronize()
+
+
+def test_captured_staging_survives_later_growth(loop, oracle, gpu):
+    """a captured graph keeps the address of each virtual rank's staging buffer. A
+    later eager allreduce with a larger bucket must not free it (the engine retires it instead):
+    replaying the graph afterwards still equals MPICH's order bit for bit."""
+    lib = loop
+    P, n_small, n_big = 6, 70_001, 4_000_003
+    s = torch.cuda.Stream()
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=64 << 10):
+        ins = [torch.zeros(n_small, device=gpu) for _ in range(P)]
+        outs = [torch.empty_like(t) for t in ins]
+        with torch.cuda.stream(s):
+            assert _loop_allreduce(lib, ins, outs, n_small, DT_FLOAT, s.cuda_stream) == 0, lib.ddl_last_error()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            assert _loop_allreduce(lib, ins, outs, n_small, DT_FLOAT, s.cuda_stream) == 0, lib.ddl_last_error()
+        big_in = [torch.randn(n_big, device=gpu) for _ in range(P)]
+        big_out = [torch.empty_like(t) for t in big_in]
+        with torch.cuda.stream(s):  # grows every rank's staging
+            assert _loop_allreduce(lib, big_in, big_out, n_big, DT_FLOAT, s.cuda_stream) == 0, lib.ddl_last_error()
+        torch.cuda.synchronize()
+        # memory freed by a growth would be handed out again: fill fresh allocations with garbage
+        junk = [torch.full((n_big,), float('nan'), device=gpu) for _ in range(P)]
+        torch.cuda.synchronize()
+        for rep in range(2):
+            xs = [random_input(DT_FLOAT, n_small, 101 + 31 * rep + 7919 * r) for r in range(P)]
+            for r in range(P):
+                ins[r].copy_(_t(xs[r], gpu))
+            g.replay()
+            torch.cuda.synchronize()
+            want = oracle.fold_ref_order(DT_FLOAT, xs).tobytes()
+            for r in range(P):
+                assert outs[r].cpu().numpy().tobytes() == want, (rep, r)
+        del g, junk

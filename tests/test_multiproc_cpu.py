@@ -387,3 +387,68 @@ def test_token_rings_per_communicator_concurrent():
                 rounds, err = res[r]
                 assert rounds is not None and not err, f'rank {r}: {err}'
                 assert rounds[name][rd] == want, f'ring {name} rank {r} round {rd}'
+
+
+def _config_worker(rank, world, port, bad, eps_q, go_q, out_q):
+    """One rank of the shared-config agreement: rank `bad` runs with a different slice_bytes. Both
+    the direct path's agreement (ddl_testing_agree_config: the exchange and comparison the engine
+    makes at a communicator's first collective, over gloo host copies) and a keyed negotiation
+    round over the token star (its tokens carry each rank's config hash) must return
+    DDL_STATUS_CONFIG_MISMATCH on EVERY rank; once the rank restores the value both succeed."""
+    try:
+        _setup_paths()
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'tools'))
+        import gloo_transport
+        from ddl.torch.cpp_backend import CPPBackend
+        lib = CPPBackend.c_api()
+        lib.ddl_testing_agree_config.argtypes = [ctypes.c_int, ctypes.c_int, gloo_transport.GROUP_FN, ctypes.c_void_p]
+        dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+        group_fn, _ = gloo_transport.make_callbacks(dist, torch, rank, world)
+        old = lib.ddl_get_config(b'slice_bytes')
+        if rank == bad:
+            assert lib.ddl_set_config(b'slice_bytes', old // 2) == 0
+        ep = ctypes.create_string_buffer(256)
+        assert lib.ddl_control_listen(ep, 256) == 0, lib.ddl_last_error()
+        eps_q.put((rank, ep.value.decode()))
+        assert lib.ddl_control_connect_ranked(rank, world, go_q.get(timeout=60).encode()) == 0, lib.ddl_last_error()
+        out = ctypes.create_string_buffer(1 << 12)
+        res = {'agree_bad': lib.ddl_testing_agree_config(rank, world, group_fn, None),
+               'agree_bad_msg': lib.ddl_last_error().decode(),
+               'negotiate_bad': lib.ddl_control_negotiate(b'grad_a\ngrad_b', out, len(out))}
+        if rank == bad:
+            assert lib.ddl_set_config(b'slice_bytes', old) == 0
+        res['agree_ok'] = lib.ddl_testing_agree_config(rank, world, group_fn, None)
+        res['negotiate_ok'] = lib.ddl_control_negotiate(b'grad_a\ngrad_b', out, len(out))
+        res['agreed'] = out.value.decode()
+        dist.destroy_process_group()
+        out_q.put((rank, res, ''))
+    except Exception as e:  # noqa: BLE001
+        out_q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize('bad', [0, 2])
+def test_config_mismatch_returns_status_on_every_rank(bad):
+    """with one rank on a different slice_bytes, P = 3 processes get
+    DDL_STATUS_CONFIG_MISMATCH (8) on every rank within a bounded time instead of hanging — from
+    the direct path's agreement and from a keyed round; after the rank restores it, both pass."""
+    world = 3
+    ctx = mp.get_context('spawn')
+    eps_q, out_q = ctx.Queue(), ctx.Queue()
+    go = [ctx.Queue() for _ in range(world)]
+    port = _free_port()
+    procs = [ctx.Process(target=_config_worker, args=(r, world, port, bad, eps_q, go[r], out_q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    eps = dict(eps_q.get(timeout=60) for _ in range(world))
+    for q in go:
+        q.put(';'.join(eps[r] for r in range(world)))
+    res = dict((r, (out, err)) for r, out, err in (out_q.get(timeout=60) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(world):
+        out, err = res[r]
+        assert out is not None, f'rank {r}: {err}'
+        assert out['agree_bad'] == 8 and out['negotiate_bad'] == 8, (r, out)
+        assert 'slice_bytes' in out['agree_bad_msg'] and f'{bad}' in out['agree_bad_msg'], out['agree_bad_msg']
+        assert out['agree_ok'] == 0 and out['negotiate_ok'] == 0, (r, out)
+        assert out['agreed'] == 'grad_a\ngrad_b\n', (r, out)

@@ -1,5 +1,5 @@
 """Host-side half of the engine's test-harness transport (ddl_init_test_transport,
-include/ddl_amd.h): the point-to-point groups of every tick move through torch.distributed gloo
+include/ddl_amd_testing.h): the point-to-point groups of every tick move through torch.distributed gloo
 on host copies, so several processes can run the whole N>1 engine on one GPU (RCCL refuses two
 ranks on one device). Used by tests/_mp_gpu_worker.py and by `bench.py --rehearse` (a
 rehearsal of the N>1 bench legs, not a measurement). Never part of the product path."""
@@ -67,7 +67,9 @@ def make_callbacks(dist, torch, rank, world):
 def init_world(lib, dist, torch, rank, world, device=0):
     """ddl_init_test_transport + the token ring, as ddl.torch.communicator.init() does with RCCL.
     Returns the callbacks, which must stay alive as long as the engine."""
+    import os
     from ddl.torch.cpp_backend import check
+    os.environ['DDL_ALLOW_TEST_TRANSPORT'] = '1'  # the engine refuses the test transport otherwise
     lib.ddl_init_test_transport.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, GROUP_FN, MAX_FN,
                                             ctypes.c_void_p]
     lib.ddl_init_test_transport.restype = ctypes.c_int

@@ -6,6 +6,8 @@
   fold    — one N-input fold kernel launch (single stream)
   ring2   — local world P = 2, ring schedule (two-input reduce kernels, no fold)
   rawlocal— `local` captured with hipStreamBeginCapture through ctypes (no torch graph)
+    python graph_probe.py <mode> [algo] [forked: 1 = config capture_forked, the program on its
+    forked comm / compute streams inside the capture; 0 = posted serially]
 Prints one line per stage; a crash names the last stage reached."""
 import ctypes
 import os
@@ -22,10 +24,11 @@ def say(*a):
     print(*a, flush=True)
 
 
-def main(mode, P=3, n=300, algo=1):
+def main(mode, P=3, n=300, algo=1, forked=0):
     lib = CPPBackend.c_api()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
+    lib.ddl_set_config(b'capture_forked', forked)
     lib.ddl_set_config(b'tune', 0)
     lib.ddl_set_config(b'algo', algo)
     lib.ddl_set_config(b'slice_bytes', 64 << 10)
@@ -78,8 +81,24 @@ def main(mode, P=3, n=300, algo=1):
         assert lib.ddl_rccl_loopback_finalize() == 0
 
 
+def hip_runtime():
+    """The HIP runtime torch and the engine already share, matched by soname with RTLD_NOLOAD.
+    (r02's probe loaded 'libamdhip64.so' by file name: /opt/rocm's copy, a SECOND runtime beside
+    torch's bundled one, handed torch's stream to it — the `rawlocal` segfault.)"""
+    vp, ci = ctypes.c_void_p, ctypes.c_int
+    hip = ctypes.CDLL('libamdhip64.so.7', mode=os.RTLD_NOLOAD | os.RTLD_NOW)
+    for name, res, args in (('hipStreamBeginCapture', ci, [vp, ci]),
+                            ('hipStreamEndCapture', ci, [vp, ctypes.POINTER(vp)]),
+                            ('hipGraphGetNodes', ci, [vp, vp, ctypes.POINTER(ctypes.c_size_t)]),
+                            ('hipGraphInstantiate', ci, [ctypes.POINTER(vp), vp, vp, vp, ctypes.c_size_t]),
+                            ('hipGraphLaunch', ci, [vp, vp])):
+        f = getattr(hip, name)
+        f.restype, f.argtypes = res, args
+    return hip
+
+
 def raw_capture(lib, s, P, send, recv, n, outs):
-    hip = ctypes.CDLL('libamdhip64.so')
+    hip = hip_runtime()
     vp = ctypes.c_void_p
     st = ctypes.c_void_p(s.cuda_stream)
     assert lib.ddl_local_ring_allreduce(P, send, recv, n, 1, 0, s.cuda_stream) == 0
@@ -109,6 +128,7 @@ def raw_capture(lib, s, P, send, recv, n, outs):
 if __name__ == '__main__':
     m = sys.argv[1]
     algo = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    forked = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     if m == 'group':  # the one-shot schedule: one group of self pairs, one fold
         algo = 2
-    main(m, algo=algo)
+    main(m, algo=algo, forked=forked)

@@ -12,7 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "ddl_amd.h"
+#include "ddl_amd_testing.h"
 
 #define CK(x)                                                                                         \
     do {                                                                                              \
