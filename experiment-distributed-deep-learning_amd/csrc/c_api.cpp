@@ -149,6 +149,17 @@ void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len)
 
 // The submitter's input-ready event: device requests are ordered after hip_stream's current
 // position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
+ThreadWorld &thread_world(int nranks) {
+    static std::mutex mu;
+    static auto *worlds = new std::map<std::pair<int, int>, std::unique_ptr<ThreadWorld>>();
+    int dev = current_device();
+    std::lock_guard<std::mutex> g(mu);
+    auto key = std::make_pair(nranks, dev);
+    auto it = worlds->find(key);
+    if (it == worlds->end()) it = worlds->emplace(key, std::unique_ptr<ThreadWorld>(new ThreadWorld(nranks, dev))).first;
+    return *it->second;
+}
+
 std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
     DDL_REQUIRE(memory == DDL_MEMORY_DEVICE || memory == DDL_MEMORY_HOST, DDL_STATUS_INVALID_ARGUMENT,
                 "memory must be DDL_MEMORY_DEVICE (0) or DDL_MEMORY_HOST (1), not " << memory);
@@ -779,6 +790,37 @@ int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recv
         (void)current_device();
         local_world(nranks).allgatherv(sends, recvs, counts, displs, dtype, as_stream(hip_stream));
     });
+}
+
+// ---- thread world: the production RingExecutor per rank, asynchronous transport --------------------
+int ddl_testing_thread_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements, int dtype,
+                                 void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && sends && recvs, DDL_STATUS_INVALID_ARGUMENT, "bad thread allreduce");
+        thread_world(nranks).allreduce(sends, recvs, elements, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_testing_thread_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
+                                 void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && root >= 0 && root < nranks && bufs, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad thread broadcast");
+        thread_world(nranks).broadcast(bufs, elements, dtype, root, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                                  const size_t *displs, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && sends && recvs && counts && displs, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad thread allgatherv");
+        thread_world(nranks).allgatherv(sends, recvs, counts, displs, dtype, as_stream(hip_stream));
+    });
+}
+
+int ddl_testing_drop_wait(int tick) {
+    return guarded([&] { set_testing_drop_wait(tick); });
 }
 
 // ---- RCCL loopback (one GPU, real RCCL transport) --------------------------------------------

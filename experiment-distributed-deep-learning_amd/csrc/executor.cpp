@@ -2,8 +2,26 @@
 #include "executor.h"
 
 #include <map>
+#include <thread>
 
 namespace ddl {
+
+// Step-by-step trace of the program posting (log_level >= 4): every HIP call of run_, flushed
+// before the call, so a crash inside the runtime names the call it was in.
+#define DDL_TRACE(msg)                                                                          \
+    do {                                                                                        \
+        if (::ddl::log_level() >= 4) {                                                          \
+            std::ostringstream _os;                                                             \
+            _os << msg;                                                                         \
+            std::fprintf(stderr, "[ddl trace] %s\n", _os.str().c_str());                         \
+            std::fflush(stderr);                                                                \
+        }                                                                                       \
+    } while (0)
+
+namespace {
+std::atomic<int> g_drop_wait_tick{-1};
+}
+void set_testing_drop_wait(int tick) { g_drop_wait_tick = tick; }
 
 bool stream_capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -244,10 +262,15 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
         DDL_HIP(hipEventRecord(res_.fork_ev, user));
         DDL_HIP(hipStreamWaitEvent(comm, res_.fork_ev, 0));
         DDL_HIP(hipStreamWaitEvent(compute, res_.fork_ev, 0));
+        if (capturing) {  // no event recorded on a forked stream before its first node (common.h)
+            launch_capture_anchor(comm);
+            launch_capture_anchor(compute);
+        }
     }
+    const int drop = g_drop_wait_tick.load();
     for (size_t t = 0; t < prog_.ticks.size(); ++t) {
         const Tick &tk = prog_.ticks[t];
-        if (tk.wait_reduce >= 0 && !serial) {
+        if (tk.wait_reduce >= 0 && !serial && (int)t != drop) {
             int w = last_reduce_at_or_before(prog_, tk.wait_reduce);
             if (w >= 0) DDL_HIP(hipStreamWaitEvent(comm, res_.red_ev[w], 0));
         }
@@ -291,6 +314,173 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     DDL_HIP(hipEventRecord(res_.join_cp_ev, compute));
     DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
     DDL_HIP(hipStreamWaitEvent(user, res_.join_cp_ev, 0));
+}
+
+ThreadFabric::~ThreadFabric() {
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+}
+
+hipEvent_t ThreadFabric::event_() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (next_event_ < events_.size()) return events_[next_event_++];
+    }
+    hipEvent_t e;
+    DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    std::lock_guard<std::mutex> g(mu_);
+    events_.push_back(e);
+    next_event_ = events_.size();
+    return e;
+}
+
+void ThreadFabric::recycle() {
+    std::lock_guard<std::mutex> g(mu_);
+    next_event_ = 0;
+}
+
+void ThreadFabric::abort() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        aborted_ = true;
+    }
+    cv_.notify_all();
+}
+
+void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t stream) {
+    if (ops.empty()) return;
+    // 1) post every send: the send buffers are ready at this point of `stream`
+    hipEvent_t ready = event_();
+    DDL_HIP(hipEventRecord(ready, stream));
+    std::vector<std::shared_ptr<Send>> mine;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (const P2POp &op : ops) {
+            if (!op.send) continue;
+            DDL_REQUIRE(op.peer >= 0 && op.peer < P_ && op.peer != rank, DDL_STATUS_ERROR_UNKNOWN, "bad peer " << op.peer);
+            auto sd = std::make_shared<Send>(Send{op.ptr, op.bytes, op.tag, ready});
+            q_[(size_t)rank * P_ + op.peer].push_back(sd);
+            mine.push_back(sd);
+        }
+    }
+    cv_.notify_all();
+    // 2) receives in posting order: the peer's matching send once it is POSTED (enqueue only)
+    for (const P2POp &op : ops) {
+        if (op.send) continue;
+        std::shared_ptr<Send> sd;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            auto &qq = q_[(size_t)op.peer * P_ + rank];
+            cv_.wait(g, [&] { return aborted_ || !qq.empty(); });
+            DDL_REQUIRE(!aborted_, DDL_STATUS_COMM_ERROR, "thread fabric aborted");
+            sd = qq.front();
+            qq.pop_front();
+        }
+        DDL_REQUIRE(sd->bytes == op.bytes && sd->tag == op.tag, DDL_STATUS_ERROR_UNKNOWN,
+                    "thread fabric: rank " << rank << " receives " << op.bytes << " B (tag " << op.tag << ") from "
+                                           << op.peer << ", whose matching send is " << sd->bytes << " B (tag "
+                                           << sd->tag << ")");
+        DDL_HIP(hipStreamWaitEvent(stream, sd->ready, 0));
+        if (op.bytes) DDL_HIP(hipMemcpyAsync(op.ptr, sd->ptr, op.bytes, hipMemcpyDeviceToDevice, stream));
+        hipEvent_t copied = event_();
+        DDL_HIP(hipEventRecord(copied, stream));
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            sd->copied = copied;
+        }
+        cv_.notify_all();
+    }
+    // 3) the group completes for a sender once every receiver's copy has run (device order):
+    //    the host waits only for the receivers to have ENQUEUED their copies
+    for (const auto &sd : mine) {
+        hipEvent_t copied;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] { return aborted_ || sd->copied != nullptr; });
+            DDL_REQUIRE(!aborted_, DDL_STATUS_COMM_ERROR, "thread fabric aborted");
+            copied = sd->copied;
+        }
+        DDL_HIP(hipStreamWaitEvent(stream, copied, 0));
+    }
+}
+
+void ThreadTransport::allgather(const GatherOp &g, hipStream_t stream) {
+    const int P = fab_->size();
+    char *recv = static_cast<char *>(g.recv);
+    if (recv + (size_t)rank_ * g.bytes != g.send)
+        DDL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * g.bytes, g.send, g.bytes, hipMemcpyDeviceToDevice, stream));
+    std::vector<P2POp> ops;
+    for (int d = 1; d < P; ++d) {
+        const int to = (rank_ + d) % P, from = (rank_ + P - d) % P;
+        ops.push_back(P2POp{true, to, 0, const_cast<void *>(g.send), g.bytes});
+        ops.push_back(P2POp{false, from, 0, recv + (size_t)from * g.bytes, g.bytes});
+    }
+    group(ops, stream);
+}
+
+ThreadWorld::ThreadWorld(int nranks, int device) : P_(nranks), device_(device) {
+    fab_ = std::make_shared<ThreadFabric>(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        ex_.emplace_back(new RingExecutor(r, nranks, device, std::unique_ptr<Transport>(new ThreadTransport(fab_, r))));
+        hipStream_t s;
+        DDL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        streams_.push_back(s);
+        hipEvent_t e;
+        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        done_.push_back(e);
+    }
+    DDL_HIP(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+}
+
+ThreadWorld::~ThreadWorld() {
+    (void)hipDeviceSynchronize();
+    ex_.clear();
+    for (hipStream_t s : streams_) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : done_) (void)hipEventDestroy(e);
+    if (fork_) (void)hipEventDestroy(fork_);
+}
+
+void ThreadWorld::run_(hipStream_t user, const std::function<void(int, hipStream_t)> &body) {
+    DDL_HIP(hipEventRecord(fork_, user));
+    for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(streams_[r], fork_, 0));
+    std::vector<std::thread> th;
+    std::vector<Error> errs;
+    std::mutex emu;
+    for (int r = 0; r < P_; ++r)
+        th.emplace_back([&, r] {
+            try {
+                DDL_HIP(hipSetDevice(device_));
+                body(r, streams_[r]);
+                DDL_HIP(hipEventRecord(done_[r], streams_[r]));
+            } catch (const Error &e) {
+                std::lock_guard<std::mutex> g(emu);
+                errs.push_back(e);
+                fab_->abort();
+            }
+        });
+    for (auto &t : th) t.join();
+    if (!errs.empty()) {
+        (void)hipDeviceSynchronize();
+        fab_ = std::make_shared<ThreadFabric>(P_);  // a fresh fabric: the aborted one has stale posts
+        for (int r = 0; r < P_; ++r)
+            ex_[r].reset(new RingExecutor(r, P_, device_, std::unique_ptr<Transport>(new ThreadTransport(fab_, r))));
+        throw errs.front();
+    }
+    for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(user, done_[r], 0));
+    fab_->recycle();
+}
+
+void ThreadWorld::allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
+                            const RingConfig &cfg) {
+    run_(user, [&](int r, hipStream_t s) { ex_[r]->allreduce(in[r], out[r], n, dtype, s, cfg); });
+}
+
+void ThreadWorld::broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg) {
+    run_(user, [&](int r, hipStream_t s) { ex_[r]->broadcast(bufs[r], n, dtype, root, s, cfg); });
+}
+
+void ThreadWorld::allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
+                             int dtype, hipStream_t user) {
+    run_(user, [&](int r, hipStream_t s) { ex_[r]->allgatherv(sends[r], recvs[r], counts, displs, dtype, s); });
 }
 
 LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks) {
@@ -371,16 +561,29 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
     auto compute = [&](int r) { return serial ? user : res_[r]->compute; };
     auto loop_stream = [&] { return serial ? user : loop_stream_; };
     auto record = [&](hipEvent_t e, hipStream_t st) {
+        DDL_TRACE("record ev " << (void *)e << " on " << (void *)st);
         if (!serial) DDL_HIP(hipEventRecord(e, st));
     };
     auto wait = [&](hipStream_t st, hipEvent_t e) {
+        DDL_TRACE("wait " << (void *)st << " on ev " << (void *)e);
         if (!serial) DDL_HIP(hipStreamWaitEvent(st, e, 0));
     };
+    DDL_TRACE("local world run: P " << P_ << " ticks " << T << " serial " << serial << " user " << (void *)user);
     hipEvent_t fork = res_[0]->fork_ev;
     record(fork, user);
     for (int r = 0; r < P_; ++r) {
         wait(comm(r), fork);
         wait(compute(r), fork);
+    }
+    if (!serial && stream_capturing(user)) {  // no event recorded on a forked stream before its first node
+        for (int r = 0; r < P_; ++r) {
+            launch_capture_anchor(comm(r));
+            launch_capture_anchor(compute(r));
+        }
+        if (loop_) {
+            wait(loop_stream(), fork);
+            launch_capture_anchor(loop_stream());
+        }
     }
     for (size_t t = 0; t < T; ++t) {
         // 1) each rank's comm stream reaches the tick (after its reduce dependency)
@@ -391,8 +594,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 int w = last_reduce_at_or_before(progs_[r], tk.wait_reduce);
                 if (w >= 0) wait(comm(r), rr.red_ev[w]);
             }
-            for (const CopyOp &c : tk.copies)
+            for (const CopyOp &c : tk.copies) {
+                DDL_TRACE("copy " << c.bytes << " B on " << (void *)comm(r));
                 DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, comm(r)));
+            }
             record(rr.pre_ev[t], comm(r));
         }
         // 1b) allgather ticks: rank q's block into every rank's recv at q * bytes, once q has
@@ -460,6 +665,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                     if (op.send) continue;
                     const P2POp &match = match_(r, t, op, seen);
                     wait(comm(r), res_[op.peer]->pre_ev[t]);
+                    DDL_TRACE("recv copy " << op.bytes << " B on " << (void *)comm(r));
                     DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, comm(r)));
                 }
                 record(rr.post_ev[t], comm(r));
@@ -477,6 +683,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             if (!tk.has_reduce) continue;
             record(rr.comm_ev[t], comm(r));
             wait(compute(r), rr.comm_ev[t]);
+            DDL_TRACE("reduce launch on " << (void *)compute(r));
             launch_tick_reduce(tk, dtype, compute(r));
             record(rr.red_ev[t], compute(r));
         }

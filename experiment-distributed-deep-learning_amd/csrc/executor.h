@@ -9,6 +9,9 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -88,6 +91,63 @@ private:
     char *pinned_ = nullptr;  // host side of a group's device buffers (pinned: truly async copies)
     size_t pinned_bytes_ = 0;
 };
+
+// In-process thread transport (test / diagnostic, ddl_testing_thread_*): P threads, each driving
+// its own RingExecutor — the production executor, asynchronously — exchange through device
+// copies with RCCL's contract: group() only rendezvous with the peers on the HOST ENQUEUE (a
+// receive waits until the matching send is posted, never until it has run), the k-th send from q
+// to r matches r's k-th receive from q (per-pair FIFO, as RCCL), a receive is a
+// hipStreamWaitEvent on the sender's "ready" event (recorded where the send was posted) plus a
+// D2D copy, and the sender's stream waits for the receiver's "copied" event before anything
+// after the group may overwrite the send buffer. No hipStreamSynchronize anywhere: a missing
+// event wait inside the executor shows up as wrong data, which the host-synchronising test
+// transport (CallbackTransport) would hide.
+class ThreadFabric {
+public:
+    explicit ThreadFabric(int P) : P_(P), q_((size_t)P * P) {}
+    ~ThreadFabric();
+    ThreadFabric(const ThreadFabric &) = delete;
+    ThreadFabric &operator=(const ThreadFabric &) = delete;
+    struct Send {
+        const void *ptr;
+        size_t bytes;
+        int tag;
+        hipEvent_t ready;
+        hipEvent_t copied = nullptr;  // set by the receiver once its copy is enqueued
+    };
+    int size() const { return P_; }
+    void group(int rank, const std::vector<P2POp> &ops, hipStream_t stream);
+    void abort();  // wakes every waiter with an error (a rank failed)
+    // Between calls (every rank's host enqueue done, so every wait on them has been issued): the
+    // events handed out become reusable.
+    void recycle();
+
+private:
+    hipEvent_t event_();  // an event no pending host wait refers to
+    int P_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<std::deque<std::shared_ptr<Send>>> q_;  // q_[from * P + to]: posted, not yet received
+    std::vector<hipEvent_t> events_;
+    size_t next_event_ = 0;
+    bool aborted_ = false;
+};
+
+class ThreadTransport : public Transport {
+public:
+    ThreadTransport(std::shared_ptr<ThreadFabric> fab, int rank) : fab_(std::move(fab)), rank_(rank) {}
+    void group(const std::vector<P2POp> &ops, hipStream_t stream) override { fab_->group(rank_, ops, stream); }
+    void allgather(const GatherOp &g, hipStream_t stream) override;
+    bool capturable() const override { return false; }
+
+private:
+    std::shared_ptr<ThreadFabric> fab_;
+    int rank_;
+};
+
+// Mutation knob for the executor's ordering tests (ddl_testing_drop_wait): RingExecutor::run_
+// skips the wait_reduce wait of this tick (-1: none).
+void set_testing_drop_wait(int tick);
 
 // Streams, events and staging memory of one rank (reused across calls).
 class RankResources {
@@ -188,6 +248,28 @@ private:
     std::vector<hipEvent_t> loop_ev_;
     hipEvent_t loop_join_ = nullptr;
     long long loop_pairs_ = 0;
+};
+
+// P RingExecutors over one ThreadFabric, each driven by its own thread per call; every rank works
+// on its own stream forked from / joined to the caller's (test / diagnostic path).
+class ThreadWorld {
+public:
+    ThreadWorld(int nranks, int device);
+    ~ThreadWorld();
+    void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
+                   const RingConfig &cfg);
+    void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
+    void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
+                    int dtype, hipStream_t user);
+
+private:
+    void run_(hipStream_t user, const std::function<void(int, hipStream_t)> &body);
+    int P_, device_;
+    std::shared_ptr<ThreadFabric> fab_;
+    std::vector<std::unique_ptr<RingExecutor>> ex_;
+    std::vector<hipStream_t> streams_;
+    std::vector<hipEvent_t> done_;
+    hipEvent_t fork_ = nullptr;
 };
 
 // Most recent tick <= w that launched a reduce (-1 if none).

@@ -497,8 +497,10 @@ Agreed negotiate_member(ControlChannel &ch, const Token &sync,
     Token s;
     s.type = sync.type;
     s.request = sync.request;
-    s.cfg = config().shared_hash();
     s.msg = cached ? ch.cache.encode(by_index(ch.cache.decode(sync.msg))) : encode_keys(by_string(decode_keys(sync.msg)));
+    // the config this rank runs the round under: read once its first proposed request is registered
+    // (by_string / by_index wait for it), not when the proposal arrives
+    s.cfg = config().shared_hash();
     s.seq = snapshot ? snapshot() : -1;
     ch.send(s);  // this rank's intersection with the proposal
     Token c;

@@ -440,6 +440,14 @@ int g_cu_count = 0;
 
 }  // namespace
 
+// An empty node (one wavefront, no memory access) for graph captures: see launch_capture_anchor.
+__global__ void k_capture_anchor() {}
+
+void launch_capture_anchor(hipStream_t stream) {
+    hipLaunchKernelGGL(k_capture_anchor, dim3(1), dim3(64), 0, stream);
+    DDL_HIP(hipGetLastError());
+}
+
 int device_cu_count() {
     if (g_cu_count == 0) {
         int dev = 0, cus = 0;

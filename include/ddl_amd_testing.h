@@ -123,6 +123,23 @@ int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements
 int ddl_local_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
                          const size_t *displs, int dtype, void *hip_stream);
 
+/* ---- thread world: the production executor, asynchronously --------------------------------
+ * P threads, each driving its own RingExecutor (the class ddl_allreduce runs at N > 1) over an
+ * in-process transport with RCCL's asynchronous contract: a group rendezvous with its peers only
+ * on the host ENQUEUE; a receive is a stream wait on the sender's event plus a D2D copy; the
+ * sender's stream waits for the receiver's copy event; nothing synchronises the host. Every
+ * rank works on its own stream forked from / joined to hip_stream. sends[r] / recvs[r] / bufs[r]
+ * are rank r's buffers; the schedule is the configured one (ddl_set_config "algo", ...). */
+int ddl_testing_thread_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements, int dtype,
+                                 void *hip_stream);
+int ddl_testing_thread_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
+                                 void *hip_stream);
+int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
+                                  const size_t *displs, int dtype, void *hip_stream);
+/* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
+ * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
+int ddl_testing_drop_wait(int tick);
+
 /* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
  * A one-rank RCCL communicator (ncclGetUniqueId + ncclCommInitRank, the calls ddl_init makes at
  * size > 1) carries the matched send/recv pairs of P virtual ranks' programs as self-send /

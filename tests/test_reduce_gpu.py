@@ -217,3 +217,43 @@ def test_reduce_fold_ordered_rejects_bad_order(lib, gpu):
     P = ctypes.c_void_p * 1
     assert lib.ddl_reduce_fold_ordered(x.data_ptr(), x.data_ptr(), P(x.data_ptr()), 1, 16, 1, 3,
                                        torch.cuda.current_stream().cuda_stream) == 3
+
+
+# C2's headline sizes: the bench's 256 MiB and 1 GiB launches, at full
+# size, in every cache-policy band default_variant picks (reduce_kernels.hip: below 32 MiB plain
+# loads + write-through stores, 32-256 MiB non-temporal loads + write-through stores, from 256 MiB
+# all non-temporal). Integer-valued fp32 in (-2^22, 2^22): every sum is exact in fp32, so the WHOLE
+# output is checked against the exact sum; then random data against the oracle's MPI_SUM on a
+# strided sample of the same launch.
+C2_SIZES = [(16 << 20) // 4 + 7, (64 << 20) // 4 + 5, (256 << 20) // 4, (1 << 30) // 4 + 13]
+
+
+@pytest.mark.parametrize('in_place', [True, False], ids=['local', 'sum2'])
+@pytest.mark.parametrize('n', C2_SIZES, ids=lambda n: f'{n * 4 >> 20}MiB+{n % 1024}')
+def test_c2_headline_sizes_exact(lib, oracle, gpu, n, in_place):
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=gpu).manual_seed(n)
+    a = torch.randint(-(1 << 22), 1 << 22, (n,), device=gpu, generator=g, dtype=torch.int32).float()
+    b = torch.randint(-(1 << 22), 1 << 22, (n,), device=gpu, generator=g, dtype=torch.int32).float()
+    want = a + b  # exact: |a + b| < 2^23
+    if in_place:
+        assert lib.ddl_reduce_local(a.data_ptr(), b.data_ptr(), n, DT_FLOAT, s) == 0, lib.ddl_last_error()
+        out = a
+    else:
+        out = torch.full_like(a, float('nan'))
+        assert lib.ddl_reduce_sum2(out.data_ptr(), a.data_ptr(), b.data_ptr(), n, DT_FLOAT, s) == 0
+    torch.cuda.synchronize()
+    bad = torch.nonzero(out.view(torch.int32) != want.view(torch.int32))
+    assert bad.numel() == 0, f'{bad.numel()} elements differ, first at {bad[:4].flatten().tolist()}'
+    del a, b, out, want
+    # random data: the oracle on a strided sample plus the tail
+    x = torch.randn(n, device=gpu, generator=g)
+    y = torch.randn(n, device=gpu, generator=g)
+    z = torch.empty_like(x)
+    assert lib.ddl_reduce_sum2(z.data_ptr(), x.data_ptr(), y.data_ptr(), n, DT_FLOAT, s) == 0
+    torch.cuda.synchronize()
+    idx = torch.cat([torch.arange(0, n, 4099, device=gpu), torch.arange(max(0, n - 4096), n, device=gpu)])
+    xs, ys, zs = (t[idx].cpu().numpy() for t in (x, y, z))
+    assert zs.tobytes() == oracle.sum2(DT_FLOAT, xs, ys).tobytes()
+    del x, y, z
+    torch.cuda.empty_cache()

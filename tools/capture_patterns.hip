@@ -10,6 +10,12 @@
 //   8 a side stream with work joined only indirectly (through another side stream)
 //   9 the engine's P = 2 ring program as LocalWorld posts it: per rank a comm and a compute
 //     stream, per tick pre / post / comm / reduce events, 1200-byte copies (argv[2] = ticks)
+//  10 s1 records e1 after a kernel; s2 (with a node) waits e1; s1 captures nothing after e1
+//  11 RingExecutor's direct shape, K = argv[2] slices: comm: group k (a kernel), record ce[k];
+//     compute waits ce[k], fold k, record re[k]; then comm waits re[k] and allgather k — so comm
+//     waits re[0] AFTER compute captured fold 1 .. K-1 behind it
+//  12 s1 records e1 after a kernel, then captures another kernel; s2 (with a node) waits e1
+//  13 as 12, but s2 has no node of its own when it waits e1
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -135,6 +141,44 @@ int main(int argc, char **argv) {
                 CK(hipStreamWaitEvent(o, join[r], 0));
             }
             CK(hipMemcpyAsync(c, b, 4, hipMemcpyDeviceToDevice, o));
+            break;
+        }
+        case 10:
+        case 12:
+        case 13:
+            hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s1, a, n);
+            CK(hipEventRecord(e1, s1));
+            if (k != 10) hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s1, a, n);
+            if (k != 13) hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s2, b, n);
+            CK(hipStreamWaitEvent(s2, e1, 0));
+            CK(hipMemcpyAsync(c, a, 4, hipMemcpyDeviceToDevice, s2));
+            CK(hipEventRecord(j1, s1));
+            CK(hipEventRecord(j2, s2));
+            CK(hipStreamWaitEvent(o, j1, 0));
+            CK(hipStreamWaitEvent(o, j2, 0));
+            break;
+        case 11: {  // s1 = comm, s2 = compute
+            const int K = argc > 2 ? std::atoi(argv[2]) : 3;
+            hipEvent_t ce[16], re[16];
+            for (int i = 0; i < K; ++i) {
+                CK(hipEventCreateWithFlags(&ce[i], hipEventDisableTiming));
+                CK(hipEventCreateWithFlags(&re[i], hipEventDisableTiming));
+            }
+            for (int i = 0; i < K; ++i) {
+                hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s1, a, n);  // RS group i
+                CK(hipEventRecord(ce[i], s1));
+                CK(hipStreamWaitEvent(s2, ce[i], 0));
+                hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s2, b, n);  // fold i
+                CK(hipEventRecord(re[i], s2));
+            }
+            for (int i = 0; i < K; ++i) {
+                CK(hipStreamWaitEvent(s1, re[i], 0));
+                hipLaunchKernelGGL(inc, dim3(n / 256), dim3(256), 0, s1, c, n);  // AG group i
+            }
+            CK(hipEventRecord(j1, s1));
+            CK(hipEventRecord(j2, s2));
+            CK(hipStreamWaitEvent(o, j1, 0));
+            CK(hipStreamWaitEvent(o, j2, 0));
             break;
         }
         case 5:

@@ -88,6 +88,28 @@ __global__ void __launch_bounds__(T) k_fold_serial(f4 *o, Ins in, size_t nv) {
     else o[i] = s;
 }
 
+// Buffer form (the two-input reduce's mapping): one descriptor per input tile, 32-bit lane
+// offsets, the cache bits in each access's aux word. AUXL: loads' aux (2 = nt), AUXS: store's
+// aux (2 = nt, 17 = sc0 sc1 write-through, 0 plain).
+template <int T, int AUXL, int AUXS>
+__global__ void __launch_bounds__(T) k_fold_buf(f4 *o, Ins in, size_t nv) {
+    const size_t base = (size_t)blockIdx.x * T;
+    if (base >= nv) return;
+    const int bytes = (int)((nv - base < (size_t)T ? nv - base : (size_t)T) * 16);
+    const int off = (int)threadIdx.x * 16;
+    u4 r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4 *>(in.x[k] + base), 0, bytes, 0x00020000);
+        r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL);
+    }
+    f4 s = __builtin_bit_cast(f4, r[0]);
+#pragma unroll
+    for (int k = 1; k < K; ++k) s += __builtin_bit_cast(f4, r[k]);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(o + base, 0, bytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, s), ro, off, 0, AUXS);
+}
+
 struct Variant {
     std::string name;
     std::function<void(f4 *, Ins, size_t, hipStream_t)> run;
@@ -111,10 +133,15 @@ int main(int argc, char **argv) {
     const size_t bytes = mib << 20, nv = bytes / 16;
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    // argv[3]: skew in bytes between the inputs' bases (input k starts k * skew bytes into its
+    // allocation): tests whether 8 streams at the same offsets alias the same HBM channels
+    const size_t skew = argc > 3 ? std::atol(argv[3]) : 0;
     std::vector<f4 *> bufs((K + 1) * sets);
-    for (auto &b : bufs) {
-        CK(hipMalloc(&b, bytes));
-        CK(hipMemset(b, 0, bytes));
+    for (size_t j = 0; j < bufs.size(); ++j) {
+        char *b;
+        CK(hipMalloc(&b, bytes + K * skew));
+        CK(hipMemset(b, 0, bytes + K * skew));
+        bufs[j] = reinterpret_cast<f4 *>(b + (j % (K + 1)) * skew);
     }
     std::vector<Variant> vs = {
         make<128, 1, 3>("(shipped: 128 lanes, 1 vector, all NT)"),
@@ -130,6 +157,18 @@ int main(int argc, char **argv) {
         make<256, 4, 1>("NT loads"),
         make<128, 2, 1>("NT loads"),
         make<128, 1, 5>("NT loads, write-through store"),
+        Variant{"fold_buf T128 nt loads, nt store", [](f4 *o, Ins in, size_t nv, hipStream_t st) {
+                    hipLaunchKernelGGL((k_fold_buf<128, 2, 2>), dim3((unsigned)((nv + 127) / 128)), dim3(128), 0, st, o, in, nv);
+                }},
+        Variant{"fold_buf T128 nt loads, wt store", [](f4 *o, Ins in, size_t nv, hipStream_t st) {
+                    hipLaunchKernelGGL((k_fold_buf<128, 2, 17>), dim3((unsigned)((nv + 127) / 128)), dim3(128), 0, st, o, in, nv);
+                }},
+        Variant{"fold_buf T64 nt loads, nt store", [](f4 *o, Ins in, size_t nv, hipStream_t st) {
+                    hipLaunchKernelGGL((k_fold_buf<64, 2, 2>), dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, st, o, in, nv);
+                }},
+        Variant{"fold_buf T128 plain loads, wt store", [](f4 *o, Ins in, size_t nv, hipStream_t st) {
+                    hipLaunchKernelGGL((k_fold_buf<128, 0, 17>), dim3((unsigned)((nv + 127) / 128)), dim3(128), 0, st, o, in, nv);
+                }},
         make<128, 1, 4>("plain loads, write-through store"),
         Variant{"fold_serial T128 pol3",
                 [](f4 *o, Ins in, size_t nv, hipStream_t st) {
@@ -163,8 +202,8 @@ int main(int argc, char **argv) {
             ms[v].push_back(t / reps);
         }
     }
-    std::printf("# fp32 fold of %d inputs, %zu MiB chunk, %d rounds x %d reps, %d rotating sets; GB/s = (K+1)*chunk / t\n",
-                K, mib, rounds, reps, sets);
+    std::printf("# fp32 fold of %d inputs, %zu MiB chunk, %d rounds x %d reps, %d rotating sets, input skew %zu B; GB/s = (K+1)*chunk / t\n",
+                K, mib, rounds, reps, sets, skew);
     for (size_t v = 0; v < vs.size(); ++v) {
         auto x = ms[v];
         std::sort(x.begin(), x.end());
