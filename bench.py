@@ -309,6 +309,14 @@ def single_gpu(args):
         if not args.no_host:
             out['keyed_host_c5'] = keyed_host_c5(lib, Communicator.world(), steps=3)
             out['keyed_host_c5_pinned'] = keyed_host_c5(lib, Communicator.world(), steps=3, pinned=True)
+            # A/B: the large pinned inputs uploaded by DMA straight from the tensors (host_direct_dma,
+            # off by default) instead of packed by the copy threads into the pinned slots
+            out['keyed_host_c5_pinned_direct_dma'] = keyed_host_c5(
+                lib, Communicator.world(), steps=3, pinned=True, settings={'host_direct_dma': 1})
+            # pageable tensors with the opt-in registration cache: registered on the first batch,
+            # then the pinned paths
+            out['keyed_host_c5_registered'] = keyed_host_c5(
+                lib, Communicator.world(), steps=3, settings={'host_register_cache_bytes': 4 << 30})
     if not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline()
         out['cpu_reduce_op_port'] = cpu_reduce_port(64 << 20, args.cpu_seconds)
@@ -538,7 +546,7 @@ def keyed_c1_latency(lib, comm, dev, reps=200):
             'path': 'keyed submit -> star negotiation -> allreduce in place on the tensor -> done'}
 
 
-def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
+def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
     buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks
     through pinned slots: host pack -> H2D -> allreduce -> D2H -> host unpack; with pinned tensors
@@ -565,9 +573,12 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     ptrs = V(*[t.data_ptr() for t in tensors])
     args = (k, K(*keys), ptrs, ptrs, (ctypes.c_size_t * k)(*[t.numel() for t in tensors]), (ctypes.c_int * k)(*dts),
             0, MEMORY_HOST, None, DONE_FN(), None)
-    old = lib.ddl_get_config(b'one_rank_shortcut')
+    settings = dict(settings or {})
+    settings['one_rank_shortcut'] = 0
+    old = {kk: lib.ddl_get_config(kk.encode()) for kk in settings}
     try:
-        check(lib.ddl_set_config(b'one_rank_shortcut', 0), 'ddl_set_config')
+        for kk, v in settings.items():
+            check(lib.ddl_set_config(kk.encode(), v), 'ddl_set_config')
 
         def step():
             check(lib.ddl_allreduce_submit_batch_mem(comm.id, *args), 'ddl_allreduce_submit_batch_mem')
@@ -580,7 +591,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
         dt = (time.perf_counter() - t0) / steps
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
     finally:
-        lib.ddl_set_config(b'one_rank_shortcut', old)
+        for kk, v in old.items():
+            lib.ddl_set_config(kk.encode(), v)
     path = ('pinned host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
             'allreduce), unpack kernel writes the results straight into the tensors over PCIe, in place' if pinned else
             'pageable host tensors -> keyed batch -> negotiation -> plans -> pinned chunks (host pack, H2D, '
@@ -588,7 +600,10 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False):
     return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3), 'bucket_GiBs': round(total / GiB / dt, 2),
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
-            'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path}
+            'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path,
+            'host_direct_dma': int(lib.ddl_get_config(b'host_direct_dma')) if 'host_direct_dma' not in settings
+            else settings['host_direct_dma'],
+            'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'}}
 
 
 def host_resident_rate(lib, comm, S, reps):

@@ -335,6 +335,14 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
             c.host_copy_threads = value;
         } else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
+        else if (k == "host_direct_dma") c.host_direct_dma = value ? 1 : 0;
+        else if (k == "host_register_cache_bytes") {
+            DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "host_register_cache_bytes must be >= 0");
+            c.host_register_cache_bytes = value;
+            if (value == 0)  // off: every cached registration goes now (before the caller frees memory)
+                for (auto &comm : Registry::get().all())
+                    if (RequestHandler *h = comm->handler_if_created()) h->release_registrations();
+        }
         else if (k == "tune") c.tune = value ? 1 : 0;
         else if (k == "fusion_pipeline_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "fusion_pipeline_bytes must be >= 0");
@@ -363,6 +371,8 @@ long long ddl_get_config(const char *key) {
     if (k == "tune") return c.tune;
     if (k == "host_copy_threads") return c.host_copy_threads;
     if (k == "host_zero_copy") return c.host_zero_copy;
+    if (k == "host_direct_dma") return c.host_direct_dma;
+    if (k == "host_register_cache_bytes") return c.host_register_cache_bytes;
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;

@@ -729,6 +729,11 @@ LocalWorld &RcclLoopback::world(int nranks) {
     return *it->second;
 }
 
+RequestHandler *Communicator::handler_if_created() {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    return handler_.get();
+}
+
 RequestHandler &Communicator::handler() {
     std::lock_guard<std::mutex> g(handler_mu_);
     if (!handler_) handler_.reset(new RequestHandler(this));
@@ -788,6 +793,13 @@ void Registry::clear() {
     }
     comms.clear();
     w.reset();
+}
+
+std::vector<std::shared_ptr<Communicator>> Registry::all() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::shared_ptr<Communicator>> v;
+    for (auto &kv : comms_) v.push_back(kv.second);
+    return v;
 }
 
 bool Registry::initialized() {

@@ -43,6 +43,18 @@ struct Config {
     // address space (torch pin_memory, hipHostMalloc, hipHostRegister): the unpack kernel writes
     // them over PCIe in place of the D2H copy and the host unpack memcpy (1 on, 0 always stage)
     std::atomic<long long> host_zero_copy{1};
+    // keyed host plans: input segments in pinned memory of >= 256 KiB are uploaded by DMA straight
+    // from the tensor instead of host memcpy into the pinned slot + one DMA per chunk (1 on, 0 off,
+    // default: measured slower on the C5 set, 111 vs 62 ms — the many small DMAs of one chunk
+    // serialise on the upload stream; bench keyed_host_c5_pinned_direct_dma)
+    std::atomic<long long> host_direct_dma{0};
+    // keyed host requests: pageable tensors are hipHostRegister'ed once and the registration kept
+    // (up to this many bytes, least recently used out), so repeated allreduce(cpu_tensor) calls take
+    // the pinned paths. 0 (default) = off: a registered range must stay allocated while cached —
+    // the caller opts in for tensors that live as long as the training loop (gradients), and
+    // setting it back to 0 unregisters every cached range at once (ddl_set_config), before the
+    // caller frees them: a freed range left registered poisons later copies from that address.
+    std::atomic<long long> host_register_cache_bytes{0};
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
     // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};
@@ -154,6 +166,7 @@ public:
     // Keyed requests: the handler (created on first use; not collective), this communicator's
     // token ring and the private data-plane communicator its handler reduces on.
     RequestHandler &handler();
+    RequestHandler *handler_if_created();
     ControlChannel *control() const { return control_.get(); }
     // Collective over this communicator: adopts `ch` (already connected over these ranks) as the
     // token ring and creates the keyed data-plane communicator (world: ddl_control_connect).
@@ -236,6 +249,7 @@ public:
     std::shared_ptr<Communicator> find(long long id);  // throws if unknown
     void detach(long long id);
     std::shared_ptr<Communicator> world();              // throws if not initialized
+    std::vector<std::shared_ptr<Communicator>> all();   // every registered communicator
     void set_world(const std::shared_ptr<Communicator> &c);
     void clear();
     bool initialized();

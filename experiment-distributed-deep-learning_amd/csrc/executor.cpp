@@ -245,6 +245,7 @@ void RingExecutor::allgatherv(const void *send, void *recv, const size_t *counts
 
 void RingExecutor::run_(int dtype, hipStream_t user) {
     if (prog_.ticks.empty()) return;
+    DDL_TRACE("executor rank " << rank_ << "/" << size_ << " run: " << prog_.ticks.size() << " ticks, user " << (void *)user);
     // Inside a graph capture the ticks are posted in order on the captured stream itself (every
     // dependency of the program points backwards in tick order, so stream order implies it).
     // Posted on the forked comm / compute streams, the program made hipStreamEndCapture segfault
@@ -348,6 +349,7 @@ void ThreadFabric::abort() {
 
 void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t stream) {
     if (ops.empty()) return;
+    DDL_TRACE("fabric rank " << rank << " group of " << ops.size() << " ops on " << (void *)stream);
     // 1) post every send: the send buffers are ready at this point of `stream`
     hipEvent_t ready = event_();
     DDL_HIP(hipEventRecord(ready, stream));
@@ -379,6 +381,8 @@ void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t st
                     "thread fabric: rank " << rank << " receives " << op.bytes << " B (tag " << op.tag << ") from "
                                            << op.peer << ", whose matching send is " << sd->bytes << " B (tag "
                                            << sd->tag << ")");
+        DDL_TRACE("fabric rank " << rank << " recv " << op.bytes << " B from " << op.peer << " tag " << op.tag << " "
+                                  << sd->ptr << " -> " << op.ptr);
         DDL_HIP(hipStreamWaitEvent(stream, sd->ready, 0));
         if (op.bytes) DDL_HIP(hipMemcpyAsync(op.ptr, sd->ptr, op.bytes, hipMemcpyDeviceToDevice, stream));
         hipEvent_t copied = event_();

@@ -227,6 +227,7 @@ RequestHandler::~RequestHandler() {
     }
     for (hipEvent_t e : hev_)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : reg_) (void)hipHostUnregister(reinterpret_cast<void *>(e.first));
     for (hipStream_t st : {h2d_, d2h_})
         if (st) (void)hipStreamDestroy(st);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -706,18 +707,23 @@ size_t seg_starts(const std::vector<Seg> &segs, bool padded, std::vector<size_t>
     return total;
 }
 
-// Host range [p, p + bytes) is pinned memory the device reaches at the same address, inside one
-// allocation, 16-byte aligned (the unpack kernel's vector path; byte stores over PCIe would
-// crawl). A failed query (pageable memory) leaves no sticky error behind.
-bool mapped_host_range(const void *p, size_t bytes) {
-    if (bytes == 0) return true;
-    if (!p || (reinterpret_cast<uintptr_t>(p) & 15u) != 0) return false;
+// Host range [p, p + bytes) is pinned (page-locked) host memory inside one allocation. With
+// `alias` the range must also be mapped into the device's address space, 16-byte aligned (the
+// unpack kernel's vector path; byte stores over PCIe would crawl): *alias = the device address of
+// p — p itself for torch pin_memory / hipHostMalloc, the mapping's address for a hipHostRegister'ed
+// range. A failed query (pageable memory) leaves no sticky error behind.
+bool mapped_host_range(const void *p, size_t bytes, char **alias = nullptr) {
+    if (bytes == 0) {
+        if (alias) *alias = static_cast<char *>(const_cast<void *>(p));
+        return true;
+    }
+    if (!p || (alias && (reinterpret_cast<uintptr_t>(p) & 15u) != 0)) return false;
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    if (a.type != hipMemoryTypeHost || a.devicePointer != p) return false;
+    if (a.type != hipMemoryTypeHost) return false;
     void *start = nullptr;
     size_t size = 0;
     if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<void *>(p)) != hipSuccess ||
@@ -726,13 +732,18 @@ bool mapped_host_range(const void *p, size_t bytes) {
         return false;
     }
     const uintptr_t s0 = reinterpret_cast<uintptr_t>(start), q = reinterpret_cast<uintptr_t>(p);
-    return start && q >= s0 && q + bytes <= s0 + size;
+    if (!start || q < s0 || q + bytes > s0 + size) return false;
+    if (alias) {
+        if (!a.devicePointer || (reinterpret_cast<uintptr_t>(a.devicePointer) & 15u) != 0) return false;
+        *alias = static_cast<char *>(a.devicePointer);
+    }
+    return true;
 }
 }  // namespace
 
-bool RequestHandler::mapped_host_dsts_(const std::vector<HostSeg> &segs) {
-    for (const HostSeg &sg : segs)
-        if (!mapped_host_range(sg.dst, sg.bytes)) return false;
+bool RequestHandler::mapped_host_dsts_(std::vector<HostSeg> &segs) {
+    for (HostSeg &sg : segs)
+        if (!mapped_host_range(sg.dst, sg.bytes, &sg.ddst)) return false;
     return true;
 }
 
@@ -784,6 +795,17 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     };
     std::vector<void *> dst;
     std::vector<size_t> len;
+    // inputs in pinned, device-mapped memory (torch pin_memory, hipHostMalloc, hipHostRegister):
+    // their large pieces are uploaded by DMA straight from the tensors
+    std::vector<char> direct;
+    if (upload && config().host_direct_dma.load()) {
+        bool any = false;
+        direct.assign(segs.size(), 0);
+        for (size_t i = 0; i < segs.size(); ++i)
+            if (segs[i].bytes >= kDirectDmaMin && mapped_host_range(segs[i].src, segs[i].bytes))
+                direct[i] = any = true;
+        if (!any) direct.clear();
+    }
     for (size_t i = 0; i < nchunks; ++i) {
         const int k = (int)(i % kHostSlots);
         if (i >= (size_t)kHostSlots && !device_unpack) unpack(i - kHostSlots);  // frees slot k (pinned and device)
@@ -794,10 +816,43 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
             // the pinned slot's last upload must have left it (device-unpack plans do not wait
             // for their D2H on the host)
             if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
-            pieces.clear();
-            host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
-            pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
-            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
+            if (!direct.empty()) {
+                // pieces of pinned inputs (segments flagged in `direct`) go straight from the
+                // tensor to the device slot by DMA, no host memcpy; the others are packed into
+                // the pinned slot and uploaded as runs between them
+                pieces.clear();
+                std::vector<std::pair<size_t, size_t>> runs;  // [lo, hi) of the chunk, from pin_[k]
+                std::vector<CopyPool::Piece> dmas;             // straight from the tensors
+                char *pin = static_cast<char *>(pin_[k]);
+                char *dev = static_cast<char *>(dslot_[k]);
+                bool after_dma = true;
+                const size_t end = off + n;
+                for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+                     j < segs.size() && starts[j] < end; ++j) {
+                    const size_t lo = std::max(off, starts[j]), hi = std::min(end, starts[j] + segs[j].bytes);
+                    if (hi <= lo) continue;
+                    const char *src = segs[j].src + (lo - starts[j]);
+                    if (direct[j]) {
+                        dmas.push_back(CopyPool::Piece{dev + (lo - off), src, hi - lo});
+                        after_dma = true;
+                        continue;
+                    }
+                    pieces.push_back(CopyPool::Piece{pin + (lo - off), src, hi - lo});
+                    if (after_dma) runs.emplace_back(lo - off, hi - off);
+                    else runs.back().second = hi - off;  // padding between pieces is harmless
+                    after_dma = false;
+                }
+                pool_->run(pieces);
+                for (const auto &r : runs)
+                    DDL_HIP(hipMemcpyAsync(dev + r.first, pin + r.first, r.second - r.first, hipMemcpyHostToDevice, h2d_));
+                for (const CopyPool::Piece &d : dmas)
+                    DDL_HIP(hipMemcpyAsync(d.dst, d.src, d.bytes, hipMemcpyHostToDevice, h2d_));
+            } else {
+                pieces.clear();
+                host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
+                pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
+                DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
+            }
         }
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
@@ -817,7 +872,7 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
                 const size_t lo = std::max(off, starts[j]), hi = std::min(off + n, starts[j] + segs[j].bytes);
                 if (hi <= lo) continue;
                 DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "device-unpack chunk layout");
-                dst.push_back(segs[j].dst + (lo - starts[j]));
+                dst.push_back(segs[j].ddst + (lo - starts[j]));  // the device's address of the output
                 len.push_back(hi - lo);
                 flat += round256(hi - lo);
             }
@@ -834,6 +889,68 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         return;
     }
     for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) unpack(j);
+}
+
+void RequestHandler::release_registrations() {
+    std::lock_guard<std::mutex> g(reg_mu_);
+    DeviceGuard dg(owner_->device());
+    if (!reg_.empty()) unregister_all_();
+}
+
+void RequestHandler::unregister_all_() {
+    for (hipStream_t st : {h2d_, d2h_, stream_})  // rounds in flight may still DMA from / to them
+        if (st) DDL_HIP(hipStreamSynchronize(st));
+    for (auto &e : reg_) (void)hipHostUnregister(reinterpret_cast<void *>(e.first));
+    reg_.clear();
+    reg_bytes_ = 0;
+}
+
+void RequestHandler::register_host_(const void *p, size_t bytes) {
+    if (!p || bytes == 0) return;
+    constexpr uintptr_t kPage = 4096;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1);
+    const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes + kPage - 1) & ~(kPage - 1);
+    const uint64_t tick = ++reg_tick_;
+    // inside a range registered here before: touch it
+    auto it = reg_.upper_bound(lo);
+    if (it != reg_.begin()) {
+        auto prev = std::prev(it);
+        if (prev->first <= lo && hi <= prev->first + prev->second.first) {
+            prev->second.second = tick;
+            return;
+        }
+    }
+    if (mapped_host_range(p, bytes)) return;  // pinned already (the framework's own)
+    const size_t cap = (size_t)config().host_register_cache_bytes.load();
+    if (hi - lo > cap) return;
+    // overlapping an entry (a tensor that grew or moved): drop the overlapping entries first
+    std::vector<uintptr_t> drop;
+    for (auto &e : reg_)
+        if (e.first < hi && lo < e.first + e.second.first) drop.push_back(e.first);
+    auto release = [&](uintptr_t a) {
+        if (!sync_for_unregister_) {  // rounds in flight may still DMA from / to it
+            for (hipStream_t st : {h2d_, d2h_, stream_})
+                if (st) DDL_HIP(hipStreamSynchronize(st));
+            sync_for_unregister_ = true;
+        }
+        (void)hipHostUnregister(reinterpret_cast<void *>(a));
+        reg_bytes_ -= reg_[a].first;
+        reg_.erase(a);
+    };
+    for (uintptr_t a : drop) release(a);
+    while (reg_bytes_ + (hi - lo) > cap && !reg_.empty()) {  // least recently used out
+        auto lru = reg_.begin();
+        for (auto e = reg_.begin(); e != reg_.end(); ++e)
+            if (e->second.second < lru->second.second) lru = e;
+        release(lru->first);
+    }
+    sync_for_unregister_ = false;
+    if (hipHostRegister(reinterpret_cast<void *>(lo), hi - lo, hipHostRegisterMapped) != hipSuccess) {
+        (void)hipGetLastError();  // e.g. part of the range is registered by someone else: stage as before
+        return;
+    }
+    reg_[lo] = std::make_pair((size_t)(hi - lo), tick);
+    reg_bytes_ += hi - lo;
 }
 
 // allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
@@ -855,6 +972,13 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
         for (size_t i : g.second) {
             elems.push_back(reqs[i].n);
             esz.push_back(es);
+        }
+        if (host && config().host_register_cache_bytes.load() > 0) {
+            std::lock_guard<std::mutex> rg(reg_mu_);
+            for (size_t i : g.second) {  // pageable tensors used again and again: registered once
+                register_host_(reqs[i].in, reqs[i].n * es);
+                if (reqs[i].out != reqs[i].in) register_host_(reqs[i].out, reqs[i].n * es);
+            }
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
@@ -1037,6 +1161,13 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
         for (size_t i : g.second) {
             elems.push_back(reqs[i].n);
             esz.push_back(es);
+        }
+        if (host && config().host_register_cache_bytes.load() > 0) {
+            std::lock_guard<std::mutex> rg(reg_mu_);
+            for (size_t i : g.second) {  // pageable tensors used again and again: registered once
+                register_host_(reqs[i].in, reqs[i].n * es);
+                if (reqs[i].out != reqs[i].in) register_host_(reqs[i].out, reqs[i].n * es);
+            }
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);

@@ -164,6 +164,9 @@ public:
     ~RequestHandler();
 
     void submit(Request r);
+    // Unregisters every range of the host registration cache (ddl_set_config
+    // "host_register_cache_bytes" 0): waits for the handler's streams first.
+    void release_registrations();
     // All-or-nothing registration of several requests under one lock (one wake-up).
     void submit_batch(std::vector<Request> &rs);
     void wait_all();
@@ -204,6 +207,9 @@ private:
     // a round of at most this many bytes, with no earlier round in flight, completes on the
     // engine thread even when pipelined (its data plane is microseconds: the hand-off costs more)
     static constexpr size_t kInlineRoundBytes = 256u << 10;
+    // host staging: a pinned input segment of at least this many bytes is uploaded by DMA straight
+    // from the tensor (config "host_direct_dma"); smaller ones are packed by the copy threads
+    static constexpr size_t kDirectDmaMin = 256u << 10;
     size_t record_plan_(size_t &nplans);  // records the round's next plan event on stream_
     void complete_(Round &rd);            // waits the plan events, fires done(), frees the events
     void completer_();                    // the completion thread
@@ -233,6 +239,7 @@ private:
         const char *src;
         char *dst;
         size_t bytes;
+        char *ddst = nullptr;  // the device's address of dst (device unpack; mapped_host_dsts_)
     };
     void host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
                       const std::function<void(void *dev, size_t elems)> &coll, bool padded = false,
@@ -241,7 +248,8 @@ private:
                       char *pinned, bool pack, std::vector<CopyPool::Piece> &out);
     // true when every segment's destination range is 16-byte-aligned pinned host memory that the
     // device reaches at the same address, inside one allocation
-    static bool mapped_host_dsts_(const std::vector<HostSeg> &segs);
+    // fills every segment's ddst; false unless all of them are mapped
+    static bool mapped_host_dsts_(std::vector<HostSeg> &segs);
     size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
@@ -271,6 +279,16 @@ private:
     hipEvent_t hev_[3 * kHostSlots] = {};  // per slot: input landed, collective done, output landed
     bool slot_used_[kHostSlots] = {};        // hev_[3k + 2] marks the slot's last device use
     std::unique_ptr<CopyPool> pool_;
+    // opt-in registration cache (config "host_register_cache_bytes"): pageable host tensors of
+    // keyed requests are hipHostRegister'ed once and kept (least recently used out past the cap),
+    // so a training loop's CPU gradients take the pinned paths (direct DMA in, device unpack out)
+    void register_host_(const void *p, size_t bytes);
+    void unregister_all_();  // the cache was switched off (host_register_cache_bytes 0)
+    std::mutex reg_mu_;  // reg_: the engine thread registers, ddl_set_config may release
+    std::map<uintptr_t, std::pair<size_t, uint64_t>> reg_;  // page-aligned start -> (bytes, last use)
+    size_t reg_bytes_ = 0;
+    uint64_t reg_tick_ = 0;
+    bool sync_for_unregister_ = false;
     void *pin_gather_ = nullptr;  // host allgather staging
     size_t pin_gather_bytes_ = 0;
 

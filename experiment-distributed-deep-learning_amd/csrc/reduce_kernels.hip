@@ -250,27 +250,29 @@ int reduce_threads() {
     return v;
 }
 
-// Fold cache policy: bit 0 non-temporal loads of the received inputs, bit 1 non-temporal store.
-// Large chunks stream every operand once: 3, 5.77 TB/s vs 5.50 plain on a P=8 chunk (32 MiB
-// fp32, 7 inputs, rotating buffers, r01). Chunks up to 8 MiB (the whole fold's operands fit the
+// Fold cache policy (FV bits): 1 non-temporal loads, 2 non-temporal store, 4 write-through
+// (sc0 sc1) store. Chunks above 8 MiB stream every input once: non-temporal loads, and the output
+// written through (it leaves the XCD's L2 at once; r03 tools/fold_tune.hip at 32 MiB, 8 inputs:
+// 6.48-6.51 TB/s vs 6.35-6.36 all-nt, the r02 policy). Chunks up to 8 MiB (their operands fit the
 // 256 MiB Infinity Cache, where RCCL has just written the received slices) read through the
-// caches: 0, 4.6 vs 6.0 us on a 4 MiB chunk (profiles/r02/pack/small_fold_v*.jsonl).
-// DDL_FOLD_VARIANT (0..3) forces one policy for measurement.
+// caches: 5.53 vs 5.05 TB/s at 4 MiB (plain loads + write-through store vs all-nt).
+// DDL_FOLD_VARIANT (0..7) forces one policy for measurement (4 or 5; anything else maps to 5).
 int fold_variant(size_t chunk_bytes) {
     static const int forced = [] {
         const char *e = std::getenv("DDL_FOLD_VARIANT");
-        return e ? std::atoi(e) & 3 : -1;
+        return e ? std::atoi(e) & 7 : -1;
     }();
-    if (forced >= 0) return forced;
-    return chunk_bytes <= (8u << 20) ? 0 : 3;
+    if (forced >= 0) return forced == 4 ? 4 : 5;
+    return chunk_bytes <= (8u << 20) ? 4 : 5;
 }
 
-// One 4 KiB tile of the output per workgroup: each lane folds its 16 bytes across a and the nb
-// received inputs (loads of all inputs issued before the adds), one store. HBM bytes per
-// element: (nb + 2) * sizeof(T).
-// NB (received inputs) is a template parameter: every load is unconditional and all of them
-// are in flight before the first add (a runtime "load or skip" per input makes hipcc wait
-// vmcnt(0) per input).
+// One 2 KiB tile of the output per 128-lane workgroup: each lane folds its 16 bytes across a
+// and the nb received inputs, one buffer_load_dwordx4 per input through one descriptor per input
+// tile (32-bit lane offsets, the cache bits in each access's aux word; lanes past the tile's last
+// vector read 0 and drop their store) — the two-input reduce's mapping. All NB + 1 loads are in
+// flight before the first add. HBM bytes per element: (nb + 2) * sizeof(T).
+// NB (received inputs) is a template parameter: every load is unconditional (a runtime "load or
+// skip" per input makes hipcc wait vmcnt(0) per input).
 constexpr int kFoldThreads = 128;
 template <int DT, int NB, int FV, int ORDER>
 __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
@@ -279,16 +281,24 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
     using S = typename Add<DT>::S;
     using T = typename A::T;
     constexpr int V = 16 / sizeof(S);
+    constexpr int kLoadAux = (FV & 1) ? kAuxNt : 0;
+    constexpr int kStoreAux = ((FV & 2) ? kAuxNt : 0) | ((FV & 4) ? (kAuxSc0 | kAuxSc1) : 0);
     const uint64_t nv = t.n / V;
-    const uint64_t i = (uint64_t)blockIdx.x * kTileVec + threadIdx.x;
-    if (i < nv) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTileVec;
+    if (base < nv) {
+        const int bytes = (int)((nv - base < kTileVec ? nv - base : kTileVec) * 16);
+        const int off = (int)threadIdx.x * 16;
         u32x4 raw[NB + 1];
-        raw[0] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.a) + i);
+        raw[0] = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(static_cast<const u32x4 *>(t.a) + base), 0, bytes,
+                                              kRsrcWord3),
+            off, 0, kLoadAux);
 #pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            if (FV & 1) raw[k + 1] = __builtin_nontemporal_load(static_cast<const u32x4 *>(t.b[k]) + i);
-            else raw[k + 1] = static_cast<const u32x4 *>(t.b[k])[i];
-        }
+        for (int k = 0; k < NB; ++k)
+            raw[k + 1] = __builtin_amdgcn_raw_buffer_load_b128(
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(static_cast<const u32x4 *>(t.b[k]) + base), 0,
+                                                  bytes, kRsrcWord3),
+                off, 0, kLoadAux);
         u32x4 res;
         S *rs = reinterpret_cast<S *>(&res);
 #pragma unroll
@@ -298,8 +308,9 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
             for (int k = 0; k <= NB; ++k) w[k] = A::widen(reinterpret_cast<const S *>(&raw[k])[e]);
             rs[e] = A::narrow(fold_values<DT, NB + 1, ORDER>(w));
         }
-        if (FV & 2) __builtin_nontemporal_store(res, static_cast<u32x4 *>(t.out) + i);
-        else static_cast<u32x4 *>(t.out)[i] = res;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            res, __builtin_amdgcn_make_buffer_rsrc(static_cast<u32x4 *>(t.out) + base, 0, bytes, kRsrcWord3), off, 0,
+            kStoreAux);
     }
     const uint64_t rem = t.n - nv * V;
     if (rem && blockIdx.x == nv / kTileVec && threadIdx.x < rem) {
@@ -337,10 +348,10 @@ void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
     } else {
         if (t.nb == NB) {
-            // cache policy (fold_variant): 3 = every operand non-temporal (large chunks),
-            // 0 = plain (chunks up to 8 MiB, in cache)
-            if (fold_variant((size_t)t.n * sizeof(typename Add<DT>::S)) == 0) launch_sumN_order<DT, NB, 0>(t, stream, tiles);
-            else launch_sumN_order<DT, NB, 3>(t, stream, tiles);
+            // cache policy (fold_variant): 5 = non-temporal loads + write-through store (large
+            // chunks), 4 = plain loads + write-through store (chunks up to 8 MiB, in cache)
+            if (fold_variant((size_t)t.n * sizeof(typename Add<DT>::S)) == 4) launch_sumN_order<DT, NB, 4>(t, stream, tiles);
+            else launch_sumN_order<DT, NB, 5>(t, stream, tiles);
         } else {
             launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
         }

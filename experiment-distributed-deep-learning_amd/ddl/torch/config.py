@@ -1,7 +1,10 @@
 """Engine tunables from Python (ddl_set_config / ddl_get_config, include/ddl_amd.h).
 
-Every rank must set the same values in the same order: the schedule, the fusion plans and the
-summation order are collective decisions. The reference has no tunables beyond its compiled
+The SHARED tunables (SHARED below) must be equal on every rank: the schedule, the fusion plans and
+the summation order are collective decisions. The ranks agree on a hash of them at a
+communicator's first collective and after any change (change them on every rank between the same
+two collectives), and every keyed round carries it: a mismatch fails the collective or round on
+every rank with CONFIG_MISMATCH instead of hanging. The other keys are per process. The reference has no tunables beyond its compiled
 constants (MAX_MPI_BUFFER_SIZE, MPIBackend.h:12); the defaults reproduce its behaviour, with
 `reference_order` = 1 making every sum bit-equal to its MPI_Allreduce.
 
@@ -15,8 +18,10 @@ import contextlib
 from ddl.torch.cpp_backend import CPPBackend, check
 
 KEYS = ('algo', 'slice_bytes', 'rings', 'max_slices', 'fusion_threshold_bytes', 'log_level', 'cycle_time_us',
-        'host_chunk_bytes', 'host_copy_threads', 'host_zero_copy', 'tune', 'fusion_pipeline_bytes', 'one_rank_shortcut', 'pipeline_rounds',
-        'reference_order')
+        'host_chunk_bytes', 'host_copy_threads', 'host_zero_copy', 'tune', 'fusion_pipeline_bytes', 'one_rank_shortcut',
+        'pipeline_rounds', 'reference_order', 'host_direct_dma', 'host_register_cache_bytes', 'capture_forked')
+SHARED = ('algo', 'slice_bytes', 'rings', 'max_slices', 'fusion_threshold_bytes', 'tune', 'fusion_pipeline_bytes',
+          'reference_order', 'host_chunk_bytes')
 
 
 def set(key: str, value: int) -> None:  # noqa: A001 (mirrors ddl_set_config)

@@ -134,6 +134,11 @@ class CPPBackend:
         sig('ddl_local_ring_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, ci, vp)
         # RCCL loopback (test / diagnostic: the RCCL transport on one GPU)
         fp, lp = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_longlong)
+        sig('ddl_testing_thread_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, vp)
+        sig('ddl_testing_thread_broadcast', ci, ci, ci, ctypes.POINTER(vp), sz, ci, vp)
+        sig('ddl_testing_thread_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
+            ctypes.POINTER(sz), ci, vp)
+        sig('ddl_testing_drop_wait', ci, ci)
         sig('ddl_rccl_loopback_init', ci, ci)
         sig('ddl_rccl_loopback_split', ci, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci))
         sig('ddl_rccl_loopback_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, vp)

@@ -123,6 +123,14 @@ int ddl_is_initialized(void);
  * pin_memory, hipHostMalloc, hipHostRegister — is unpacked by the fusion kernel straight into
  * them over PCIe, no D2H copy or host memcpy; 0: always stage through the pinned slots; the
  * read-only "host_zero_copy_plans" counts the plans that took that path),
+ * "host_direct_dma" (0, default; 1: pinned input segments of >= 256 KiB of a keyed host plan are
+ * uploaded by DMA straight from the tensors instead of through the copy threads — slower on the C5
+ * set), "host_register_cache_bytes" (0, default = off; > 0: pageable host tensors of keyed requests
+ * are hipHostRegister'ed once and the registrations kept, least recently used out past this many
+ * bytes, so repeated allreduce(cpu_tensor) calls take the pinned paths — the caller keeps those
+ * tensors allocated while cached; setting it to 0 unregisters every cached range at once, after
+ * ddl_wait_all), "capture_forked" (0, default: inside a hipGraph capture the program is posted
+ * serially on the captured stream; 1: on the forked comm / compute streams — see DESIGN §9),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "pipeline_rounds" (1,

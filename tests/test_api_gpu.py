@@ -349,7 +349,8 @@ def test_keyed_fusion_pipeline_large_segment(world, lib, data_plane_at_one_rank)
         assert torch.equal(h.wait(timeout=60), w)
 
 
-@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'pinned_outputs', 'mixed', 'pinned_misaligned'])
+@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'pinned_outputs', 'mixed', 'pinned_misaligned',
+                                    'pinned_direct', 'registered'])
 @pytest.mark.parametrize('chunk', [4096, 64 << 10, 32 << 20])
 def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     """Keyed requests on host tensors with the one-rank shortcut off: every plan goes through the
@@ -358,24 +359,32 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     bit (one rank). Pageable outputs are staged back (D2H -> host unpack); when every output of a
     plan is pinned the unpack kernel writes them over PCIe — the plan counter says which path
     ran. A pinned output viewed at a 2-byte offset, or one pageable output in the dtype group,
-    sends its plan back to staging."""
+    sends its plan back to staging. 'pinned_direct': pinned inputs of >= 256 KiB uploaded by DMA
+    straight from the tensors (host_direct_dma 1); 'registered': pageable tensors with the opt-in
+    registration cache take the pinned paths (the unpack kernel writes the registered outputs
+    through their device mapping); switching the cache off unregisters them again."""
     from ddl.torch.tensor_communicate import allreduce_async_batch, broadcast_async
-    keys = (b'one_rank_shortcut', b'host_chunk_bytes')
+    keys = (b'one_rank_shortcut', b'host_chunk_bytes', b'host_direct_dma', b'host_register_cache_bytes')
     old = {k: lib.ddl_get_config(k) for k in keys}
     try:
         assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
         assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
+        if memory == 'pinned_direct':
+            assert lib.ddl_set_config(b'host_direct_dma', 1) == 0
+        if memory == 'registered':
+            assert lib.ddl_set_config(b'host_register_cache_bytes', 1 << 30) == 0
         g = torch.Generator().manual_seed(chunk)
         dts = [torch.float32, torch.float64, torch.int32, torch.float16, torch.bfloat16, torch.int64]
         xs = [(torch.randn(n, generator=g) * 100).to(dts[i % 6]) for i, n in enumerate([1, 7, 1000, 65_537, 300_001,
                                                                                        5, 2_000_003, 4096])]
-        if memory in ('pinned', 'mixed', 'pinned_misaligned'):
+        if memory in ('pinned', 'mixed', 'pinned_misaligned', 'pinned_direct'):
             xs = [x.pin_memory() for x in xs]
         if memory == 'pinned_misaligned':  # fp16 tensor 3 (in place) seen from its second element: 2-byte offset
             xs[3] = xs[3][1:]
         keep = [x.clone() for x in xs]
         # odd tensors in place, even ones into fresh outputs (int32 tensor 2: pageable when mixed)
-        outs = [x if i % 2 else torch.empty_like(x, pin_memory=memory != 'pageable' and (memory, i) != ('mixed', 2))
+        outs = [x if i % 2 else torch.empty_like(x, pin_memory=memory not in ('pageable', 'registered') and
+                                                 (memory, i) != ('mixed', 2))
                 for i, x in enumerate(xs)]
         if memory == 'pinned_outputs':  # pageable inputs, every output pinned
             outs = [torch.empty_like(x, pin_memory=True) for x in xs]
@@ -391,7 +400,7 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
         # misaligned fp16 group
         device_unpacked = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
         assert device_unpacked == {'pageable': 0, 'pinned': 6, 'pinned_outputs': 6, 'mixed': 5,
-                                   'pinned_misaligned': 5}[memory]
+                                   'pinned_misaligned': 5, 'pinned_direct': 6, 'registered': 6}[memory]
         t = torch.arange(100_003, dtype=torch.float64)
         assert torch.equal(broadcast_async(t, 'hk_b', 0, world).wait(timeout=60), t)
     finally:

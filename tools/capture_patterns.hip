@@ -16,6 +16,10 @@
 //     waits re[0] AFTER compute captured fold 1 .. K-1 behind it
 //  12 s1 records e1 after a kernel, then captures another kernel; s2 (with a node) waits e1
 //  13 as 12, but s2 has no node of its own when it waits e1
+//  14 the minimal crash found by bisecting the engine's P = 3 program (tools/capture_replay.hip,
+//     profiles/r03/graph/): three forked streams A B C record pA pB pC before any node; A waits
+//     pC, copies, waits pB, copies; C copies, then waits pA; all joined. Every wait is on an event
+//     recorded in the capture and every stream is joined — hipStreamEndCapture segfaults.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -179,6 +183,29 @@ int main(int argc, char **argv) {
             CK(hipEventRecord(j2, s2));
             CK(hipStreamWaitEvent(o, j1, 0));
             CK(hipStreamWaitEvent(o, j2, 0));
+            break;
+        }
+        case 14: {
+            hipStream_t s3;
+            hipEvent_t pa, pb, pc, j3;
+            CK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+            for (hipEvent_t *e : {&pa, &pb, &pc, &j3}) CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            CK(hipStreamWaitEvent(s3, fork, 0));  // A = s1, B = s2, C = s3 (s1, s2 waited above)
+            CK(hipEventRecord(pa, s1));
+            CK(hipEventRecord(pb, s2));
+            CK(hipEventRecord(pc, s3));
+            CK(hipStreamWaitEvent(s1, pc, 0));
+            CK(hipMemcpyAsync(b, a, 256, hipMemcpyDeviceToDevice, s1));
+            CK(hipStreamWaitEvent(s1, pb, 0));
+            CK(hipMemcpyAsync(b + 64, a + 64, 256, hipMemcpyDeviceToDevice, s1));
+            CK(hipMemcpyAsync(c, a, 432, hipMemcpyDeviceToDevice, s3));
+            CK(hipStreamWaitEvent(s3, pa, 0));
+            CK(hipEventRecord(j1, s1));
+            CK(hipEventRecord(j2, s2));
+            CK(hipEventRecord(j3, s3));
+            CK(hipStreamWaitEvent(o, j1, 0));
+            CK(hipStreamWaitEvent(o, j2, 0));
+            CK(hipStreamWaitEvent(o, j3, 0));
             break;
         }
         case 5:
