@@ -343,21 +343,37 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False):
                                           nb, n, 19 if half else DT_FLOAT, order, sh), 'ddl_reduce_fold_ordered')
     for k in range(4):
         run(k)
+    torch.cuda.synchronize()
+    # the 20 launches captured once into a hipGraph and replayed: back-to-back kernels with no
+    # host launch between them (a 4 us kernel would otherwise measure the Python launch rate)
+    gs = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=gs):
+        sh_g = gs.cuda_stream
+        for k in range(20):
+            b = sets[k % 2]
+            check(lib.ddl_reduce_fold_ordered(b[-1].data_ptr(), b[0].data_ptr(),
+                                              P(*[t.data_ptr() for t in b[1:-1]]), nb, n, 19 if half else DT_FLOAT,
+                                              order, sh_g), 'ddl_reduce_fold_ordered (captured)')
     best = float('inf')
     for _ in range(3):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for k in range(20):
-            run(k)
-        e1.record()
+        with torch.cuda.stream(gs):
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(gs)
+            graph.replay()
+            e1.record(gs)
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
+    del graph
     byts = (nb + 2) * n * es
     return {'kernel': f'k_sumN_tile<{"DDL_HALF" if half else "DDL_FLOAT"},{nb},order {order}>', 'chunk_bytes': n * es,
+            'timing': '20 launches captured into a hipGraph, replayed between HIP events on the replay stream',
             'us': round(best * 1e6, 1),
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
             'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
-            'traffic': pmc_traffic('fold_fp32_P8_chunk') if S == 256 << 20 and order == 0 and not half else None}
+            'traffic': (pmc_traffic('fold_fp16_P8_C4_chunk') if half else pmc_traffic('fold_fp32_P8_chunk'))
+            if order == 0 and ((S == 256 << 20 and not half) or (S == 16 << 20 and half)) else None}
 
 
 def half_dtypes(lib, dev, sh, S):
@@ -590,6 +606,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             step()
         dt = (time.perf_counter() - t0) / steps
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
+        registered = {'host_registered_bytes': int(lib.ddl_get_config(b'host_registered_bytes')),
+                      'host_register_failures': int(lib.ddl_get_config(b'host_register_failures'))}
     finally:
         for kk, v in old.items():
             lib.ddl_set_config(kk.encode(), v)
@@ -603,7 +621,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path,
             'host_direct_dma': int(lib.ddl_get_config(b'host_direct_dma')) if 'host_direct_dma' not in settings
             else settings['host_direct_dma'],
-            'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'}}
+            'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},
+            **(registered if 'host_register_cache_bytes' in settings else {})}
 
 
 def host_resident_rate(lib, comm, S, reps):

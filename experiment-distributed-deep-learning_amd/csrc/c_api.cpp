@@ -373,6 +373,8 @@ long long ddl_get_config(const char *key) {
     if (k == "host_zero_copy") return c.host_zero_copy;
     if (k == "host_direct_dma") return c.host_direct_dma;
     if (k == "host_register_cache_bytes") return c.host_register_cache_bytes;
+    if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
+    if (k == "host_register_failures") return c.host_register_failures;  // statistic, not settable
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;

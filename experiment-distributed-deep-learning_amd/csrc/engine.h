@@ -55,6 +55,9 @@ struct Config {
     // setting it back to 0 unregisters every cached range at once (ddl_set_config), before the
     // caller frees them: a freed range left registered poisons later copies from that address.
     std::atomic<long long> host_register_cache_bytes{0};
+    // read-only statistics of that cache (ddl_get_config): bytes registered now, failed registrations
+    std::atomic<long long> host_registered_bytes{0};
+    std::atomic<long long> host_register_failures{0};
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
     // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};

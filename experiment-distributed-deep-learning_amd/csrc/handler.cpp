@@ -900,57 +900,80 @@ void RequestHandler::release_registrations() {
 void RequestHandler::unregister_all_() {
     for (hipStream_t st : {h2d_, d2h_, stream_})  // rounds in flight may still DMA from / to them
         if (st) DDL_HIP(hipStreamSynchronize(st));
-    for (auto &e : reg_) (void)hipHostUnregister(reinterpret_cast<void *>(e.first));
+    for (auto &e : reg_) {
+        (void)hipHostUnregister(reinterpret_cast<void *>(e.first));
+        config().host_registered_bytes.fetch_sub((long long)e.second.first);
+    }
+    (void)hipGetLastError();
     reg_.clear();
     reg_bytes_ = 0;
 }
 
-void RequestHandler::register_host_(const void *p, size_t bytes) {
-    if (!p || bytes == 0) return;
+void RequestHandler::register_hosts_(const std::vector<std::pair<const void *, size_t>> &ranges) {
     constexpr uintptr_t kPage = 4096;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1);
-    const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes + kPage - 1) & ~(kPage - 1);
-    const uint64_t tick = ++reg_tick_;
-    // inside a range registered here before: touch it
-    auto it = reg_.upper_bound(lo);
-    if (it != reg_.begin()) {
-        auto prev = std::prev(it);
-        if (prev->first <= lo && hi <= prev->first + prev->second.first) {
-            prev->second.second = tick;
-            return;
-        }
-    }
-    if (mapped_host_range(p, bytes)) return;  // pinned already (the framework's own)
     const size_t cap = (size_t)config().host_register_cache_bytes.load();
-    if (hi - lo > cap) return;
-    // overlapping an entry (a tensor that grew or moved): drop the overlapping entries first
-    std::vector<uintptr_t> drop;
-    for (auto &e : reg_)
-        if (e.first < hi && lo < e.first + e.second.first) drop.push_back(e.first);
+    // 1) the page ranges of the tensors not pinned already, merged where they share pages (small
+    //    tensors of one heap page; hipHostRegister refuses a page registered twice)
+    std::vector<std::pair<uintptr_t, uintptr_t>> want;
+    for (const auto &r : ranges) {
+        if (!r.first || r.second == 0) continue;
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1);
+        const uintptr_t hi = (reinterpret_cast<uintptr_t>(r.first) + r.second + kPage - 1) & ~(kPage - 1);
+        auto it = reg_.upper_bound(lo);  // inside an entry already: touch it
+        if (it != reg_.begin() && std::prev(it)->first <= lo && hi <= std::prev(it)->first + std::prev(it)->second.first) {
+            std::prev(it)->second.second = ++reg_tick_;
+            continue;
+        }
+        if (mapped_host_range(r.first, r.second)) continue;  // pinned already (the framework's own)
+        want.emplace_back(lo, hi);
+    }
+    std::sort(want.begin(), want.end());
+    std::vector<std::pair<uintptr_t, uintptr_t>> merged;
+    for (const auto &w : want) {
+        if (!merged.empty() && w.first < merged.back().second) merged.back().second = std::max(merged.back().second, w.second);
+        else merged.push_back(w);
+    }
+    if (merged.empty()) return;
+    bool synced = false;
     auto release = [&](uintptr_t a) {
-        if (!sync_for_unregister_) {  // rounds in flight may still DMA from / to it
+        if (!synced) {  // rounds in flight may still DMA from / to it
             for (hipStream_t st : {h2d_, d2h_, stream_})
                 if (st) DDL_HIP(hipStreamSynchronize(st));
-            sync_for_unregister_ = true;
+            synced = true;
         }
         (void)hipHostUnregister(reinterpret_cast<void *>(a));
+        (void)hipGetLastError();
         reg_bytes_ -= reg_[a].first;
+        config().host_registered_bytes.fetch_sub((long long)reg_[a].first);
         reg_.erase(a);
     };
-    for (uintptr_t a : drop) release(a);
-    while (reg_bytes_ + (hi - lo) > cap && !reg_.empty()) {  // least recently used out
-        auto lru = reg_.begin();
-        for (auto e = reg_.begin(); e != reg_.end(); ++e)
-            if (e->second.second < lru->second.second) lru = e;
-        release(lru->first);
+    for (auto m : merged) {
+        // 2) entries overlapping it (a tensor that grew, moved or shares a page) join the union
+        std::vector<uintptr_t> drop;
+        for (auto &e : reg_)
+            if (e.first < m.second && m.first < e.first + e.second.first) {
+                drop.push_back(e.first);
+                m.first = std::min(m.first, e.first);
+                m.second = std::max(m.second, (uintptr_t)(e.first + e.second.first));
+            }
+        const size_t bytes = m.second - m.first;
+        if (bytes > cap) continue;
+        for (uintptr_t a : drop) release(a);
+        while (reg_bytes_ + bytes > cap && !reg_.empty()) {  // least recently used out
+            auto lru = reg_.begin();
+            for (auto e = reg_.begin(); e != reg_.end(); ++e)
+                if (e->second.second < lru->second.second) lru = e;
+            release(lru->first);
+        }
+        if (hipHostRegister(reinterpret_cast<void *>(m.first), bytes, hipHostRegisterMapped) != hipSuccess) {
+            (void)hipGetLastError();  // e.g. registered by someone else: staged as before
+            config().host_register_failures.fetch_add(1);
+            continue;
+        }
+        reg_[m.first] = std::make_pair(bytes, ++reg_tick_);
+        reg_bytes_ += bytes;
+        config().host_registered_bytes.fetch_add((long long)bytes);
     }
-    sync_for_unregister_ = false;
-    if (hipHostRegister(reinterpret_cast<void *>(lo), hi - lo, hipHostRegisterMapped) != hipSuccess) {
-        (void)hipGetLastError();  // e.g. part of the range is registered by someone else: stage as before
-        return;
-    }
-    reg_[lo] = std::make_pair((size_t)(hi - lo), tick);
-    reg_bytes_ += hi - lo;
 }
 
 // allreduceRequests (MPIRingTokenCommunication.cc:105-157): dtype groups in ascending enum order,
@@ -975,10 +998,12 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         if (host && config().host_register_cache_bytes.load() > 0) {
             std::lock_guard<std::mutex> rg(reg_mu_);
-            for (size_t i : g.second) {  // pageable tensors used again and again: registered once
-                register_host_(reqs[i].in, reqs[i].n * es);
-                if (reqs[i].out != reqs[i].in) register_host_(reqs[i].out, reqs[i].n * es);
+            std::vector<std::pair<const void *, size_t>> ranges;  // pageable tensors used again and again
+            for (size_t i : g.second) {
+                ranges.emplace_back(reqs[i].in, reqs[i].n * es);
+                if (reqs[i].out != reqs[i].in) ranges.emplace_back(reqs[i].out, reqs[i].n * es);
             }
+            register_hosts_(ranges);  // registered once, kept
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);
@@ -1164,10 +1189,12 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
         }
         if (host && config().host_register_cache_bytes.load() > 0) {
             std::lock_guard<std::mutex> rg(reg_mu_);
-            for (size_t i : g.second) {  // pageable tensors used again and again: registered once
-                register_host_(reqs[i].in, reqs[i].n * es);
-                if (reqs[i].out != reqs[i].in) register_host_(reqs[i].out, reqs[i].n * es);
+            std::vector<std::pair<const void *, size_t>> ranges;  // pageable tensors used again and again
+            for (size_t i : g.second) {
+                ranges.emplace_back(reqs[i].in, reqs[i].n * es);
+                if (reqs[i].out != reqs[i].in) ranges.emplace_back(reqs[i].out, reqs[i].n * es);
             }
+            register_hosts_(ranges);  // registered once, kept
         }
         for (const Plan &p : make_plans(elems, esz, (size_t)config().fusion_threshold_bytes.load())) {
             for (size_t q = p.req_begin; q <= p.req_end; ++q) wait_inputs_(reqs[g.second[q]], waited);

@@ -282,13 +282,14 @@ private:
     // opt-in registration cache (config "host_register_cache_bytes"): pageable host tensors of
     // keyed requests are hipHostRegister'ed once and kept (least recently used out past the cap),
     // so a training loop's CPU gradients take the pinned paths (direct DMA in, device unpack out)
-    void register_host_(const void *p, size_t bytes);
+    // registers the page ranges of (pointer, bytes) that are not pinned yet: ranges sharing a page
+    // are merged (a page cannot be registered twice), overlapping entries join the union
+    void register_hosts_(const std::vector<std::pair<const void *, size_t>> &ranges);
     void unregister_all_();  // the cache was switched off (host_register_cache_bytes 0)
     std::mutex reg_mu_;  // reg_: the engine thread registers, ddl_set_config may release
     std::map<uintptr_t, std::pair<size_t, uint64_t>> reg_;  // page-aligned start -> (bytes, last use)
     size_t reg_bytes_ = 0;
     uint64_t reg_tick_ = 0;
-    bool sync_for_unregister_ = false;
     void *pin_gather_ = nullptr;  // host allgather staging
     size_t pin_gather_bytes_ = 0;
 
