@@ -8,7 +8,7 @@
 // read-heavy stream mix tops out lower on this HBM?
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_mix.hip -o tools/bin/stream_mix
-//   ./stream_mix [total MiB per launch = 288] [rounds = 5]
+//   ./stream_mix [total MiB per launch = 288] [rounds = 5] [occ: occupancy-cap sweep instead]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -79,13 +79,18 @@ struct Case {
     std::function<void(const Streams &, unsigned long long, hipStream_t)> launch;
 };
 
+// lds_kib > 0 reserves that much (unused) dynamic LDS per workgroup: 160 KiB per CU / lds_kib caps
+// the workgroups resident on a CU, so fewer tiles of every stream are in flight at once
 template <int R, int W, int AUX>
-Case mk(const char *pol) {
+Case mk(const char *pol, int lds_kib = 0) {
     char nm[96];
-    std::snprintf(nm, sizeof nm, "R%d W%d (%d:%d) %s", R, W, R, W, pol);
-    return Case{nm, R, W, [](const Streams &s, unsigned long long nv, hipStream_t st) {
+    if (lds_kib)
+        std::snprintf(nm, sizeof nm, "R%d W%d (%d:%d) %s, <= %d WG/CU", R, W, R, W, pol, 160 / lds_kib);
+    else
+        std::snprintf(nm, sizeof nm, "R%d W%d (%d:%d) %s", R, W, R, W, pol);
+    return Case{nm, R, W, [lds_kib](const Streams &s, unsigned long long nv, hipStream_t st) {
                     const unsigned tiles = (unsigned)((nv + kT - 1) / kT);
-                    hipLaunchKernelGGL((k_mix<R, W, AUX>), dim3(tiles), dim3(kT), 0, st, s, nv);
+                    hipLaunchKernelGGL((k_mix<R, W, AUX>), dim3(tiles), dim3(kT), (size_t)lds_kib << 10, st, s, nv);
                 }};
 }
 
@@ -93,6 +98,7 @@ int main(int argc, char **argv) {
     const size_t total_mib = argc > 1 ? std::atoi(argv[1]) : 288;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 5;
     const int reps = 8, sets = 3;
+    const bool occ = argc > 3 && std::string(argv[3]) == "occ";
     std::vector<Case> cases = {
         mk<1, 0, kAuxNt>("nt loads"),           mk<2, 0, kAuxNt>("nt loads"),
         mk<4, 0, kAuxNt>("nt loads"),           mk<8, 0, kAuxNt>("nt loads"),
@@ -100,6 +106,14 @@ int main(int argc, char **argv) {
         mk<4, 1, kAuxNt>("nt loads, wt store"), mk<8, 1, kAuxNt>("nt loads, wt store"),
         mk<8, 0, 0>("plain loads"),             mk<8, 1, 0>("plain loads, wt store"),
     };
+    if (occ) {  // occupancy caps: does a smaller in-flight window per stream lift the many-stream mixes?
+        cases.clear();
+        for (int lds : {0, 10, 20, 27, 32, 40, 64}) {
+            cases.push_back(mk<8, 1, kAuxNt>("nt loads, wt store", lds));
+            cases.push_back(mk<2, 1, kAuxNt>("nt loads, wt store", lds));
+            cases.push_back(mk<8, 0, kAuxNt>("nt loads", lds));
+        }
+    }
     // every case moves the same total: stream bytes C = total / (R + W)
     const size_t max_stream = (total_mib << 20) / 1;  // R = 1, W = 0 needs one stream of the total
     std::vector<std::vector<u4 *>> bufs(sets, std::vector<u4 *>(kMaxR + 1));
