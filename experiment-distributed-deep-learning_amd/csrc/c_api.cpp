@@ -350,7 +350,11 @@ int ddl_set_config(const char *key, long long value) {
         } else if (k == "one_rank_shortcut") c.one_rank_shortcut = value ? 1 : 0;
         else if (k == "pipeline_rounds") c.pipeline_rounds = value ? 1 : 0;
         else if (k == "reference_order") c.reference_order = value ? 1 : 0;
-        else if (k == "capture_forked") c.capture_forked = value ? 1 : 0;
+        else if (k == "capture_mode") {
+            DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT,
+                        "capture_mode must be 0 (serial), 1 (forked streams) or 2 (single-stream DAG)");
+            c.capture_mode = value;
+        } else if (k == "capture_forked") c.capture_mode = value ? 1 : 0;
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
     });
@@ -380,7 +384,8 @@ long long ddl_get_config(const char *key) {
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;
     if (k == "reference_order") return c.reference_order;
-    if (k == "capture_forked") return c.capture_forked;
+    if (k == "capture_mode") return c.capture_mode;
+    if (k == "capture_forked") return c.capture_mode.load() == 1 ? 1 : 0;
     return -1;
 }
 

@@ -51,7 +51,7 @@ uint64_t Config::shared_hash() const {
 }
 
 int log_level() { return (int)config().log_level.load(); }
-bool config_capture_forked() { return config().capture_forked.load() != 0; }
+int config_capture_mode() { return (int)config().capture_mode.load(); }
 
 void log_line(int level, const std::string &msg) {
     static std::mutex mu;

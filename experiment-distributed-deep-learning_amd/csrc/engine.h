@@ -80,10 +80,14 @@ struct Config {
     // one-shot folds in MPICH's order, the ring replaced by the direct schedule at P > 2
     // (RingConfig::ref_order); 0: ring order / left folds (error-bounded against the reference)
     std::atomic<long long> reference_order{1};
-    // inside a hipGraph capture: 1 — the program forks onto the comm / compute streams as it does
-    // eagerly (recv / reduce / send overlap kept in the graph); 0 — posted serially on the
-    // captured stream
-    std::atomic<long long> capture_forked{0};
+    // how a program is posted inside a hipGraph capture: 2 (default) — as a
+    // single-stream DAG: every op on the captured stream with its dependencies set explicitly
+    // from its logical stream (comm / compute of each rank), so the graph keeps the recv / reduce /
+    // send overlap without forked streams; 1 — forked onto the comm / compute streams as eagerly
+    // (crashes hipStreamEndCapture in this HIP runtime once 3+ forked streams cross-wait); 0 —
+    // serially on the captured stream (no overlap). Config key "capture_forked" (1 / 0) is the
+    // r02/r03 spelling of modes 1 / 0.
+    std::atomic<long long> capture_mode{2};
     // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'

@@ -1,6 +1,7 @@
 // executor.cpp — see executor.h.
 #include "executor.h"
 
+#include <algorithm>
 #include <map>
 #include <thread>
 
@@ -243,50 +244,115 @@ void RingExecutor::allgatherv(const void *send, void *recv, const size_t *counts
     run_(dtype, user);
 }
 
+Poster::Mode Poster::mode_for(hipStream_t user) {
+    if (!stream_capturing(user)) return kStreams;
+    const int m = config_capture_mode();
+    return m == 0 ? kSerial : m == 1 ? kStreams : kDag;
+}
+
+Poster::Poster(Mode m, hipStream_t user) : m_(m), user_(user) {
+    if (m_ != kDag) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t *deps = nullptr;
+    size_t nd = 0;
+    DDL_HIP(hipStreamGetCaptureInfo_v2(user_, &cs, &id, &g, &deps, &nd));
+    DDL_REQUIRE(cs == hipStreamCaptureStatusActive, DDL_STATUS_ERROR_UNKNOWN, "DAG posting outside a capture");
+    tail_[user_].assign(deps, deps + nd);
+}
+
+hipStream_t Poster::on(hipStream_t s) {
+    if (m_ == kStreams) return s;
+    if (m_ == kSerial) return user_;
+    std::vector<hipGraphNode_t> &t = tail_[s];
+    DDL_HIP(hipStreamUpdateCaptureDependencies(user_, t.empty() ? nullptr : t.data(), t.size(),
+                                               hipStreamSetCaptureDependencies));
+    return user_;
+}
+
+void Poster::posted(hipStream_t s) {
+    if (m_ != kDag) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t *deps = nullptr;
+    size_t nd = 0;
+    DDL_HIP(hipStreamGetCaptureInfo_v2(user_, &cs, &id, &g, &deps, &nd));
+    tail_[s].assign(deps, deps + nd);
+}
+
+void Poster::record(hipEvent_t e, hipStream_t s) {
+    DDL_TRACE("record ev " << (void *)e << " on " << (void *)s);
+    if (m_ == kStreams) DDL_HIP(hipEventRecord(e, s));
+    else if (m_ == kDag) ev_[e] = tail_[s];
+}
+
+void Poster::wait(hipStream_t s, hipEvent_t e) {
+    DDL_TRACE("wait " << (void *)s << " on ev " << (void *)e);
+    if (m_ == kStreams) {
+        DDL_HIP(hipStreamWaitEvent(s, e, 0));
+    } else if (m_ == kDag) {
+        std::vector<hipGraphNode_t> &t = tail_[s];
+        for (hipGraphNode_t n : ev_[e])
+            if (std::find(t.begin(), t.end(), n) == t.end()) t.push_back(n);
+    }
+}
+
+void Poster::finish() {
+    if (m_ != kDag) return;
+    std::vector<hipGraphNode_t> &t = tail_[user_];
+    DDL_HIP(hipStreamUpdateCaptureDependencies(user_, t.empty() ? nullptr : t.data(), t.size(),
+                                               hipStreamSetCaptureDependencies));
+}
+
 void RingExecutor::run_(int dtype, hipStream_t user) {
     if (prog_.ticks.empty()) return;
     DDL_TRACE("executor rank " << rank_ << "/" << size_ << " run: " << prog_.ticks.size() << " ticks, user " << (void *)user);
-    // Inside a graph capture the ticks are posted in order on the captured stream itself (every
-    // dependency of the program points backwards in tick order, so stream order implies it).
-    // Posted on the forked comm / compute streams, the program made hipStreamEndCapture segfault
-    // in the HIP runtime torch loads (7.0.2; tools/graph_probe.py), although every fork / join
-    // shape it uses passes alone (tools/capture_patterns.hip) — DESIGN §9. A graph is for
-    // latency-bound buckets, where the reduce / exchange overlap inside one call buys little.
+    // Eagerly the program forks from the caller's stream onto the comm / compute streams and joins
+    // back. Inside a graph capture the Poster turns the same posting into a single-stream DAG
+    // (default), forked streams, or a serial order on the captured stream (config capture_mode;
+    // executor.h).
     const bool capturing = stream_capturing(user);
-    const bool serial = capturing && !config_capture_forked();
     DDL_REQUIRE(!capturing || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
                 "this communicator's transport synchronises the host and cannot be captured into a graph");
+    Poster p(Poster::mode_for(user), user);
     const bool timing = timing_ && !capturing;
-    hipStream_t comm = serial ? user : res_.comm, compute = serial ? user : res_.compute;
+    const hipStream_t comm = res_.comm, compute = res_.compute;
     res_.ensure_events(prog_.ticks.size());
-    if (!serial) {
-        DDL_HIP(hipEventRecord(res_.fork_ev, user));
-        DDL_HIP(hipStreamWaitEvent(comm, res_.fork_ev, 0));
-        DDL_HIP(hipStreamWaitEvent(compute, res_.fork_ev, 0));
-        if (capturing) {  // no event recorded on a forked stream before its first node (common.h)
-            launch_capture_anchor(comm);
-            launch_capture_anchor(compute);
-        }
+    p.record(res_.fork_ev, user);
+    p.wait(comm, res_.fork_ev);
+    p.wait(compute, res_.fork_ev);
+    if (capturing && p.mode() == Poster::kStreams) {  // no event recorded on a forked stream before its first node (common.h)
+        launch_capture_anchor(comm);
+        launch_capture_anchor(compute);
     }
     const int drop = g_drop_wait_tick.load();
     for (size_t t = 0; t < prog_.ticks.size(); ++t) {
         const Tick &tk = prog_.ticks[t];
-        if (tk.wait_reduce >= 0 && !serial && (int)t != drop) {
+        if (tk.wait_reduce >= 0 && (int)t != drop) {
             int w = last_reduce_at_or_before(prog_, tk.wait_reduce);
-            if (w >= 0) DDL_HIP(hipStreamWaitEvent(comm, res_.red_ev[w], 0));
+            if (w >= 0) p.wait(comm, res_.red_ev[w]);
         }
-        for (const CopyOp &c : tk.copies) DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, comm));
+        for (const CopyOp &c : tk.copies) {
+            DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, p.on(comm)));
+            p.posted(comm);
+        }
         if (transport_) {
-            if (tk.gather.bytes) transport_->allgather(tk.gather, comm);
-            transport_->group(tk.ops, comm);
+            if (tk.gather.bytes) {
+                transport_->allgather(tk.gather, p.on(comm));
+                p.posted(comm);
+            }
+            if (!tk.ops.empty()) {
+                transport_->group(tk.ops, p.on(comm));
+                p.posted(comm);
+            }
         } else {
             DDL_REQUIRE(tk.ops.empty() && !tk.gather.bytes, DDL_STATUS_ERROR_UNKNOWN, "no transport for a multi-rank program");
         }
         if (tk.has_reduce) {
-            if (!serial) {
-                DDL_HIP(hipEventRecord(res_.comm_ev[t], comm));
-                DDL_HIP(hipStreamWaitEvent(compute, res_.comm_ev[t], 0));
-            }
+            p.record(res_.comm_ev[t], comm);
+            p.wait(compute, res_.comm_ev[t]);
             std::pair<hipEvent_t, hipEvent_t> tp{nullptr, nullptr};
             if (timing) {
                 if (free_pairs_.empty()) {
@@ -298,23 +364,24 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
                 }
                 DDL_HIP(hipEventRecord(tp.first, compute));
             }
-            const double bytes = launch_tick_reduce(tk, dtype, compute);
+            const double bytes = launch_tick_reduce(tk, dtype, p.on(compute));
+            p.posted(compute);
             if (timing) {
                 DDL_HIP(hipEventRecord(tp.second, compute));
                 timed_.push_back(tp);
                 timed_bytes_.push_back(bytes);
             }
-            if (!serial) DDL_HIP(hipEventRecord(res_.red_ev[t], compute));
+            p.record(res_.red_ev[t], compute);
         }
     }
-    if (serial) return;
     // join both forked streams back into the caller's: every stream a capture forked must be
     // joined before it ends (the compute stream of a program with no reduce — broadcast,
     // allgatherv — only waited on the fork)
-    DDL_HIP(hipEventRecord(res_.join_ev, comm));
-    DDL_HIP(hipEventRecord(res_.join_cp_ev, compute));
-    DDL_HIP(hipStreamWaitEvent(user, res_.join_ev, 0));
-    DDL_HIP(hipStreamWaitEvent(user, res_.join_cp_ev, 0));
+    p.record(res_.join_ev, comm);
+    p.record(res_.join_cp_ev, compute);
+    p.wait(user, res_.join_ev);
+    p.wait(user, res_.join_cp_ev);
+    p.finish();
 }
 
 ThreadFabric::~ThreadFabric() {
@@ -558,36 +625,33 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         loop_ev_.push_back(e);
     }
-    // under a graph capture every rank's work goes on the captured stream in posting order
-    // (as RingExecutor::run_ does): event waits are then implied by stream order
-    const bool serial = stream_capturing(user) && !config_capture_forked();
-    auto comm = [&](int r) { return serial ? user : res_[r]->comm; };
-    auto compute = [&](int r) { return serial ? user : res_[r]->compute; };
-    auto loop_stream = [&] { return serial ? user : loop_stream_; };
-    auto record = [&](hipEvent_t e, hipStream_t st) {
-        DDL_TRACE("record ev " << (void *)e << " on " << (void *)st);
-        if (!serial) DDL_HIP(hipEventRecord(e, st));
+    // posted through a Poster as RingExecutor::run_ is: real streams eagerly; inside a capture a
+    // single-stream DAG (default), forked streams or the serial order (config capture_mode)
+    const bool capturing = stream_capturing(user);
+    Poster p(Poster::mode_for(user), user);
+    auto comm = [&](int r) { return res_[r]->comm; };
+    auto compute = [&](int r) { return res_[r]->compute; };
+    auto record = [&](hipEvent_t e, hipStream_t st) { p.record(e, st); };
+    auto wait = [&](hipStream_t st, hipEvent_t e) { p.wait(st, e); };
+    auto copy = [&](void *dst, const void *src, size_t bytes, hipStream_t st) {
+        DDL_TRACE("copy " << bytes << " B on " << (void *)st);
+        DDL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, p.on(st)));
+        p.posted(st);
     };
-    auto wait = [&](hipStream_t st, hipEvent_t e) {
-        DDL_TRACE("wait " << (void *)st << " on ev " << (void *)e);
-        if (!serial) DDL_HIP(hipStreamWaitEvent(st, e, 0));
-    };
-    DDL_TRACE("local world run: P " << P_ << " ticks " << T << " serial " << serial << " user " << (void *)user);
+    DDL_TRACE("local world run: P " << P_ << " ticks " << T << " mode " << (int)p.mode() << " user " << (void *)user);
     hipEvent_t fork = res_[0]->fork_ev;
     record(fork, user);
     for (int r = 0; r < P_; ++r) {
         wait(comm(r), fork);
         wait(compute(r), fork);
     }
-    if (!serial && stream_capturing(user)) {  // no event recorded on a forked stream before its first node
+    if (loop_) wait(loop_stream_, fork);
+    if (capturing && p.mode() == Poster::kStreams) {  // no event recorded on a forked stream before its first node
         for (int r = 0; r < P_; ++r) {
             launch_capture_anchor(comm(r));
             launch_capture_anchor(compute(r));
         }
-        if (loop_) {
-            wait(loop_stream(), fork);
-            launch_capture_anchor(loop_stream());
-        }
+        if (loop_) launch_capture_anchor(loop_stream_);
     }
     for (size_t t = 0; t < T; ++t) {
         // 1) each rank's comm stream reaches the tick (after its reduce dependency)
@@ -598,10 +662,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 int w = last_reduce_at_or_before(progs_[r], tk.wait_reduce);
                 if (w >= 0) wait(comm(r), rr.red_ev[w]);
             }
-            for (const CopyOp &c : tk.copies) {
-                DDL_TRACE("copy " << c.bytes << " B on " << (void *)comm(r));
-                DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, comm(r)));
-            }
+            for (const CopyOp &c : tk.copies) copy(c.dst, c.src, c.bytes, comm(r));
             record(rr.pre_ev[t], comm(r));
         }
         // 1b) allgather ticks: rank q's block into every rank's recv at q * bytes, once q has
@@ -620,14 +681,15 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                         pairs.push_back(P2POp{false, 0, 0, dst, g.bytes});
                     } else {
                         wait(comm(r), res_[q]->pre_ev[t]);
-                        DDL_HIP(hipMemcpyAsync(dst, src.send, g.bytes, hipMemcpyDeviceToDevice, comm(r)));
+                        copy(dst, src.send, g.bytes, comm(r));
                     }
                 }
             }
             if (loop_) {
-                for (int r = 0; r < P_; ++r) wait(loop_stream(), res_[r]->pre_ev[t]);
-                loop_->group(pairs, loop_stream());
-                record(loop_ev_[t], loop_stream());
+                for (int r = 0; r < P_; ++r) wait(loop_stream_, res_[r]->pre_ev[t]);
+                loop_->group(pairs, p.on(loop_stream_));
+                p.posted(loop_stream_);
+                record(loop_ev_[t], loop_stream_);
                 for (int r = 0; r < P_; ++r) wait(comm(r), loop_ev_[t]);
                 loop_pairs_ += (long long)pairs.size() / 2;
             } else {
@@ -652,9 +714,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                 }
             }
             if (!pairs.empty()) {
-                for (int r = 0; r < P_; ++r) wait(loop_stream(), res_[r]->pre_ev[t]);
-                loop_->group(pairs, loop_stream());
-                record(loop_ev_[t], loop_stream());
+                for (int r = 0; r < P_; ++r) wait(loop_stream_, res_[r]->pre_ev[t]);
+                loop_->group(pairs, p.on(loop_stream_));
+                p.posted(loop_stream_);
+                record(loop_ev_[t], loop_stream_);
                 for (int r = 0; r < P_; ++r) wait(comm(r), loop_ev_[t]);
                 loop_pairs_ += (long long)pairs.size() / 2;
             }
@@ -670,7 +733,8 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                     const P2POp &match = match_(r, t, op, seen);
                     wait(comm(r), res_[op.peer]->pre_ev[t]);
                     DDL_TRACE("recv copy " << op.bytes << " B on " << (void *)comm(r));
-                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, comm(r)));
+                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, p.on(comm(r))));
+                    p.posted(comm(r));
                 }
                 record(rr.post_ev[t], comm(r));
             }
@@ -688,7 +752,8 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             record(rr.comm_ev[t], comm(r));
             wait(compute(r), rr.comm_ev[t]);
             DDL_TRACE("reduce launch on " << (void *)compute(r));
-            launch_tick_reduce(tk, dtype, compute(r));
+            launch_tick_reduce(tk, dtype, p.on(compute(r)));
+            p.posted(compute(r));
             record(rr.red_ev[t], compute(r));
         }
     }
@@ -699,9 +764,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         wait(user, res_[r]->join_cp_ev);
     }
     if (loop_) {  // the transport stream too (its groups are joined through the comm streams already)
-        record(loop_join_, loop_stream());
+        record(loop_join_, loop_stream_);
         wait(user, loop_join_);
     }
+    p.finish();
 }
 
 }  // namespace ddl

@@ -39,9 +39,45 @@ public:
 // autotuning — the calls that need those must run once outside the capture first (the same
 // warm-up rule as for any captured workload).
 bool stream_capturing(hipStream_t s);
-// Config "capture_forked": inside a capture, post the program on the forked comm / compute
-// streams as eagerly (1) or serially on the captured stream (0).
-bool config_capture_forked();
+// Config "capture_mode": how a program is posted inside a capture — 0 serially on the captured
+// stream, 1 on the forked comm / compute streams as eagerly, 2 as a single-stream DAG (Poster).
+int config_capture_mode();
+
+// Posts a program's ops on its logical streams (each rank's comm / compute stream, a transport
+// stream) with event records and waits between them, in one of three ways:
+//  * kStreams — on the real streams: record / wait are hipEventRecord / hipStreamWaitEvent (eager
+//    calls, and capture_mode 1);
+//  * kSerial — every op on the caller's stream in posting order, records and waits dropped
+//    (stream order implies every dependency: they all point backwards; capture_mode 0);
+//  * kDag — inside a capture: every op on the captured stream, whose capture dependency set is
+//    replaced right before the op by the op's logical stream's node set
+//    (hipStreamUpdateCaptureDependencies) and read back right after it (the op's terminal nodes,
+//    hipStreamGetCaptureInfo_v2); records copy a logical stream's node set, waits union one in.
+//    The graph gets exactly the forked program's DAG — recv / reduce / send overlap included —
+//    with no forked stream, which sidesteps the runtime's capture defect with three or more
+//    cross-waiting forked streams (capture_mode 2, the default).
+// Use: `X(..., p.on(s)); p.posted(s);` around every op posted on logical stream s.
+class Poster {
+public:
+    enum Mode { kStreams, kSerial, kDag };
+    Poster(Mode m, hipStream_t user);
+    // the mode run_ uses for a call on `user`: kStreams unless `user` is being captured
+    static Mode mode_for(hipStream_t user);
+    Mode mode() const { return m_; }
+    hipStream_t on(hipStream_t s);  // the real stream to post logical stream s's next op on
+    void posted(hipStream_t s);     // after that op (kDag: s's node set = the op's terminal nodes)
+    void record(hipEvent_t e, hipStream_t s);
+    void wait(hipStream_t s, hipEvent_t e);
+    // kDag: leave the captured stream depending on the caller's logical node set (after the
+    // program's joins, every branch); a no-op otherwise
+    void finish();
+
+private:
+    Mode m_;
+    hipStream_t user_;
+    std::map<hipStream_t, std::vector<hipGraphNode_t>> tail_;
+    std::map<hipEvent_t, std::vector<hipGraphNode_t>> ev_;
+};
 
 class RcclTransport : public Transport {
 public:

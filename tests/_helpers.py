@@ -390,3 +390,22 @@ def live_mpich(xs, dt):
         outs = [np.fromfile(os.path.join(d, f'out_{r}.bin'), dtype=xs[0].dtype) for r in range(len(xs))]
     assert all(o.tobytes() == outs[0].tobytes() for o in outs), 'MPICH ranks disagree'
     return outs[0]
+
+
+def hip_runtime():
+    """The HIP runtime torch and the engine already share, bound by soname with RTLD_NOLOAD (a
+    second runtime loaded by file name would be handed torch's streams: tools/graph_probe.py),
+    with the graph-capture entry points' signatures."""
+    vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    hip = ctypes.CDLL('libamdhip64.so.7', mode=os.RTLD_NOLOAD | os.RTLD_NOW)
+    for name, res, args in (('hipStreamBeginCapture', ci, [vp, ci]),
+                            ('hipStreamEndCapture', ci, [vp, ctypes.POINTER(vp)]),
+                            ('hipGraphGetNodes', ci, [vp, vp, ctypes.POINTER(sz)]),
+                            ('hipGraphGetEdges', ci, [vp, vp, vp, ctypes.POINTER(sz)]),
+                            ('hipGraphInstantiate', ci, [ctypes.POINTER(vp), vp, vp, vp, sz]),
+                            ('hipGraphLaunch', ci, [vp, vp]),
+                            ('hipGraphExecDestroy', ci, [vp]),
+                            ('hipGraphDestroy', ci, [vp])):
+        f = getattr(hip, name)
+        f.restype, f.argtypes = res, args
+    return hip

@@ -5,7 +5,10 @@
 //   ./capture_replay <trace file> <flags>
 //     flags: E = replay the same program eagerly first (events / streams used before the capture,
 //            as the engine's are), C = include the copies, K = include the kernels,
-//            1 = events only on a single extra stream per original stream (no change), empty = "-"
+//            1 = events only on a single extra stream per original stream (no change), empty = "-",
+//            D = single-stream DAG posting: every op goes on the origin stream, its dependencies set
+//                explicitly (hipStreamUpdateCaptureDependencies) from the logical stream's node set;
+//                records / waits become node-set bookkeeping (no forked stream at all)
 // The trace's first "local world run" block is the eager call, the second the captured one; the
 // second is replayed (its stream and event handles are mapped to fresh objects).
 #include <hip/hip_runtime.h>
@@ -13,7 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <sstream>
 #include <string>
@@ -127,7 +132,52 @@ int main(int argc, char **argv) {
             if (keep[i]) limit = i + 1;
         if (limit == ops.size()) limit = ops.size() - 1;
     }
+    const bool dag = flags.find('D') != std::string::npos;
+    auto post_dag = [&]() -> int {
+        std::map<std::string, std::vector<hipGraphNode_t>> tail, evn;
+        auto add = [](std::vector<hipGraphNode_t> &a, const std::vector<hipGraphNode_t> &b) {
+            for (hipGraphNode_t x : b)
+                if (std::find(a.begin(), a.end(), x) == a.end()) a.push_back(x);
+        };
+        auto node_op = [&](const std::string &s, const std::function<void()> &fn) -> int {
+            std::vector<hipGraphNode_t> &t = tail[s];
+            CK(hipStreamUpdateCaptureDependencies(o, t.empty() ? nullptr : t.data(), t.size(),
+                                                  hipStreamSetCaptureDependencies));
+            fn();
+            hipStreamCaptureStatus cs;
+            unsigned long long id = 0;
+            hipGraph_t cg = nullptr;
+            const hipGraphNode_t *deps = nullptr;
+            size_t nd = 0;
+            CK(hipStreamGetCaptureInfo_v2(o, &cs, &id, &cg, &deps, &nd));
+            t.assign(deps, deps + nd);
+            return 0;
+        };
+        for (size_t i = 0; i < limit; ++i) {
+            if (!keep[i]) continue;
+            const Op &op = ops[i];
+            switch (op.kind) {
+                case 'r': evn[op.a] = tail[op.b]; break;
+                case 'w': add(tail[op.a], evn[op.b]); break;
+                case 'c':
+                    if (copies && node_op(op.a, [&] { (void)hipMemcpyAsync(buf + n, buf, op.bytes, hipMemcpyDeviceToDevice, o); }))
+                        return 1;
+                    break;
+                case 'k':
+                    if (kernels && node_op(op.a, [&] { hipLaunchKernelGGL(inc, dim3(2), dim3(256), 0, o, buf, 300); }))
+                        return 1;
+                    break;
+            }
+        }
+        std::vector<hipGraphNode_t> all = tail[user];  // join every logical stream into the origin
+        for (auto &kv : tail) add(all, kv.second);
+        CK(hipStreamUpdateCaptureDependencies(o, all.empty() ? nullptr : all.data(), all.size(),
+                                              hipStreamSetCaptureDependencies));
+        std::printf("  dag: %zu logical streams, %zu terminal nodes\n", tail.size(), all.size());
+        return 0;
+    };
     auto post = [&]() -> int {
+        if (dag) return post_dag();
         std::map<std::string, int> touched, anchored;
         for (size_t i = 0; i < limit; ++i) {
             if (!keep[i]) continue;
@@ -183,7 +233,7 @@ int main(int argc, char **argv) {
         std::printf("replay '%s': ok (%zu nodes)\n", flags.c_str(), nodes);
         return 0;
     }
-    if (eager) {
+    if (eager && !dag) {
         if (post()) return 1;
         CK(hipDeviceSynchronize());
         std::printf("  eager replay ok\n");
