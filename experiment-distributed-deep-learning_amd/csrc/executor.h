@@ -48,14 +48,15 @@ int config_capture_mode();
 //  * kStreams — on the real streams: record / wait are hipEventRecord / hipStreamWaitEvent (eager
 //    calls, and capture_mode 1);
 //  * kSerial — every op on the caller's stream in posting order, records and waits dropped
-//    (stream order implies every dependency: they all point backwards; capture_mode 0);
+//    (stream order implies every dependency: they all point backwards; capture_mode 0, the
+//    default: the chain replays fastest in HIP 7.0's graph executor);
 //  * kDag — inside a capture: every op on the captured stream, whose capture dependency set is
 //    replaced right before the op by the op's logical stream's node set
 //    (hipStreamUpdateCaptureDependencies) and read back right after it (the op's terminal nodes,
 //    hipStreamGetCaptureInfo_v2); records copy a logical stream's node set, waits union one in.
 //    The graph gets exactly the forked program's DAG — recv / reduce / send overlap included —
 //    with no forked stream, which sidesteps the runtime's capture defect with three or more
-//    cross-waiting forked streams (capture_mode 2, the default).
+//    cross-waiting forked streams (capture_mode 2).
 // Use: `X(..., p.on(s)); p.posted(s);` around every op posted on logical stream s.
 class Poster {
 public:

@@ -106,15 +106,14 @@ def test_config_roundtrip(lib):
     assert lib.ddl_get_config(b'reference_order') == 1
     # keyed rounds pipelined by default (done() fired by the completion thread)
     assert lib.ddl_get_config(b'pipeline_rounds') == 1
-    # captures post a single-stream DAG by default; capture_forked is the older spelling of 1 / 0
-    assert lib.ddl_get_config(b'capture_mode') == 2
+    # captures post serially by default (2: single-stream DAG); capture_forked spells modes 1 / 0
+    assert lib.ddl_get_config(b'capture_mode') == 0
     assert lib.ddl_get_config(b'capture_forked') == 0
     assert lib.ddl_set_config(b'capture_mode', 3) == 3
     assert lib.ddl_set_config(b'capture_forked', 1) == 0
     assert lib.ddl_get_config(b'capture_mode') == 1 and lib.ddl_get_config(b'capture_forked') == 1
     assert lib.ddl_set_config(b'capture_forked', 0) == 0
     assert lib.ddl_get_config(b'capture_mode') == 0
-    assert lib.ddl_set_config(b'capture_mode', 2) == 0
 
 
 def test_product_does_not_reference_oracle():

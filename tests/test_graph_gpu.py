@@ -3,9 +3,9 @@ stream): one replay of a captured training step runs the engine's kernels and RC
 host work per call — the small-bucket lever the host launch rate sets.
 
 The engine is graph-safe by construction (executor.cpp `stream_capturing`): under capture it
-enqueues only stream work — by default as a single-stream DAG (capture_mode 2: every op on the
-captured stream, its dependencies set from its logical comm / compute stream, so the graph keeps
-the recv / reduce / send overlap), or serially (capture_mode 0) — takes the size class's tuned
+enqueues only stream work — serially on the captured stream by default (capture_mode 0), or as a
+single-stream DAG (capture_mode 2: every op on the captured stream, its dependencies set from its
+logical comm / compute stream, so the graph keeps the recv / reduce / send overlap) — takes the size class's tuned
 schedule or the configured one without tuning, and
 refuses — loudly, before enqueueing anything — to grow its staging buffer or to capture a
 transport that synchronises the host. Warm up once outside the capture, as for any captured
@@ -102,7 +102,7 @@ TORCH_DT = {DT_FLOAT: torch.float32, DT_DOUBLE: torch.float64, DT_INT32: torch.i
 def test_rccl_allreduce_graph_replay(loop, oracle, gpu, P, dt, algo, mode):
     """P virtual ranks' allreduce, moves through RCCL, captured once and replayed on fresh
     inputs: every rank equals MPICH's order bit for bit on both sides of the 2048-byte switch,
-    out of place and in place; posted as a single-stream DAG (the default) and serially."""
+    out of place and in place; posted as a single-stream DAG and serially (the default)."""
     lib = loop
     s = torch.cuda.Stream()
     with config(lib, algo=algo, reference_order=1, tune=0, slice_bytes=64 << 10, capture_mode=mode):

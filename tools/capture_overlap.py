@@ -19,9 +19,38 @@ from _helpers import hip_runtime  # noqa: E402
 from test_graph_gpu import _graph_shape  # noqa: E402
 
 
+def transitive_reduction(hip, g):
+    """Removes every edge a -> b of g that another path a -> ... -> b implies."""
+    vp = ctypes.c_void_p
+    ne = ctypes.c_size_t(0)
+    assert hip.hipGraphGetEdges(g, None, None, ctypes.byref(ne)) == 0
+    src, dst = (vp * ne.value)(), (vp * ne.value)()
+    assert hip.hipGraphGetEdges(g, src, dst, ctypes.byref(ne)) == 0
+    succ = {}
+    for a, b in zip(src, dst):
+        succ.setdefault(a, set()).add(b)
+    reach = {}
+
+    def reachable(a):  # nodes reachable from a by a path of >= 1 edge
+        if a not in reach:
+            r = set()
+            for b in succ.get(a, ()):
+                r.add(b)
+                r |= reachable(b)
+            reach[a] = r
+        return reach[a]
+    sys.setrecursionlimit(100000)
+    drop = [(a, b) for a in succ for b in succ[a] if any(b in reachable(c) for c in succ[a] if c != b)]
+    if drop:
+        fa, fb = (vp * len(drop))(*[a for a, _ in drop]), (vp * len(drop))(*[b for _, b in drop])
+        assert hip.hipGraphRemoveDependencies(g, fa, fb, ctypes.c_size_t(len(drop))) == 0
+
+
 def main(world='local', P=4):
     lib = CPPBackend.c_api()
     hip = hip_runtime()
+    f = hip.hipGraphRemoveDependencies
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     if world == 'rccl':
@@ -52,9 +81,9 @@ def main(world='local', P=4):
             eager = min(eager, (time.perf_counter() - t0) / 10)
         print(json.dumps({'world': world, 'P': P, 'bytes_per_rank': nbytes, 'slice_bytes': slice_bytes,
                           'eager_us': round(eager * 1e6, 1)}), flush=True)
-        for mode in (0, 2):
+        for mode in (0, 2, 3):  # 3: the DAG with its transitively implied edges removed before instantiation
             for k, v in (('algo', 1), ('reference_order', 1), ('tune', 0), ('slice_bytes', slice_bytes),
-                         ('capture_mode', mode)):
+                         ('capture_mode', min(mode, 2))):
                 assert lib.ddl_set_config(k.encode(), v) == 0
             assert call() == 0, lib.ddl_last_error()
             torch.cuda.synchronize()
@@ -62,6 +91,8 @@ def main(world='local', P=4):
             rc = call()
             g = ctypes.c_void_p()
             assert hip.hipStreamEndCapture(st, ctypes.byref(g)) == 0 and rc == 0
+            if mode == 3:
+                transitive_reduction(hip, g)
             nodes, edges, chain = _graph_shape(hip, g)
             x = ctypes.c_void_p()
             assert hip.hipGraphInstantiate(ctypes.byref(x), g, None, None, ctypes.c_size_t(0)) == 0
@@ -77,7 +108,7 @@ def main(world='local', P=4):
             hip.hipGraphExecDestroy(x)
             hip.hipGraphDestroy(g)
             print(json.dumps({'world': world, 'P': P, 'bytes_per_rank': nbytes, 'slice_bytes': slice_bytes,
-                              'capture_mode': ('serial', None, 'dag')[mode], 'nodes': nodes, 'edges': edges,
+                              'capture_mode': ('serial', None, 'dag', 'dag_reduced')[mode], 'nodes': nodes, 'edges': edges,
                               'longest_chain': chain, 'replay_us': round(best * 1e6, 1)}), flush=True)
     if world == 'rccl':
         assert lib.ddl_rccl_loopback_finalize() == 0
