@@ -601,11 +601,19 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
         step()
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
+        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us')
+        tl0 = [lib.ddl_get_config(kk) for kk in tl_keys]
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         dt = (time.perf_counter() - t0) / steps
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
+        # the engine thread's timeline per step: packing chunks into the pinned slots, waiting
+        # for a slot's DMA / device work, unpacking staged results; the rest is negotiation,
+        # planning and posting
+        tl = [(lib.ddl_get_config(kk) - v) / steps / 1e3 for kk, v in zip(tl_keys, tl0)]
+        timeline = {'pack_ms': round(tl[0], 3), 'slot_wait_ms': round(tl[1], 3), 'unpack_ms': round(tl[2], 3),
+                    'other_ms': round(dt * 1e3 - sum(tl), 3)}
         registered = {'host_registered_bytes': int(lib.ddl_get_config(b'host_registered_bytes')),
                       'host_register_failures': int(lib.ddl_get_config(b'host_register_failures'))}
     finally:
@@ -618,7 +626,7 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
     return {'buckets': k, 'total_bytes': int(total), 'ms': round(dt * 1e3, 3), 'bucket_GiBs': round(total / GiB / dt, 2),
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
-            'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path,
+            'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path, 'engine_thread': timeline,
             'host_direct_dma': int(lib.ddl_get_config(b'host_direct_dma')) if 'host_direct_dma' not in settings
             else settings['host_direct_dma'],
             'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},

@@ -61,6 +61,13 @@ struct Config {
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
     // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};
+    // read-only statistics of the keyed host plans' timeline (ddl_get_config, microseconds summed
+    // over every plan of the process): the engine thread packing chunks into pinned slots (host
+    // memcpy, with the copy threads), waiting for a slot whose earlier DMA / device work is still
+    // in flight, and unpacking staged results
+    std::atomic<long long> host_pack_us{0};
+    std::atomic<long long> host_wait_us{0};
+    std::atomic<long long> host_unpack_us{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};

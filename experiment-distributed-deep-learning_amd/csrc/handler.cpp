@@ -775,23 +775,45 @@ size_t RequestHandler::host_slots_(size_t total) {
     return chunk;
 }
 
+CopyPool &RequestHandler::pool_for_config_() {
+    // rebuilt when the setting changed (only the engine thread runs host plans, so no plan is
+    // using the old pool here); r02's thread-count sweep ran every setting on the first pool
+    const int want = (int)std::max(0ll, config().host_copy_threads.load());
+    if (!pool_ || pool_->threads() != want) {
+        pool_.reset();
+        pool_.reset(new CopyPool(want));
+    }
+    return *pool_;
+}
+
 void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
                                   const std::function<void(void *, size_t)> &coll, bool padded, bool device_unpack) {
     std::vector<size_t> starts;
     const size_t total = seg_starts(segs, padded || device_unpack, starts);
     if (total == 0) return;
     const size_t chunk = host_slots_(total);
-    if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
+    pool_for_config_();
     if (device_unpack) config().host_zero_copy_plans.fetch_add(1);
     const size_t nchunks = (total + chunk - 1) / chunk;
     std::vector<CopyPool::Piece> pieces;
+    // timeline statistics (config "host_pack_us" / "host_wait_us" / "host_unpack_us"): where the
+    // engine thread spends a host plan — packing chunks, waiting for a slot's DMA / device work,
+    // unpacking chunks
+    using clk = std::chrono::steady_clock;
+    auto us_since = [](clk::time_point t0) {
+        return (long long)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count();
+    };
     auto unpack = [&](size_t j) {
         const int k = (int)(j % kHostSlots);
+        clk::time_point t0 = clk::now();
         DDL_HIP(hipEventSynchronize(hev_[3 * k + 2]));  // D2H of chunk j landed
+        config().host_wait_us.fetch_add(us_since(t0));
+        t0 = clk::now();
         const size_t off = j * chunk;
         pieces.clear();
         host_pieces_(segs, starts, off, std::min(chunk, total - off), static_cast<char *>(pin_[k]), false, pieces);
         pool_->run(pieces);
+        config().host_unpack_us.fetch_add(us_since(t0));
     };
     std::vector<void *> dst;
     std::vector<size_t> len;
@@ -815,7 +837,10 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         if (upload) {
             // the pinned slot's last upload must have left it (device-unpack plans do not wait
             // for their D2H on the host)
+            clk::time_point t0 = clk::now();
             if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
+            config().host_wait_us.fetch_add(us_since(t0));
+            t0 = clk::now();
             if (!direct.empty()) {
                 // pieces of pinned inputs (segments flagged in `direct`) go straight from the
                 // tensor to the device slot by DMA, no host memcpy; the others are packed into
@@ -853,6 +878,7 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
                 pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
                 DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
             }
+            config().host_pack_us.fetch_add(us_since(t0));
         }
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
@@ -1024,8 +1050,7 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     std::vector<CopyPool::Piece> pieces;
                     for (const HostSeg &sg : segs)
                         if (sg.src != sg.dst) pieces.push_back(CopyPool::Piece{sg.dst, sg.src, sg.bytes});
-                    if (!pool_) pool_.reset(new CopyPool((int)std::max(0ll, config().host_copy_threads.load())));
-                    pool_->run(pieces);
+                    pool_for_config_().run(pieces);
                 } else {
                     // chunks of the padded stream either way, so ranks that differ in which
                     // outputs are pinned still issue the same collectives

@@ -85,6 +85,7 @@ public:
     CopyPool &operator=(const CopyPool &) = delete;
     // Copies every piece; returns when all are done (the caller's thread takes a share).
     void run(const std::vector<Piece> &pieces);
+    int threads() const { return (int)threads_.size(); }
 
 private:
     void worker_();
@@ -251,6 +252,7 @@ private:
     // fills every segment's ddst; false unless all of them are mapped
     static bool mapped_host_dsts_(std::vector<HostSeg> &segs);
     size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
+    CopyPool &pool_for_config_();     // the copy threads, rebuilt when host_copy_threads changed
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);

@@ -390,6 +390,8 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
             outs = [torch.empty_like(x, pin_memory=True) for x in xs]
         dev = torch.randn(1234, device='cuda')
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
+        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us')
+        tl0 = [lib.ddl_get_config(k) for k in tl_keys]
         hs = allreduce_async_batch(xs + [dev], [f'hk_{i}' for i in range(len(xs))] + ['hk_dev'], world,
                                    outputs=outs + [torch.empty_like(dev)])
         for h, k in zip(hs, keep):
@@ -401,6 +403,11 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
         device_unpacked = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
         assert device_unpacked == {'pageable': 0, 'pinned': 6, 'pinned_outputs': 6, 'mixed': 5,
                                    'pinned_misaligned': 5, 'pinned_direct': 6, 'registered': 6}[memory]
+        # the engine thread's timeline statistics moved: chunks were packed, and unpacked on the
+        # host when every plan was staged back (microseconds: a tiny staged plan may read 0)
+        pack, wait, unpack = [lib.ddl_get_config(k) - v for k, v in zip(tl_keys, tl0)]
+        assert pack > 0 and wait >= 0 and unpack >= 0, (pack, wait, unpack)
+        assert unpack > 0 or device_unpacked > 0, (memory, unpack)
         t = torch.arange(100_003, dtype=torch.float64)
         assert torch.equal(broadcast_async(t, 'hk_b', 0, world).wait(timeout=60), t)
     finally:

@@ -17,12 +17,15 @@ def main():
     torch.cuda.set_device(0)
     lib = CPPBackend.c_api()
     comm = Communicator.world()
-    for threads, chunk in ((0, 32), (3, 32), (7, 32), (15, 32), (15, 16), (15, 64), (23, 32)):
-        check(lib.ddl_set_config(b'host_copy_threads', threads), 'cfg')
-        check(lib.ddl_set_config(b'host_chunk_bytes', chunk << 20), 'cfg')
-        r = bench.keyed_host_c5(lib, comm, steps=2)
-        print(json.dumps({'host_copy_threads': threads, 'chunk_MiB': chunk, 'ms': r['ms'], 'GiBs': r['bucket_GiBs']}),
-              flush=True)
+    # (r03: the copy pool is rebuilt when host_copy_threads changes — r02's sweep ran every
+    # setting on the pool built for the first one)
+    for pinned in (True, False):
+        for threads, chunk in ((0, 32), (3, 32), (7, 32), (11, 32), (15, 32), (15, 16), (15, 64)):
+            check(lib.ddl_set_config(b'host_copy_threads', threads), 'cfg')
+            check(lib.ddl_set_config(b'host_chunk_bytes', chunk << 20), 'cfg')
+            r = bench.keyed_host_c5(lib, comm, steps=3, pinned=pinned)
+            print(json.dumps({'pinned': pinned, 'host_copy_threads': threads, 'chunk_MiB': chunk, 'ms': r['ms'],
+                              'GiBs': r['bucket_GiBs'], 'engine_thread': r['engine_thread']}), flush=True)
 
 
 if __name__ == '__main__':
