@@ -118,21 +118,48 @@ CopyPool::~CopyPool() {
 
 void CopyPool::worker_() {
     for (;;) {
-        std::vector<Piece> work;
+        std::function<void()> task;
         {
             std::unique_lock<std::mutex> lk(mu_);
             cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
             if (stop_ && queue_.empty()) return;
-            work.swap(queue_.back());
+            task = std::move(queue_.back());
             queue_.pop_back();
         }
-        for (const Piece &p : work) std::memcpy(p.dst, p.src, p.bytes);
+        task();
         {
             std::lock_guard<std::mutex> g(mu_);
             --outstanding_;
         }
         done_cv_.notify_all();
     }
+}
+
+void CopyPool::submit_and_wait_(std::vector<std::function<void()>> &tasks) {
+    if (tasks.empty()) return;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (size_t i = 1; i < tasks.size(); ++i) queue_.push_back(std::move(tasks[i]));
+        outstanding_ += tasks.size() - 1;
+    }
+    cv_.notify_all();
+    tasks[0]();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return outstanding_ == 0; });
+}
+
+void CopyPool::parallel(size_t n, const std::function<void(size_t, size_t)> &fn) {
+    const size_t T = std::min(threads_.size() + 1, n);
+    if (T <= 1) {
+        if (n) fn(0, n);
+        return;
+    }
+    std::vector<std::function<void()>> tasks;
+    for (size_t t = 0; t < T; ++t) {
+        const size_t lo = n * t / T, hi = n * (t + 1) / T;
+        tasks.push_back([&fn, lo, hi] { fn(lo, hi); });
+    }
+    submit_and_wait_(tasks);
 }
 
 void CopyPool::run(const std::vector<Piece> &pieces) {
@@ -161,16 +188,12 @@ void CopyPool::run(const std::vector<Piece> &pieces) {
             room -= n;
         }
     }
-    std::vector<Piece> mine = std::move(shares[0]);
-    {
-        std::lock_guard<std::mutex> g(mu_);
-        for (size_t i = 1; i < shares.size(); ++i) queue_.push_back(std::move(shares[i]));
-        outstanding_ += shares.size() - 1;
-    }
-    cv_.notify_all();
-    for (const Piece &p : mine) std::memcpy(p.dst, p.src, p.bytes);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return outstanding_ == 0; });
+    std::vector<std::function<void()>> tasks;
+    for (auto &sh : shares)
+        tasks.push_back([work = std::move(sh)] {
+            for (const Piece &p : work) std::memcpy(p.dst, p.src, p.bytes);
+        });
+    submit_and_wait_(tasks);
 }
 
 std::shared_ptr<ControlChannel> &standalone_control() {
@@ -742,9 +765,15 @@ bool mapped_host_range(const void *p, size_t bytes, char **alias = nullptr) {
 }  // namespace
 
 bool RequestHandler::mapped_host_dsts_(std::vector<HostSeg> &segs) {
-    for (HostSeg &sg : segs)
-        if (!mapped_host_range(sg.dst, sg.bytes, &sg.ddst)) return false;
-    return true;
+    if (segs.empty()) return true;
+    // the first query alone: a pageable output (the common staged case) answers in one call
+    if (!mapped_host_range(segs[0].dst, segs[0].bytes, &segs[0].ddst)) return false;
+    std::atomic<bool> all{true};
+    pool_for_config_().parallel(segs.size() - 1, [&](size_t lo, size_t hi) {
+        for (size_t i = lo + 1; i < hi + 1 && all.load(std::memory_order_relaxed); ++i)
+            if (!mapped_host_range(segs[i].dst, segs[i].bytes, &segs[i].ddst)) all = false;
+    });
+    return all.load();
 }
 
 size_t RequestHandler::host_slots_(size_t total) {

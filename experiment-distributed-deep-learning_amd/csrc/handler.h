@@ -85,14 +85,18 @@ public:
     CopyPool &operator=(const CopyPool &) = delete;
     // Copies every piece; returns when all are done (the caller's thread takes a share).
     void run(const std::vector<Piece> &pieces);
+    // fn(lo, hi) over [0, n) cut into one range per thread (the caller's thread takes the first);
+    // returns when every range is done
+    void parallel(size_t n, const std::function<void(size_t, size_t)> &fn);
     int threads() const { return (int)threads_.size(); }
 
 private:
     void worker_();
+    void submit_and_wait_(std::vector<std::function<void()>> &tasks);  // tasks[0] on the caller
     std::vector<std::thread> threads_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    std::vector<std::vector<Piece>> queue_;
+    std::vector<std::function<void()>> queue_;
     size_t outstanding_ = 0;
     bool stop_ = false;
 };
@@ -250,7 +254,8 @@ private:
     // true when every segment's destination range is 16-byte-aligned pinned host memory that the
     // device reaches at the same address, inside one allocation
     // fills every segment's ddst; false unless all of them are mapped
-    static bool mapped_host_dsts_(std::vector<HostSeg> &segs);
+    // (the queries of a plan's 4096 tensors run on the copy threads: ~3 HIP calls each)
+    bool mapped_host_dsts_(std::vector<HostSeg> &segs);
     size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
     CopyPool &pool_for_config_();     // the copy threads, rebuilt when host_copy_threads changed
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
