@@ -129,8 +129,13 @@ int ddl_is_initialized(void);
  * are hipHostRegister'ed once and the registrations kept, least recently used out past this many
  * bytes, so repeated allreduce(cpu_tensor) calls take the pinned paths — the caller keeps those
  * tensors allocated while cached; setting it to 0 unregisters every cached range at once, after
- * ddl_wait_all), "capture_forked" (0, default: inside a hipGraph capture the program is posted
- * serially on the captured stream; 1: on the forked comm / compute streams — see DESIGN §9),
+ * ddl_wait_all), the read-only timeline of keyed host plans "host_pack_us" / "host_wait_us" /
+ * "host_unpack_us" (microseconds the engine thread spent packing chunks, waiting for a pinned
+ * slot's DMA / device work, unpacking staged results), "capture_mode" (0, default: inside a
+ * hipGraph capture the program is posted serially on the captured stream — one chain; 2: as a
+ * single-stream DAG, every op on the captured stream with its dependencies set explicitly, which
+ * keeps the recv / reduce / send overlap in the graph; 1: on the forked comm / compute streams —
+ * DESIGN §9; "capture_forked" 1 / 0 is the older spelling of modes 1 / 0),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "pipeline_rounds" (1,
