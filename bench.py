@@ -271,6 +271,9 @@ def single_gpu(args):
         extra['fold_kernel'] = fold_roofline(lib, dev, sh, S)
         # the fold the reference-order direct schedule runs at P = 8 (MPICH's pre-fold + tree)
         extra['fold_kernel_reference_order'] = fold_roofline(lib, dev, sh, S, order=1)
+        # A/B: the same chunk in the tile form (every workgroup reads one tile of all 8 inputs at
+        # once) instead of the run form (one input at a time over 16 KiB runs)
+        extra['fold_kernel_tile_form'] = fold_roofline(lib, dev, sh, S, form=1)
         # C4's fold: one 16 MiB fp16 bucket at P = 8 -> 2 MiB chunk, 7 received inputs (cache-resident
         # operands, as RCCL has just written them)
         extra['fold_kernel_fp16_c4'] = fold_roofline(lib, dev, sh, 16 << 20, half=True)
@@ -324,15 +327,19 @@ def single_gpu(args):
     emit(out)
 
 
-def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False):
-    """k_sumN_tile<float, 7>: out = in + 7 received slices over one P=8 chunk (S/8 fp32), the
-    direct schedule's reduce; algorithmic bytes (nb + 2) * chunk. order 0: left fold; 1: MPICH's
+def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
+    """The N-input fold: out = in + 7 received slices over one P=8 chunk (S/8 fp32), the direct
+    schedule's reduce; algorithmic bytes (nb + 2) * chunk. order 0: left fold; 1: MPICH's
     pre-fold + pairwise tree (reference_order at P = 8). `half`: the fp16 fold of C4 (inputs
-    widened to fp32, one rounding)."""
+    widened to fp32, one rounding). `form` (config fold_form): 0 the engine's choice (k_sumN_run
+    above 8 MiB chunks, k_sumN_tile below), 1 the tile form, 2 the run form."""
     import torch
     from ddl.torch.cpp_backend import check
     es = 2 if half else 4
     n = S // 8 // es
+    run_form = form == 2 or (form == 0 and n * es > (8 << 20))
+    old_form = lib.ddl_get_config(b'fold_form')
+    check(lib.ddl_set_config(b'fold_form', form), 'ddl_set_config fold_form')
     sets = [[torch.rand(n, device=dev).to(torch.float16 if half else torch.float32) for _ in range(nb + 2)]
             for _ in range(2)]  # in, 7 inputs, out
     P = ctypes.c_void_p * nb
@@ -366,13 +373,16 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False):
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
     del graph
+    check(lib.ddl_set_config(b'fold_form', old_form), 'ddl_set_config fold_form')
     byts = (nb + 2) * n * es
-    return {'kernel': f'k_sumN_tile<{"DDL_HALF" if half else "DDL_FLOAT"},{nb},order {order}>', 'chunk_bytes': n * es,
+    kname = 'k_sumN_run' if run_form else 'k_sumN_tile'
+    return {'kernel': f'{kname}<{"DDL_HALF" if half else "DDL_FLOAT"},{nb},order {order}>', 'chunk_bytes': n * es,
             'timing': '20 launches captured into a hipGraph, replayed between HIP events on the replay stream',
             'us': round(best * 1e6, 1),
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
             'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
-            'traffic': (pmc_traffic('fold_fp16_P8_C4_chunk') if half else pmc_traffic('fold_fp32_P8_chunk'))
+            'traffic': (pmc_traffic('fold_fp16_P8_C4_chunk') if half else
+                        pmc_traffic('fold_fp32_P8_chunk_run' if run_form else 'fold_fp32_P8_chunk'))
             if order == 0 and ((S == 256 << 20 and not half) or (S == 16 << 20 and half)) else None}
 
 
@@ -801,7 +811,8 @@ def multi_gpu(args):
         'autotune': tune,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'kernel': (f'k_sumN_tile<float,{world - 1}> ({tune["chosen"]["algo"]} fold)'
+                     'kernel': (f'k_sumN_run / k_sumN_tile<float,{world - 1}> ({tune["chosen"]["algo"]} fold; run form '
+                                f'above 8 MiB slices)'
                                 if tune and tune['chosen']['algo'] != 'ring' else
                                 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
                      'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},

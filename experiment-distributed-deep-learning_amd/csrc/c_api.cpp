@@ -355,6 +355,11 @@ int ddl_set_config(const char *key, long long value) {
                         "capture_mode must be 0 (serial), 1 (forked streams) or 2 (single-stream DAG)");
             c.capture_mode = value;
         } else if (k == "capture_forked") c.capture_mode = value ? 1 : 0;
+        else if (k == "fold_form") {
+            DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT,
+                        "fold_form must be 0 (auto), 1 (tile form) or 2 (run form)");
+            set_fold_form((int)value);
+        }
         else fail(DDL_STATUS_INVALID_ARGUMENT, "unknown config key '" + k + "'");
         c.epoch.fetch_add(1);
     });
@@ -388,6 +393,7 @@ long long ddl_get_config(const char *key) {
     if (k == "pipeline_rounds") return c.pipeline_rounds;
     if (k == "reference_order") return c.reference_order;
     if (k == "capture_mode") return c.capture_mode;
+    if (k == "fold_form") return get_fold_form();
     if (k == "capture_forked") return c.capture_mode.load() == 1 ? 1 : 0;
     return -1;
 }

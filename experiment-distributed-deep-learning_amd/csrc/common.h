@@ -142,6 +142,11 @@ enum ReduceVariant : int {
 };
 int default_variant(size_t bytes);  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2), by bucket size
 int ring_variant();     // reduce-scatter step of the ring
+// Form of the N-input fold (config "fold_form"): 0 auto (the run form above 8 MiB chunks), 1 the
+// tile form always, 2 the run form always (the binomial order is always tiled). Local: it changes
+// no collective's program, only the kernel (the same sums either way).
+void set_fold_form(int form);
+int get_fold_form();
 
 // out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.
 // variant < 0 selects default_variant().

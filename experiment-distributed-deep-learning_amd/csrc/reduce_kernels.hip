@@ -27,6 +27,7 @@
 //     fp32 and rounds once (v_cvt_pk_bf16_f32).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <vector>
 
@@ -323,12 +324,155 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
     }
 }
 
+// ---- run form of the fold (large chunks) ----------------------------------------------------
+// The tile form above has every workgroup read one 2 KiB tile of all NB + 1 inputs at once, so
+// the chip streams NB + 2 address streams in lock step — and HBM delivers less the more streams
+// are live (tools/stream_mix.hip, DESIGN §5.2: 6.1 TB/s for a 9-stream 8:1 mix). Here a
+// workgroup owns kRunTiles consecutive tiles (a 16 KiB run of every input) and walks the inputs
+// one at a time: kRunTiles loads per lane from input k in flight, folded in, then input k + 1 —
+// each workgroup streams one input at a time in 16 KiB runs (6.6-6.7 TB/s for the same mix in the
+// harness). The addition order is the same as fold_values': the MPICH tree is evaluated depth
+// first over its leaves (left subtree, right subtree, left + right), so at most log2(pof2) + 1
+// partial sums are live; the left fold (and every half type, in fp32) is one running sum.
+constexpr int kRunTiles = 8;
+constexpr uint64_t kRunVec = (uint64_t)kFoldThreads * kRunTiles;  // 16-byte vectors per run
+
+template <int DT>
+struct RunVec {  // one lane's kRunTiles vectors of one input, widened to the accumulator type
+    using A = Acc<DT>;
+    using S = typename Add<DT>::S;
+    static constexpr int V = 16 / sizeof(S);
+    typename A::T e[kRunTiles][V];
+};
+
+// loads input j (0: t.a, j: t.b[j - 1]) of this workgroup's run into x
+template <int DT, int AUX>
+__device__ __forceinline__ void run_load(RunVec<DT> &x, const SegTableN &t, int j, uint64_t base, int bytes, int off) {
+    using S = typename Add<DT>::S;
+    constexpr int V = RunVec<DT>::V;
+    const u32x4 *src = static_cast<const u32x4 *>(j == 0 ? t.a : t.b[j - 1]) + base;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(src), 0, bytes, kRsrcWord3);
+    u32x4 raw[kRunTiles];
+#pragma unroll
+    for (int u = 0; u < kRunTiles; ++u)
+        raw[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + u * kFoldThreads * 16, 0, AUX);
+#pragma unroll
+    for (int u = 0; u < kRunTiles; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) x.e[u][e] = Acc<DT>::widen(reinterpret_cast<const S *>(&raw[u])[e]);
+}
+
+template <int DT>
+__device__ __forceinline__ void run_add(RunVec<DT> &a, const RunVec<DT> &b) {  // a = a + b
+#pragma unroll
+    for (int u = 0; u < kRunTiles; ++u)
+#pragma unroll
+        for (int e = 0; e < RunVec<DT>::V; ++e) a.e[u][e] = Acc<DT>::add(a.e[u][e], b.e[u][e]);
+}
+
+// MPICH's tree over leaves [LO, HI) of K inputs (pof2 leaves; leaf l < rem is x_2l + x_2l+1,
+// leaf l >= rem is x_l+rem), evaluated depth first into `out`
+template <int DT, int K, int LO, int HI, int AUX>
+__device__ __forceinline__ void run_tree(RunVec<DT> &out, const SegTableN &t, uint64_t base, int bytes, int off) {
+    constexpr int pof2 = K >= 16 ? 16 : K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
+    constexpr int rem = K - pof2;
+    if constexpr (HI - LO == 1) {
+        if constexpr (LO < rem) {
+            run_load<DT, AUX>(out, t, 2 * LO, base, bytes, off);
+            RunVec<DT> y;
+            run_load<DT, AUX>(y, t, 2 * LO + 1, base, bytes, off);
+            run_add<DT>(out, y);
+        } else {
+            run_load<DT, AUX>(out, t, LO + rem, base, bytes, off);
+        }
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        run_tree<DT, K, LO, MID, AUX>(out, t, base, bytes, off);
+        RunVec<DT> right;
+        run_tree<DT, K, MID, HI, AUX>(right, t, base, bytes, off);
+        run_add<DT>(out, right);
+    }
+}
+
+template <int DT, int NB, int FV, int ORDER>
+__global__ void __launch_bounds__(kFoldThreads) k_sumN_run(SegTableN t) {
+    using A = Acc<DT>;
+    using S = typename Add<DT>::S;
+    using T = typename A::T;
+    constexpr int V = RunVec<DT>::V;
+    constexpr int K = NB + 1;
+    constexpr int kLoadAux = (FV & 1) ? kAuxNt : 0;
+    constexpr int kStoreAux = ((FV & 2) ? kAuxNt : 0) | ((FV & 4) ? (kAuxSc0 | kAuxSc1) : 0);
+    const uint64_t nv = t.n / V;
+    const uint64_t base = (uint64_t)blockIdx.x * kRunVec;
+    if (base < nv) {
+        const int bytes = (int)((nv - base < kRunVec ? nv - base : kRunVec) * 16);
+        const int off = (int)threadIdx.x * 16;
+        RunVec<DT> acc;
+        if constexpr (ORDER == kFoldMpichTree) {
+            constexpr int pof2 = K >= 16 ? 16 : K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
+            run_tree<DT, K, 0, pof2, kLoadAux>(acc, t, base, bytes, off);
+        } else {  // left fold (and the half types' fp32 running sum)
+            run_load<DT, kLoadAux>(acc, t, 0, base, bytes, off);
+#pragma unroll
+            for (int j = 1; j < K; ++j) {
+                RunVec<DT> x;
+                run_load<DT, kLoadAux>(x, t, j, base, bytes, off);
+                run_add<DT>(acc, x);
+            }
+        }
+        const auto ro = __builtin_amdgcn_make_buffer_rsrc(static_cast<u32x4 *>(t.out) + base, 0, bytes, kRsrcWord3);
+#pragma unroll
+        for (int u = 0; u < kRunTiles; ++u) {
+            u32x4 res;
+            S *rs = reinterpret_cast<S *>(&res);
+#pragma unroll
+            for (int e = 0; e < V; ++e) rs[e] = A::narrow(acc.e[u][e]);
+            __builtin_amdgcn_raw_buffer_store_b128(res, ro, off + u * kFoldThreads * 16, 0, kStoreAux);
+        }
+    }
+    const uint64_t rem = t.n - nv * V;
+    if (rem && blockIdx.x == nv / kRunVec && threadIdx.x < rem) {
+        const uint64_t e = nv * V + threadIdx.x;
+        T w[NB + 1];
+        w[0] = A::widen(static_cast<const S *>(t.a)[e]);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) w[k + 1] = A::widen(static_cast<const S *>(t.b[k])[e]);
+        static_cast<S *>(t.out)[e] = A::narrow(fold_values<DT, NB + 1, ORDER>(w));
+    }
+}
+
+// Fold form (config "fold_form", set_fold_form): the run form for chunks above kFoldRunMinBytes
+// in the left or MPICH-tree order, the tile form otherwise (small chunks are cache-resident and
+// latency bound: more, smaller workgroups; the binomial order is for <= 2 KiB).
+constexpr size_t kFoldRunMinBytes = 8u << 20;
+std::atomic<int> g_fold_form{0};
+bool fold_run_form(size_t chunk_bytes, int order) {
+    if (order == kFoldBinomial) return false;
+    const int f = g_fold_form.load(std::memory_order_relaxed);
+    if (f != 0) return f == 2;
+    return chunk_bytes > kFoldRunMinBytes;
+}
+
 // Half types fold left in fp32 whatever the order: only kFoldLeft is instantiated for them.
 template <int DT>
 constexpr bool kHalfType = DT == DDL_HALF || DT == DDL_BFLOAT16;
 
 template <int DT, int NB, int FV>
 void launch_sumN_order(const SegTableN &t, hipStream_t stream, unsigned tiles) {
+    constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
+    if (fold_run_form((size_t)t.n * sizeof(typename Add<DT>::S), t.order)) {
+        const uint64_t runs = ((uint64_t)t.n / V + kRunVec) / kRunVec;  // +1 vector of room for the tail
+        if constexpr (!kHalfType<DT>) {
+            if (t.order == kFoldMpichTree) {
+                hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldMpichTree>), dim3((unsigned)runs), dim3(kFoldThreads), 0,
+                                   stream, t);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldLeft>), dim3((unsigned)runs), dim3(kFoldThreads), 0, stream, t);
+        return;
+    }
     if constexpr (!kHalfType<DT>) {
         if (t.order == kFoldMpichTree) {
             hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldMpichTree>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
@@ -450,6 +594,9 @@ inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 
 int g_cu_count = 0;
 
 }  // namespace
+
+void set_fold_form(int form) { g_fold_form.store(form, std::memory_order_relaxed); }
+int get_fold_form() { return g_fold_form.load(std::memory_order_relaxed); }
 
 // An empty node (one wavefront, no memory access) for graph captures: see launch_capture_anchor.
 __global__ void k_capture_anchor() {}

@@ -212,6 +212,55 @@ def test_reduce_fold_ordered_kernel(lib, oracle, gpu, dt, nb, order, n, misalign
     assert got.tobytes() == want.tobytes()
 
 
+# the run form of the fold (reduce_kernels.hip k_sumN_run: chunks above 8 MiB, a workgroup walks
+# the inputs one at a time over a 16 KiB run): every dtype, 2..16 inputs, the left fold and MPICH's
+# tree, chunk sizes a whole number of runs plus a ragged tail and not
+RUN_BYTES = [(9 << 20) + 16 * 1024 * 3, (9 << 20) + 4096 + 48]
+
+
+@pytest.mark.parametrize('dt', [1, 2, 3, 9, 14, 19, 23])
+@pytest.mark.parametrize('nb', [1, 2, 4, 7, 9, 15])
+@pytest.mark.parametrize('order', [0, 1])
+@pytest.mark.parametrize('nbytes', RUN_BYTES + [4100 * 4, 1 << 20], ids=['whole_runs+tail', 'ragged', 'small',
+                                                                         '1MiB'])
+def test_reduce_fold_run_form(lib, oracle, gpu, dt, nb, order, nbytes):
+    """Above 8 MiB the fold runs in its run form by default; the small sizes force it
+    (config fold_form 2) so its tails are checked at sizes of one run and less."""
+    from _helpers import config
+    es = {1: 4, 2: 8, 3: 4, 9: 8, 14: 2, 19: 2, 23: 8}[dt]
+    n = nbytes // es + (es < 8) * 3  # + a tail shorter than one 16-byte vector (for es < 8)
+    with config(lib, fold_form=0 if nbytes > (8 << 20) else 2):
+        _fold_check(lib, oracle, gpu, dt, nb, order, n, es)
+
+
+@pytest.mark.parametrize('dt', [1, 14])
+@pytest.mark.parametrize('nb', [2, 7])
+def test_reduce_fold_tile_form_forced_large(lib, oracle, gpu, dt, nb):
+    """config fold_form 1 keeps the tile form above 8 MiB (the A/B the bench reports)."""
+    from _helpers import config
+    es = 4 if dt == 1 else 2
+    with config(lib, fold_form=1):
+        _fold_check(lib, oracle, gpu, dt, nb, 1, RUN_BYTES[1] // es + 3, es)
+
+
+def _fold_check(lib, oracle, gpu, dt, nb, order, n, es):
+    xs = [random_input(dt, n, 1300 + 7 * i + dt) for i in range(nb + 1)]
+    ts = [to_dev(x, gpu) for x in xs]
+    out = torch.zeros_like(ts[0])
+    P = ctypes.c_void_p * nb
+    s = torch.cuda.current_stream().cuda_stream
+    ptrs = [t.data_ptr() for t in ts]
+    if order == 0:
+        st = lib.ddl_reduce_fold(out.data_ptr(), ptrs[0], P(*ptrs[1:]), nb, n, dt, s)
+    else:
+        st = lib.ddl_reduce_fold_ordered(out.data_ptr(), ptrs[0], P(*ptrs[1:]), nb, n, dt, 1, s)
+    assert st == 0, lib.ddl_last_error()
+    torch.cuda.synchronize()
+    want = oracle.fold(dt, xs) if order == 0 else oracle.fold_ref_order(dt, xs, 4096)
+    got = out.cpu().numpy().view(xs[0].dtype)
+    assert got.tobytes() == want.tobytes(), np.flatnonzero(got.view(np.uint8) != want.view(np.uint8))[:8]
+
+
 def test_reduce_fold_ordered_rejects_bad_order(lib, gpu):
     x = torch.zeros(16, device=gpu)
     P = ctypes.c_void_p * 1

@@ -1,4 +1,4 @@
-"""Launches the direct schedule's fold kernel (k_sumN_tile) in the two shapes the N>1 path runs, for
+"""Launches the direct schedule's fold kernel (k_sumN_run / k_sumN_tile) in the two shapes the N>1 path runs, for
 rocprofv3 PMC passes (the counters that bound them):
   fp32: one P = 8 chunk of the C3 bucket (32 MiB, 7 received inputs + own, non-temporal loads,
         write-through store) — 40 launches over 2 rotating buffer sets;
@@ -34,7 +34,10 @@ def run(lib, chunk_bytes, half, reps, sets):
 def main():
     lib = CPPBackend.c_api()
     torch.cuda.set_device(0)
-    run(lib, 32 << 20, False, 40, 2)
+    run(lib, 32 << 20, False, 40, 2)  # the run form (k_sumN_run, the default above 8 MiB)
+    check(lib.ddl_set_config(b'fold_form', 1), 'fold_form')
+    run(lib, 32 << 20, False, 40, 2)  # the tile form of the same chunk (A/B)
+    check(lib.ddl_set_config(b'fold_form', 0), 'fold_form')
     run(lib, 2 << 20, True, 200, 1)
     print('fold_pmc: done', flush=True)
 

@@ -64,6 +64,31 @@ __global__ void __launch_bounds__(kT) k_mix(Streams s, unsigned long long nv) {
     }
 }
 
+// Blocked form: a workgroup owns U consecutive tiles of the output and streams them input by
+// input — U loads per lane from input k in flight, accumulated, then input k + 1 — so each
+// workgroup reads one stream at a time in U * 2 KiB runs instead of 1 tile from all R streams.
+template <int R, int U, int T = kT, bool INPLACE = false>
+__global__ void __launch_bounds__(T) k_mix_blocked(Streams s, unsigned long long nv) {
+    const unsigned long long base = (unsigned long long)blockIdx.x * T * U;
+    if (base >= nv) return;
+    const int bytes = (int)((nv - base < (unsigned long long)T * U ? nv - base : (unsigned long long)T * U) * 16);
+    const int off = (int)threadIdx.x * 16;
+    f4 acc[U];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(s.x[k] + base, 0, bytes, kWord3);
+        u4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + u * T * 16, 0, kAuxNt);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = k == 0 ? __builtin_bit_cast(f4, raw[u]) : acc[u] + __builtin_bit_cast(f4, raw[u]);
+    }
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc((INPLACE ? s.x[0] : s.o) + base, 0, bytes, kWord3);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[u]), ro, off + u * T * 16, 0, kAuxWt);
+}
+
 __global__ void k_init(u4 *p, unsigned long long nv, unsigned seed) {
     for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < nv;
          i += (unsigned long long)gridDim.x * blockDim.x) {
@@ -94,6 +119,17 @@ Case mk(const char *pol, int lds_kib = 0) {
                 }};
 }
 
+template <int R, int U, int T = kT, bool INPLACE = false>
+Case mk_blocked() {
+    char nm[96];
+    std::snprintf(nm, sizeof nm, "R%d W1 (%d:1) blocked%s, %d lanes x %d vectors (%d KiB runs)", R, R,
+                  INPLACE ? " in place" : "", T, U, T * U * 16 / 1024);
+    return Case{nm, R, 1, [](const Streams &s, unsigned long long nv, hipStream_t st) {
+                    const unsigned wgs = (unsigned)((nv + (unsigned long long)T * U - 1) / ((unsigned long long)T * U));
+                    hipLaunchKernelGGL((k_mix_blocked<R, U, T, INPLACE>), dim3(wgs), dim3(T), 0, st, s, nv);
+                }};
+}
+
 int main(int argc, char **argv) {
     const size_t total_mib = argc > 1 ? std::atoi(argv[1]) : 288;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 5;
@@ -106,6 +142,15 @@ int main(int argc, char **argv) {
         mk<4, 1, kAuxNt>("nt loads, wt store"), mk<8, 1, kAuxNt>("nt loads, wt store"),
         mk<8, 0, 0>("plain loads"),             mk<8, 1, 0>("plain loads, wt store"),
     };
+    if (argc > 3 && std::string(argv[3]) == "blocked") {  // one stream at a time per workgroup
+        cases = {mk<8, 1, kAuxNt>("nt loads, wt store"), mk_blocked<8, 4>(), mk_blocked<8, 8>(), mk_blocked<8, 16>(),
+                 mk_blocked<8, 32>(), mk_blocked<8, 4, 256>(), mk_blocked<8, 8, 256>(), mk_blocked<8, 2, 512>(),
+                 mk_blocked<8, 4, 512>(), mk_blocked<8, 8, 64>(), mk_blocked<8, 16, 64>(),
+                 mk<4, 1, kAuxNt>("nt loads, wt store"), mk_blocked<4, 8>(), mk_blocked<4, 16>(),
+                 mk<2, 1, kAuxNt>("nt loads, wt store"), mk_blocked<2, 4>(), mk_blocked<2, 8>(), mk_blocked<2, 16>(),
+                 mk_blocked<2, 4, 256>(), mk_blocked<2, 8, 256>(), mk_blocked<2, 4, kT, true>(),
+                 mk_blocked<2, 8, kT, true>(), mk_blocked<2, 16, kT, true>()};
+    }
     if (occ) {  // occupancy caps: does a smaller in-flight window per stream lift the many-stream mixes?
         cases.clear();
         for (int lds : {0, 10, 20, 27, 32, 40, 64}) {
