@@ -443,15 +443,19 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_run(SegTableN t) {
 }
 
 // Fold form (config "fold_form", set_fold_form): the run form for chunks above kFoldRunMinBytes
-// in the left or MPICH-tree order, the tile form otherwise (small chunks are cache-resident and
-// latency bound: more, smaller workgroups; the binomial order is for <= 2 KiB).
+// of at least kFoldRunMinInputs inputs in the left or MPICH-tree order, the tile form otherwise.
+// Small chunks are cache-resident and latency bound (more, smaller workgroups); the binomial
+// order is for <= 2 KiB; and below 7 inputs the run form measured no better or worse than the
+// tile form (tools/stream_mix.hip rform, two boxes: 8:1 +2.5 to +10 %, 7:1 0 to +2 %, 2:1 to
+// 6:1 -3 to +1 %; profiles/r03/stream_mix/).
 constexpr size_t kFoldRunMinBytes = 8u << 20;
+constexpr int kFoldRunMinInputs = 7;
 std::atomic<int> g_fold_form{0};
-bool fold_run_form(size_t chunk_bytes, int order) {
+bool fold_run_form(size_t chunk_bytes, int order, int inputs) {
     if (order == kFoldBinomial) return false;
     const int f = g_fold_form.load(std::memory_order_relaxed);
     if (f != 0) return f == 2;
-    return chunk_bytes > kFoldRunMinBytes;
+    return chunk_bytes > kFoldRunMinBytes && inputs >= kFoldRunMinInputs;
 }
 
 // Half types fold left in fp32 whatever the order: only kFoldLeft is instantiated for them.
@@ -461,7 +465,7 @@ constexpr bool kHalfType = DT == DDL_HALF || DT == DDL_BFLOAT16;
 template <int DT, int NB, int FV>
 void launch_sumN_order(const SegTableN &t, hipStream_t stream, unsigned tiles) {
     constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
-    if (fold_run_form((size_t)t.n * sizeof(typename Add<DT>::S), t.order)) {
+    if (fold_run_form((size_t)t.n * sizeof(typename Add<DT>::S), t.order, NB + 1)) {
         const uint64_t runs = ((uint64_t)t.n / V + kRunVec) / kRunVec;  // +1 vector of room for the tail
         if constexpr (!kHalfType<DT>) {
             if (t.order == kFoldMpichTree) {

@@ -151,6 +151,16 @@ int main(int argc, char **argv) {
                  mk_blocked<2, 4, 256>(), mk_blocked<2, 8, 256>(), mk_blocked<2, 4, kT, true>(),
                  mk_blocked<2, 8, kT, true>(), mk_blocked<2, 16, kT, true>()};
     }
+    if (argc > 3 && std::string(argv[3]) == "rform") {  // tile vs run form for every fold width
+        cases = {mk<2, 1, kAuxNt>("nt loads, wt store"), mk_blocked<2, 8>(),
+                 mk<3, 1, kAuxNt>("nt loads, wt store"), mk_blocked<3, 8>(),
+                 mk<4, 1, kAuxNt>("nt loads, wt store"), mk_blocked<4, 8>(),
+                 mk<5, 1, kAuxNt>("nt loads, wt store"), mk_blocked<5, 8>(),
+                 mk<6, 1, kAuxNt>("nt loads, wt store"), mk_blocked<6, 8>(),
+                 mk<7, 1, kAuxNt>("nt loads, wt store"), mk_blocked<7, 8>(),
+                 mk<8, 1, kAuxNt>("nt loads, wt store"), mk_blocked<8, 8>(),
+                 mk_blocked<2, 2>(), mk_blocked<2, 2, kT, true>(), mk_blocked<2, 4, 64>(), mk_blocked<2, 4, 64, true>()};
+    }
     if (occ) {  // occupancy caps: does a smaller in-flight window per stream lift the many-stream mixes?
         cases.clear();
         for (int lds : {0, 10, 20, 27, 32, 40, 64}) {
