@@ -385,9 +385,9 @@ long long ddl_get_config(const char *key) {
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
     if (k == "host_register_failures") return c.host_register_failures;  // statistic, not settable
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
-    if (k == "host_pack_us") return c.host_pack_us;                  // statistic, not settable
-    if (k == "host_wait_us") return c.host_wait_us;                  // statistic, not settable
-    if (k == "host_unpack_us") return c.host_unpack_us;              // statistic, not settable
+    if (k == "host_pack_us") return c.host_pack_ns / 1000;      // statistic, not settable
+    if (k == "host_wait_us") return c.host_wait_ns / 1000;      // statistic, not settable
+    if (k == "host_unpack_us") return c.host_unpack_ns / 1000;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;

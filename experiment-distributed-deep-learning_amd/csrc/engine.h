@@ -65,9 +65,9 @@ struct Config {
     // over every plan of the process): the engine thread packing chunks into pinned slots (host
     // memcpy, with the copy threads), waiting for a slot whose earlier DMA / device work is still
     // in flight, and unpacking staged results
-    std::atomic<long long> host_pack_us{0};
-    std::atomic<long long> host_wait_us{0};
-    std::atomic<long long> host_unpack_us{0};
+    std::atomic<long long> host_pack_ns{0};  // read as microseconds (host_pack_us, ...)
+    std::atomic<long long> host_wait_ns{0};
+    std::atomic<long long> host_unpack_ns{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};
