@@ -6,6 +6,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "engine.h"
@@ -147,19 +148,21 @@ void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len)
     std::memcpy(out, res.c_str(), res.size() + 1);
 }
 
-// The submitter's input-ready event: device requests are ordered after hip_stream's current
-// position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
+// One thread world per (ranks, device, compute_cu_mask): its executors' compute streams are
+// created with the mask in force when the world is.
 ThreadWorld &thread_world(int nranks) {
     static std::mutex mu;
-    static auto *worlds = new std::map<std::pair<int, int>, std::unique_ptr<ThreadWorld>>();
+    static auto *worlds = new std::map<std::tuple<int, int, int>, std::unique_ptr<ThreadWorld>>();
     int dev = current_device();
     std::lock_guard<std::mutex> g(mu);
-    auto key = std::make_pair(nranks, dev);
+    auto key = std::make_tuple(nranks, dev, config_compute_cu_mask());
     auto it = worlds->find(key);
     if (it == worlds->end()) it = worlds->emplace(key, std::unique_ptr<ThreadWorld>(new ThreadWorld(nranks, dev))).first;
     return *it->second;
 }
 
+// The submitter's input-ready event: device requests are ordered after hip_stream's current
+// position; host requests are ready at submission (CPU tensors, as the reference's op inputs).
 std::shared_ptr<ReadyEvent> ready_event(int memory, void *hip_stream) {
     DDL_REQUIRE(memory == DDL_MEMORY_DEVICE || memory == DDL_MEMORY_HOST, DDL_STATUS_INVALID_ARGUMENT,
                 "memory must be DDL_MEMORY_DEVICE (0) or DDL_MEMORY_HOST (1), not " << memory);
@@ -355,7 +358,11 @@ int ddl_set_config(const char *key, long long value) {
                         "capture_mode must be 0 (serial), 1 (forked streams) or 2 (single-stream DAG)");
             c.capture_mode = value;
         } else if (k == "capture_forked") c.capture_mode = value ? 1 : 0;
-        else if (k == "fold_form") {
+        else if (k == "compute_cu_mask") {
+            DDL_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, DDL_STATUS_INVALID_ARGUMENT,
+                        "compute_cu_mask must be 0 (all CUs), 2, 4 or 8 (every n-th CU left to RCCL)");
+            c.compute_cu_mask = value;
+        } else if (k == "fold_form") {
             DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT,
                         "fold_form must be 0 (auto), 1 (tile form) or 2 (run form)");
             set_fold_form((int)value);
@@ -394,6 +401,7 @@ long long ddl_get_config(const char *key) {
     if (k == "reference_order") return c.reference_order;
     if (k == "capture_mode") return c.capture_mode;
     if (k == "fold_form") return get_fold_form();
+    if (k == "compute_cu_mask") return c.compute_cu_mask;
     if (k == "capture_forked") return c.capture_mode.load() == 1 ? 1 : 0;
     return -1;
 }
@@ -847,6 +855,20 @@ int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *co
 
 int ddl_testing_drop_wait(int tick) {
     return guarded([&] { set_testing_drop_wait(tick); });
+}
+
+int ddl_testing_compute_stream_cus(int every, int *enabled, int *total) {
+    return guarded([&] {
+        DDL_REQUIRE(enabled && total, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        RankResources rr(current_device(), every);
+        const int ncu = device_cu_count();
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        DDL_HIP(hipExtStreamGetCUMask(rr.compute, (uint32_t)mask.size(), mask.data()));
+        int on = 0;
+        for (int c = 0; c < ncu; ++c) on += (mask[(size_t)c / 32] >> (c % 32)) & 1u;
+        *enabled = on;
+        *total = ncu;
+    });
 }
 
 // ---- RCCL loopback (one GPU, real RCCL transport) --------------------------------------------

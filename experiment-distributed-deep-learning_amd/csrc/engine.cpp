@@ -52,6 +52,7 @@ uint64_t Config::shared_hash() const {
 
 int log_level() { return (int)config().log_level.load(); }
 int config_capture_mode() { return (int)config().capture_mode.load(); }
+int config_compute_cu_mask() { return (int)config().compute_cu_mask.load(); }
 
 void log_line(int level, const std::string &msg) {
     static std::mutex mu;

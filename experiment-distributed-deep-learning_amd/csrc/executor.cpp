@@ -108,9 +108,27 @@ void CallbackTransport::host_group(std::vector<ddl_p2p_op> &ops) {
     DDL_REQUIRE(rc == 0, DDL_STATUS_COMM_ERROR, "test transport: group callback failed (" << rc << ")");
 }
 
-RankResources::RankResources(int dev) : device(dev) {
+hipStream_t create_compute_stream(int every) {
+    hipStream_t s = nullptr;
+    int ncu = device_cu_count();
+    if (every >= 2 && ncu > 0) {
+        // CU c off when c % every == every - 1: the reduce / fold kernels keep their full HBM rate
+        // on such masks (tools/cu_mask_probe.py: every 8th, 4th or 2nd CU off, 6.56-6.59 TB/s vs
+        // 6.59 on all 256) and leave the masked-off CUs free for RCCL's send / recv kernels
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu; ++c)
+            if (c % every != every - 1) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return s;
+        (void)hipGetLastError();  // a runtime without CU masks: an ordinary stream
+        DDL_LOG(1, "compute_cu_mask " << every << ": hipExtStreamCreateWithCUMask failed, using an unmasked stream");
+    }
+    DDL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
+RankResources::RankResources(int dev, int cu_mask_every) : device(dev) {
     DDL_HIP(hipStreamCreateWithFlags(&comm, hipStreamNonBlocking));
-    DDL_HIP(hipStreamCreateWithFlags(&compute, hipStreamNonBlocking));
+    compute = create_compute_stream(cu_mask_every);
     DDL_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     DDL_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     DDL_HIP(hipEventCreateWithFlags(&join_cp_ev, hipEventDisableTiming));
@@ -187,7 +205,7 @@ int last_reduce_at_or_before(const RingProgram &p, int w) {
 }
 
 RingExecutor::RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport)
-    : rank_(rank), size_(size), transport_(std::move(transport)), res_(device) {}
+    : rank_(rank), size_(size), transport_(std::move(transport)), res_(device, size > 1 ? config_compute_cu_mask() : 0) {}
 
 RingExecutor::~RingExecutor() {
     for (auto *v : {&timed_, &free_pairs_})
@@ -555,7 +573,7 @@ void ThreadWorld::allgatherv(const void *const *sends, void *const *recvs, const
 }
 
 LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks) {
-    for (int r = 0; r < nranks; ++r) res_.emplace_back(new RankResources(device));
+    for (int r = 0; r < nranks; ++r) res_.emplace_back(new RankResources(device, config_compute_cu_mask()));
     progs_.resize(nranks);
     if (loopback) {
         loop_.reset(new RcclTransport(loopback));

@@ -42,6 +42,9 @@ bool stream_capturing(hipStream_t s);
 // Config "capture_mode": how a program is posted inside a capture — 0 serially on the captured
 // stream, 1 on the forked comm / compute streams as eagerly, 2 as a single-stream DAG (Poster).
 int config_capture_mode();
+// Config "compute_cu_mask" (0 off, 2 / 4 / 8): the compute streams of multi-rank executors leave
+// every n-th CU to RCCL (read when an executor is created).
+int config_compute_cu_mask();
 
 // Posts a program's ops on its logical streams (each rank's comm / compute stream, a transport
 // stream) with event records and waits between them, in one of three ways:
@@ -189,7 +192,9 @@ void set_testing_drop_wait(int tick);
 // Streams, events and staging memory of one rank (reused across calls).
 class RankResources {
 public:
-    explicit RankResources(int device);
+    // cu_mask_every >= 2: the compute stream (reduce / fold kernels) is created with every
+    // cu_mask_every-th CU masked off (config "compute_cu_mask"), leaving those to RCCL's kernels
+    RankResources(int device, int cu_mask_every = 0);
     ~RankResources();
     RankResources(const RankResources &) = delete;
     RankResources &operator=(const RankResources &) = delete;

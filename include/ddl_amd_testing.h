@@ -139,6 +139,9 @@ int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *co
 /* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
  * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
 int ddl_testing_drop_wait(int tick);
+/* The CUs enabled on an executor compute stream created with every `every`-th CU masked off
+ * (config "compute_cu_mask"; 0 = unmasked), read back with hipExtStreamGetCUMask. */
+int ddl_testing_compute_stream_cus(int every, int *enabled, int *total);
 
 /* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
  * A one-rank RCCL communicator (ncclGetUniqueId + ncclCommInitRank, the calls ddl_init makes at

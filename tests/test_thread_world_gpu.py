@@ -191,3 +191,29 @@ def test_dropping_one_reduce_wait_is_caught(lib, oracle, gpu):
         assert all(o.cpu().numpy().tobytes() == want for o in outs)
     del ins, outs
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize('every,want', [(0, 256), (8, 224), (4, 192), (2, 128)])
+def test_compute_stream_cu_mask(lib, gpu, every, want):
+    """config compute_cu_mask: a multi-rank executor's compute stream (its reduce / fold kernels)
+    leaves every n-th CU to RCCL — read back from the stream with hipExtStreamGetCUMask."""
+    on, total = ctypes.c_int(), ctypes.c_int()
+    assert lib.ddl_testing_compute_stream_cus(every, ctypes.byref(on), ctypes.byref(total)) == 0, lib.ddl_last_error()
+    assert on.value == total.value * want // 256, (every, on.value, total.value)
+
+
+@pytest.mark.parametrize('mask', [0, 2])
+def test_masked_compute_stream_bit_exact(lib, oracle, gpu, mask):
+    """The production executor with its compute stream masked (and unmasked; a thread world per
+    mask): every rank still equals MPICH's order on a P = 8 direct allreduce whose chunks take the
+    run-form fold."""
+    P, n = 8, (9 << 20) // 4 * 8 + 5  # 9 MiB chunks: the run form at 8 inputs
+    with config(lib, compute_cu_mask=mask, algo=1, reference_order=1, tune=0, slice_bytes=64 << 20):
+        xs = [random_input(DT_FLOAT, n, 4242 + 7919 * r) for r in range(P)]
+        ins = [_dev(x, gpu) for x in xs]
+        outs = [torch.empty_like(t) for t in ins]
+        _thread_allreduce(lib, ins, outs, n, DT_FLOAT)
+        torch.cuda.synchronize()
+        want = oracle.fold_ref_order(DT_FLOAT, xs).tobytes()
+        for r in range(P):
+            assert outs[r].cpu().numpy().tobytes() == want, r
