@@ -45,6 +45,9 @@ int config_capture_mode();
 // Config "compute_cu_mask" (0 off, 2 / 4 / 8): the compute streams of multi-rank executors leave
 // every n-th CU to RCCL (read when an executor is created).
 int config_compute_cu_mask();
+// A non-blocking stream whose kernels avoid every `every`-th CU (every >= 2; otherwise, or where
+// the runtime refuses CU masks, an ordinary non-blocking stream).
+hipStream_t create_compute_stream(int every);
 
 // Posts a program's ops on its logical streams (each rank's comm / compute stream, a transport
 // stream) with event records and waits between them, in one of three ways:

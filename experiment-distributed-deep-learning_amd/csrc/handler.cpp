@@ -215,7 +215,10 @@ RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
     } else {
         data_ = owner_->shared_from_this();
     }
-    DDL_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    // the fusion pack / unpack kernels overlap other plans' RCCL kernels at size > 1: the same CU
+    // mask as the executors' compute streams (config compute_cu_mask; pack / unpack keep their
+    // rate on it, tools/cu_mask_probe.py)
+    stream_ = create_compute_stream(owner_->size() > 1 ? config_compute_cu_mask() : 0);
     done_thread_ = std::thread(&RequestHandler::completer_, this);
     thread_ = std::thread(&RequestHandler::main_, this);
 }

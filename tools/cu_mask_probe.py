@@ -44,8 +44,22 @@ def main():
     fold16 = [[torch.rand(1 << 20, device=dev).half() for _ in range(9)] for _ in range(1)]
     fold8m = [[torch.rand(2 << 20, device=dev) for _ in range(9)] for _ in range(2)]  # 8 MiB: the tile form
     red = [(torch.rand(64 << 20, device=dev), torch.rand(64 << 20, device=dev)) for _ in range(3)]
+    # the fusion pack / unpack on the C5 set (4096 segments of 4 KiB - 4 MiB, bench.fusion_c5's sizes)
+    import numpy as np
+    rng = np.random.default_rng(5)
+    sizes = (np.exp(rng.uniform(np.log(4096), np.log(4 << 20), size=4096)).astype(np.int64) // 256) * 256
+    segs = [torch.empty(int(x), dtype=torch.uint8, device=dev) for x in sizes]
+    flat = torch.empty(int(sizes.sum()) + 256 * 4096, dtype=torch.uint8, device=dev)
+    sptr = (ctypes.c_void_p * 4096)(*[t.data_ptr() for t in segs])
+    sbytes = (ctypes.c_size_t * 4096)(*[int(x) for x in sizes])
 
     def run(kind, k, sh):
+        if kind in ('pack', 'unpack'):
+            if kind == 'pack':
+                check(lib.ddl_pack(flat.data_ptr(), sptr, sbytes, 4096, sh), 'pack')
+            else:
+                check(lib.ddl_unpack(sptr, flat.data_ptr(), sbytes, 4096, sh), 'unpack')
+            return 2 * int(sizes.sum())
         if kind == 'reduce':
             a, b = red[k % 3]
             check(lib.ddl_reduce_local(a.data_ptr(), b.data_ptr(), a.numel(), 1, sh), 'reduce')
@@ -66,7 +80,8 @@ def main():
             s = masked_stream(hip, ncu, enabled)
             ts = torch.cuda.ExternalStream(s.value)
             res = {}
-            for kind, reps in (('fold_fp32_32MiB', 20), ('fold_fp32_8MiB', 40), ('fold_fp16_2MiB', 50), ('reduce', 12)):
+            for kind, reps in (('fold_fp32_32MiB', 20), ('fold_fp32_8MiB', 40), ('fold_fp16_2MiB', 50), ('reduce', 12),
+                               ('pack', 4), ('unpack', 4)):
                 for i in range(3):
                     run(kind, i, s.value)
                 best = 1e9
