@@ -328,8 +328,8 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     if (prog_.ticks.empty()) return;
     DDL_TRACE("executor rank " << rank_ << "/" << size_ << " run: " << prog_.ticks.size() << " ticks, user " << (void *)user);
     // Eagerly the program forks from the caller's stream onto the comm / compute streams and joins
-    // back. Inside a graph capture the Poster turns the same posting into a single-stream DAG
-    // (default), forked streams, or a serial order on the captured stream (config capture_mode;
+    // back. Inside a graph capture the Poster turns the same posting into a serial order on the
+    // captured stream (default), a single-stream DAG or forked streams (config capture_mode;
     // executor.h).
     const bool capturing = stream_capturing(user);
     DDL_REQUIRE(!capturing || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
