@@ -339,6 +339,7 @@ int ddl_set_config(const char *key, long long value) {
             c.host_copy_threads = value;
         } else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
         else if (k == "host_direct_dma") c.host_direct_dma = value ? 1 : 0;
+        else if (k == "host_numa_bind") c.host_numa_bind = value ? 1 : 0;
         else if (k == "host_register_cache_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "host_register_cache_bytes must be >= 0");
             c.host_register_cache_bytes = value;
@@ -389,6 +390,7 @@ long long ddl_get_config(const char *key) {
     if (k == "host_zero_copy") return c.host_zero_copy;
     if (k == "host_direct_dma") return c.host_direct_dma;
     if (k == "host_register_cache_bytes") return c.host_register_cache_bytes;
+    if (k == "host_numa_bind") return c.host_numa_bind;
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
     if (k == "host_register_failures") return c.host_register_failures;  // statistic, not settable
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable

@@ -55,6 +55,11 @@ struct Config {
     // setting it back to 0 unregisters every cached range at once (ddl_set_config), before the
     // caller frees them: a freed range left registered poisons later copies from that address.
     std::atomic<long long> host_register_cache_bytes{0};
+    // keyed host path: the engine thread and the copy threads bind to the CPUs of the GPU's NUMA
+    // node (within the process's affinity) when its handler starts — pinned host memory lives
+    // there, and threads on the other socket pack it at half the rate (1 on, 0 leave placement to
+    // the OS)
+    std::atomic<long long> host_numa_bind{1};
     // read-only statistics of that cache (ddl_get_config): bytes registered now, failed registrations
     std::atomic<long long> host_registered_bytes{0};
     std::atomic<long long> host_register_failures{0};

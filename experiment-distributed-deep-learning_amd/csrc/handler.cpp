@@ -1,8 +1,12 @@
 // handler.cpp — see handler.h.
 #include "handler.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <iterator>
 #include <set>
@@ -103,7 +107,64 @@ ReadyEvent::~ReadyEvent() {
     if (e) (void)hipEventDestroy(e);
 }
 
-CopyPool::CopyPool(int threads) {
+namespace {
+// The CPUs of the NUMA node the device's PCI function hangs off, intersected with this thread's
+// affinity; empty when unknown, or when binding would not narrow the set. The keyed host path's
+// memcpy reads pinned host memory, which the HIP runtime places on the GPU's node: threads on the
+// other socket pack the C5 set at half the rate (tools/numa_probe.py).
+std::vector<int> gpu_local_cpus(int device) {
+    int dom = 0, bus = 0, dev = 0;
+    if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess ||
+        hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return {};
+    }
+    char path[128];
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%04x:%02x:%02x.0/numa_node", dom, bus, dev);
+    FILE *f = std::fopen(path, "r");
+    int node = -1;
+    if (f) {
+        if (std::fscanf(f, "%d", &node) != 1) node = -1;
+        std::fclose(f);
+    }
+    if (node < 0) return {};
+    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    f = std::fopen(path, "r");
+    if (!f) return {};
+    char buf[4096] = {};
+    const size_t got = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[got] = 0;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return {};
+    std::vector<int> cpus;
+    for (char *p = buf; *p;) {  // "0-63,128-191"
+        char *end = nullptr;
+        const long a = std::strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        if (*end == '-') b = std::strtol(end + 1, &end, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c >= 0 && CPU_ISSET((int)c, &allowed)) cpus.push_back((int)c);
+        p = *end == ',' ? end + 1 : end;
+        if (*p == '\n') break;
+    }
+    if (cpus.empty() || (int)cpus.size() == CPU_COUNT(&allowed)) return {};
+    return cpus;
+}
+
+void bind_this_thread(const std::vector<int> &cpus) {
+    if (cpus.empty()) return;
+    cpu_set_t s;
+    CPU_ZERO(&s);
+    for (int c : cpus) CPU_SET(c, &s);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof s, &s);
+}
+}  // namespace
+
+CopyPool::CopyPool(int threads, std::vector<int> cpus) : cpus_(std::move(cpus)) {
     for (int i = 0; i < threads; ++i) threads_.emplace_back(&CopyPool::worker_, this);
 }
 
@@ -117,6 +178,7 @@ CopyPool::~CopyPool() {
 }
 
 void CopyPool::worker_() {
+    bind_this_thread(cpus_);
     for (;;) {
         std::function<void()> task;
         {
@@ -359,6 +421,12 @@ void RequestHandler::fail_all_(int status) {
 void RequestHandler::main_() {
     try {
         DDL_HIP(hipSetDevice(owner_->device()));
+        // the engine thread takes a share of every host pack / unpack: it and the copy threads
+        // run on the GPU's NUMA node (config host_numa_bind, read when the handler starts)
+        if (config().host_numa_bind.load()) {
+            local_cpus_ = gpu_local_cpus(owner_->device());
+            bind_this_thread(local_cpus_);
+        }
         ControlChannel *ch = ch_;  // null at size 1
         const int P = owner_->size(), rank = owner_->rank();
         for (;;) {
@@ -813,7 +881,7 @@ CopyPool &RequestHandler::pool_for_config_() {
     const int want = (int)std::max(0ll, config().host_copy_threads.load());
     if (!pool_ || pool_->threads() != want) {
         pool_.reset();
-        pool_.reset(new CopyPool(want));
+        pool_.reset(new CopyPool(want, local_cpus_));
     }
     return *pool_;
 }

@@ -79,7 +79,8 @@ public:
         const void *src;
         size_t bytes;
     };
-    explicit CopyPool(int threads);
+    // cpus non-empty: every worker binds itself to that CPU set (the GPU's NUMA node)
+    explicit CopyPool(int threads, std::vector<int> cpus = {});
     ~CopyPool();
     CopyPool(const CopyPool &) = delete;
     CopyPool &operator=(const CopyPool &) = delete;
@@ -93,6 +94,7 @@ public:
 private:
     void worker_();
     void submit_and_wait_(std::vector<std::function<void()>> &tasks);  // tasks[0] on the caller
+    std::vector<int> cpus_;
     std::vector<std::thread> threads_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
@@ -258,6 +260,7 @@ private:
     bool mapped_host_dsts_(std::vector<HostSeg> &segs);
     size_t host_slots_(size_t total);  // chunk size for `total` bytes; (re)allocates the slots
     CopyPool &pool_for_config_();     // the copy threads, rebuilt when host_copy_threads changed
+    std::vector<int> local_cpus_;     // the GPU's NUMA node's CPUs (config host_numa_bind; empty: no binding)
     void broadcast_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void allgather_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
     void fail_all_(int status);

@@ -123,6 +123,8 @@ int ddl_is_initialized(void);
  * pin_memory, hipHostMalloc, hipHostRegister — is unpacked by the fusion kernel straight into
  * them over PCIe, no D2H copy or host memcpy; 0: always stage through the pinned slots; the
  * read-only "host_zero_copy_plans" counts the plans that took that path),
+ * "host_numa_bind" (1, default: the handler's engine thread and copy threads bind to the CPUs of
+ * the GPU's NUMA node, where pinned host memory lives; 0: placement left to the OS),
  * "host_direct_dma" (0, default; 1: pinned input segments of >= 256 KiB of a keyed host plan are
  * uploaded by DMA straight from the tensors instead of through the copy threads — slower on the C5
  * set), "host_register_cache_bytes" (0, default = off; > 0: pageable host tensors of keyed requests

@@ -4,7 +4,7 @@ C5 host batch (bench.keyed_host_c5) with the main thread pinned to a CPU set cho
 engine starts a thread (its handler thread and memcpy workers inherit it) and before the host
 tensors are allocated (first touch):
     python tools/numa_probe.py topo
-    python tools/numa_probe.py run {default|local|remote} [threads]
+    python tools/numa_probe.py run {default|nobind|local|remote} [threads]
 One JSON line per run."""
 import ctypes
 import glob
@@ -77,6 +77,9 @@ def run(mode, threads):
     from ddl.torch.cpp_backend import CPPBackend, check
     torch.cuda.set_device(0)
     lib = CPPBackend.c_api()
+    # 'nobind': the default CPU set with the engine's own NUMA binding off (host_numa_bind 0, set
+    # before the handler starts), to A/B the binding against 'default'
+    check(lib.ddl_set_config(b'host_numa_bind', 0 if mode == 'nobind' else 1), 'cfg')
     comm = Communicator.world()
     check(lib.ddl_set_config(b'host_copy_threads', threads), 'cfg')
     # raw rates of the pieces, on the same CPUs: one memcpy stream pageable -> pinned, and pinned
@@ -103,10 +106,12 @@ def run(mode, threads):
     torch.cuda.synchronize()
     d2h = 4 * src.nbytes / (time.perf_counter() - t0) / 1e9
     r = bench.keyed_host_c5(lib, comm, steps=3)
+    rp = bench.keyed_host_c5(lib, comm, steps=3, pinned=True)
     print(json.dumps({'mode': mode, 'cpus': len(pick), 'gpu_bdf': bdf, 'gpu_node': gnode,
                       'host_copy_threads': threads, 'memcpy_1thread_GBs': round(memcpy_gbs, 1),
                       'h2d_GBs': round(h2d, 1), 'd2h_GBs': round(d2h, 1), 'keyed_host_c5_ms': r['ms'],
-                      'keyed_host_c5_GiBs': r['bucket_GiBs']}), flush=True)
+                      'keyed_host_c5_GiBs': r['bucket_GiBs'], 'engine_thread': r['engine_thread'],
+                      'keyed_host_c5_pinned_ms': rp['ms'], 'pinned_engine_thread': rp['engine_thread']}), flush=True)
 
 
 if __name__ == '__main__':
