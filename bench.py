@@ -838,6 +838,28 @@ def multi_gpu(args):
                                                 'busbw_GBs': round(2 * (world - 1) / world * S / sec_rccl / 1e9, 2)}
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['rccl_comparator'] = repr(e)[:400]
+    # CUs left to RCCL (config compute_cu_mask): the same allreduce on a communicator
+    # whose executor's compute stream avoids every 8th CU, beside the world's (all CUs); the mask is
+    # read when an executor is created, so a split over every rank carries it
+    state['leg'] = 'compute_cu_mask_ab'
+    try:
+        if not args.rehearse:
+            check(lib.ddl_set_config(b'compute_cu_mask', 8), 'ddl_set_config')
+            sub = comm.split_communicator(0, rank)
+            check(lib.ddl_set_config(b'compute_cu_mask', 0), 'ddl_set_config')
+
+            def sub_step():
+                check(lib.ddl_allreduce(sub.id, send.data_ptr(), recv.data_ptr(), n, DT_FLOAT, 0, stream.cuda_stream),
+                      'ddl_allreduce (masked)')
+            reps = max(5, args.steps // 2)
+            t_masked = timed_fn(sub_step, reps, 3)  # the first warmup call tunes the new communicator
+            t_world = timed_fn(lambda: step(0), reps, 3)
+            out['compute_cu_mask_ab'] = {'every_8th_cu_off_ms': round(t_masked * 1e3, 4),
+                                         'all_cus_ms': round(t_world * 1e3, 4),
+                                         'speedup_masked': round(t_world / t_masked, 4)}
+            sub.detach()
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['compute_cu_mask_ab'] = repr(e)[:400]
     # fixed schedules, tuner off (every rank sets the same values in the same order: the
     # schedule must be identical on all ranks)
     state['leg'] = 'schedule_sweep'

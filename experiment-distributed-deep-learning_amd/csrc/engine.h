@@ -102,11 +102,12 @@ struct Config {
     // key "capture_forked" (1 / 0) is the r02/r03 spelling of modes 1 / 0.
     std::atomic<long long> capture_mode{0};
     // multi-rank executors' compute streams (the reduce / fold kernels that overlap RCCL's send /
-    // recv kernels) run on all CUs but every n-th (n = 2, 4, 8; 0 = all CUs): those stay free for
-    // RCCL. The kernels keep their full HBM rate on such masks (tools/cu_mask_probe.py: 6.56-6.59
-    // vs 6.59 TB/s). Read when an executor is created (a communicator's first
-    // collective); local — it changes no program.
-    std::atomic<long long> compute_cu_mask{8};
+    // recv kernels) run on all CUs but every n-th (n = 2, 4, 8; 0 = all CUs, the default): those
+    // stay free for RCCL. The kernels keep their full HBM rate on such masks (tools/cu_mask_probe.py:
+    // 6.56-6.59 vs 6.59 TB/s), but a CU-masked stream takes a hardware queue of its own: 8 processes
+    // sharing one GPU ran their collectives 2.6x slower with it — off until a node
+    // measures it (bench leg compute_cu_mask_ab). Read when an executor is created; local.
+    std::atomic<long long> compute_cu_mask{0};
     // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'

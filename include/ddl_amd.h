@@ -137,10 +137,11 @@ int ddl_is_initialized(void);
  * hipGraph capture the program is posted serially on the captured stream — one chain; 2: as a
  * single-stream DAG, every op on the captured stream with its dependencies set explicitly, which
  * keeps the recv / reduce / send overlap in the graph; 1: on the forked comm / compute streams —
- * DESIGN §9; "capture_forked" 1 / 0 is the older spelling of modes 1 / 0), "compute_cu_mask" (8,
- * default: the compute streams of multi-rank executors — the reduce / fold kernels that overlap
- * RCCL's send / recv kernels — run on every CU but each 8th, which stay free for RCCL; 2 / 4: every
- * 2nd / 4th; 0: all CUs; read when a communicator's executor is created), "fold_form" (0, default:
+ * DESIGN §9; "capture_forked" 1 / 0 is the older spelling of modes 1 / 0), "compute_cu_mask" (0,
+ * default: all CUs; 8 / 4 / 2: the compute streams of multi-rank executors and handlers — the
+ * reduce / fold / pack kernels that overlap RCCL's send / recv kernels — avoid every 8th / 4th /
+ * 2nd CU, which stay free for RCCL; each masked stream takes a hardware queue of its own; read
+ * when a communicator's executor / handler is created), "fold_form" (0, default:
  * the N-input fold in its run form above 8 MiB chunks of 7+ inputs, its tile form otherwise; 1 /
  * 2: always the tile / run form),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack

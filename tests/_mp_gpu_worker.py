@@ -523,6 +523,10 @@ def worker(rank, world, port, q):
         from ddl.torch.cpp_backend import CPPBackend, check
         lib = CPPBackend.c_api()
         import gloo_transport
+        # engine placement knobs for A/B runs (read when the executors / handlers are created)
+        for env, key in (('DDL_MP_NUMA_BIND', b'host_numa_bind'), ('DDL_MP_CU_MASK', b'compute_cu_mask')):
+            if os.environ.get(env):
+                check(lib.ddl_set_config(key, int(os.environ[env])), 'ddl_set_config')
         cbs = gloo_transport.init_world(lib, dist, torch, rank, world)  # noqa: F841 (keep alive)
         comm = Communicator.world()
         assert comm.size == world and comm.rank == rank

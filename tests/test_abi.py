@@ -114,10 +114,10 @@ def test_config_roundtrip(lib):
     assert lib.ddl_get_config(b'capture_mode') == 1 and lib.ddl_get_config(b'capture_forked') == 1
     assert lib.ddl_set_config(b'capture_forked', 0) == 0
     assert lib.ddl_get_config(b'capture_mode') == 0
-    # multi-rank compute streams leave every 8th CU to RCCL by default; 0, 2, 4, 8 accepted
-    assert lib.ddl_get_config(b'compute_cu_mask') == 8
+    # multi-rank compute streams on every CU by default (8 / 4 / 2: leave every n-th to RCCL)
+    assert lib.ddl_get_config(b'compute_cu_mask') == 0
     assert lib.ddl_set_config(b'compute_cu_mask', 3) == 3
-    for v in (0, 2, 4, 8):
+    for v in (2, 4, 8, 0):
         assert lib.ddl_set_config(b'compute_cu_mask', v) == 0 and lib.ddl_get_config(b'compute_cu_mask') == v
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
