@@ -848,7 +848,7 @@ def multi_gpu(args):
     # read when an executor is created, so a split over every rank carries it
     state['leg'] = 'compute_cu_mask_ab'
     try:
-        if not args.rehearse:
+        if True:  # (rehearsed too: the split and the masked executor run; the times mean nothing there)
             check(lib.ddl_set_config(b'compute_cu_mask', 8), 'ddl_set_config')
             sub = comm.split_communicator(0, rank)
             check(lib.ddl_set_config(b'compute_cu_mask', 0), 'ddl_set_config')
