@@ -337,12 +337,12 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
     schedule's reduce; algorithmic bytes (nb + 2) * chunk. order 0: left fold; 1: MPICH's
     pre-fold + pairwise tree (reference_order at P = 8). `half`: the fp16 fold of C4 (inputs
     widened to fp32, one rounding). `form` (config fold_form): 0 the engine's choice (k_sumN_run
-    above 8 MiB chunks of 7+ inputs, k_sumN_tile otherwise), 1 the tile form, 2 the run form."""
+    from 4 MiB chunks of 7+ inputs, k_sumN_tile otherwise), 1 the tile form, 2 the run form."""
     import torch
     from ddl.torch.cpp_backend import check
     es = 2 if half else 4
     n = S // 8 // es
-    run_form = form == 2 or (form == 0 and n * es > (8 << 20) and nb + 1 >= 7)
+    run_form = form == 2 or (form == 0 and n * es >= (4 << 20) and nb + 1 >= 7)
     old_form = lib.ddl_get_config(b'fold_form')
     check(lib.ddl_set_config(b'fold_form', form), 'ddl_set_config fold_form')
     sets = [[torch.rand(n, device=dev).to(torch.float16 if half else torch.float32) for _ in range(nb + 2)]
@@ -817,7 +817,7 @@ def multi_gpu(args):
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
                      'kernel': (f'k_sumN_run / k_sumN_tile<float,{world - 1}> ({tune["chosen"]["algo"]} fold; run form '
-                                f'above 8 MiB slices at P >= 7)'
+                                f'from 4 MiB slices at P >= 7)'
                                 if tune and tune['chosen']['algo'] != 'ring' else
                                 'k_sum2_tile<float> (reduce-scatter step, all rings in one launch)'),
                      'avg_kernel_ms': round(avg_kernel_ms, 4), 'launches_timed': launches.value},

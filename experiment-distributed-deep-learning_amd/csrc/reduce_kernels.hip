@@ -442,20 +442,22 @@ __global__ void __launch_bounds__(kFoldThreads) k_sumN_run(SegTableN t) {
     }
 }
 
-// Fold form (config "fold_form", set_fold_form): the run form for chunks above kFoldRunMinBytes
-// of at least kFoldRunMinInputs inputs in the left or MPICH-tree order, the tile form otherwise.
-// Small chunks are cache-resident and latency bound (more, smaller workgroups); the binomial
-// order is for <= 2 KiB; and below 7 inputs the run form measured no better or worse than the
-// tile form (tools/stream_mix.hip rform, two boxes: 8:1 +2.5 to +10 %, 7:1 0 to +2 %, 2:1 to
-// 6:1 -3 to +1 %; profiles/r03/stream_mix/).
-constexpr size_t kFoldRunMinBytes = 8u << 20;
+// Fold form (config "fold_form", set_fold_form): the run form for chunks of at least
+// kFoldRunMinBytes with at least kFoldRunMinInputs inputs in the left or MPICH-tree order, the
+// tile form otherwise. P = 8 fp32 (tools/fold_form_sizes.py): run 7.0 vs tile 8.1-8.5 us at 4 MiB,
+// 12.1-12.3 vs 12.8 at 8 MiB, 22.7 vs 24.8-25.4 at 16 MiB, but 4.0 vs 3.2 at 2 MiB, where 128
+// workgroups cannot cover one memory round trip the way 1025 do. The binomial order is for
+// <= 2 KiB; and below 7 inputs the run form measured no better or worse than the tile form
+// (tools/stream_mix.hip rform, two boxes: 8:1 +2.5 to +10 %, 7:1 0 to +2 %, 2:1 to 6:1 -3 to
+// +1 %; profiles/r03/stream_mix/).
+constexpr size_t kFoldRunMinBytes = 4u << 20;
 constexpr int kFoldRunMinInputs = 7;
 std::atomic<int> g_fold_form{0};
 bool fold_run_form(size_t chunk_bytes, int order, int inputs) {
     if (order == kFoldBinomial) return false;
     const int f = g_fold_form.load(std::memory_order_relaxed);
     if (f != 0) return f == 2;
-    return chunk_bytes > kFoldRunMinBytes && inputs >= kFoldRunMinInputs;
+    return chunk_bytes >= kFoldRunMinBytes && inputs >= kFoldRunMinInputs;
 }
 
 // Half types fold left in fp32 whatever the order: only kFoldLeft is instantiated for them.

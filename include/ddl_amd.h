@@ -142,7 +142,7 @@ int ddl_is_initialized(void);
  * reduce / fold / pack kernels that overlap RCCL's send / recv kernels — avoid every 8th / 4th /
  * 2nd CU, which stay free for RCCL; each masked stream takes a hardware queue of its own; read
  * when a communicator's executor / handler is created), "fold_form" (0, default:
- * the N-input fold in its run form above 8 MiB chunks of 7+ inputs, its tile form otherwise; 1 /
+ * the N-input fold in its run form from 4 MiB chunks of 7+ inputs, its tile form otherwise; 1 /
  * 2: always the tile / run form),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a

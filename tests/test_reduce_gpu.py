@@ -212,7 +212,7 @@ def test_reduce_fold_ordered_kernel(lib, oracle, gpu, dt, nb, order, n, misalign
     assert got.tobytes() == want.tobytes()
 
 
-# the run form of the fold (reduce_kernels.hip k_sumN_run: chunks above 8 MiB of 7+ inputs, a workgroup walks
+# the run form of the fold (reduce_kernels.hip k_sumN_run: chunks from 4 MiB with 7+ inputs, a workgroup walks
 # the inputs one at a time over a 16 KiB run): every dtype, 2..16 inputs, the left fold and MPICH's
 # tree, chunk sizes a whole number of runs plus a ragged tail and not
 RUN_BYTES = [(9 << 20) + 16 * 1024 * 3, (9 << 20) + 4096 + 48]
@@ -224,7 +224,7 @@ RUN_BYTES = [(9 << 20) + 16 * 1024 * 3, (9 << 20) + 4096 + 48]
 @pytest.mark.parametrize('nbytes', RUN_BYTES + [4100 * 4, 1 << 20], ids=['whole_runs+tail', 'ragged', 'small',
                                                                          '1MiB'])
 def test_reduce_fold_run_form(lib, oracle, gpu, dt, nb, order, nbytes):
-    """The run form (the default above 8 MiB at 7+ inputs) forced for every width and size (config
+    """The run form (the default from 4 MiB at 7+ inputs) forced for every width and size (config
     fold_form 2), so its tails are checked at sizes of one run and less too."""
     from _helpers import config
     es = {1: 4, 2: 8, 3: 4, 9: 8, 14: 2, 19: 2, 23: 8}[dt]
@@ -236,7 +236,7 @@ def test_reduce_fold_run_form(lib, oracle, gpu, dt, nb, order, nbytes):
 @pytest.mark.parametrize('dt', [1, 14])
 @pytest.mark.parametrize('nb', [2, 7])
 def test_reduce_fold_tile_form_forced_large(lib, oracle, gpu, dt, nb):
-    """config fold_form 1 keeps the tile form above 8 MiB (the A/B the bench reports)."""
+    """config fold_form 1 keeps the tile form at large chunks (the A/B the bench reports)."""
     from _helpers import config
     es = 4 if dt == 1 else 2
     with config(lib, fold_form=1):
