@@ -118,6 +118,8 @@ hipStream_t create_compute_stream(int every) {
         std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
         for (int c = 0; c < ncu; ++c)
             if (c % every != every - 1) mask[(size_t)c / 32] |= 1u << (c % 32);
+        // (hipExtStreamCreateWithCUMask takes no flags: the masked stream is a blocking one, ordered
+        // with the legacy NULL stream, where the unmasked one below is non-blocking)
         if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return s;
         (void)hipGetLastError();  // a runtime without CU masks: an ordinary stream
         DDL_LOG(1, "compute_cu_mask " << every << ": hipExtStreamCreateWithCUMask failed, using an unmasked stream");
