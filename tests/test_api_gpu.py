@@ -413,3 +413,51 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     finally:
         for k, v in old.items():
             lib.ddl_set_config(k, v)
+
+
+def _cpulist(text):
+    out = set()
+    for part in text.strip().split(','):
+        if part:
+            a, _, b = part.partition('-')
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def test_host_threads_bound_to_gpu_numa_node(world, lib):
+    """config host_numa_bind (default on): after a keyed host plan, the handler's engine thread and
+    copy threads run on the CPUs of the GPU's NUMA node (within the process's affinity) — where
+    HIP places pinned host memory. Skipped where that would not narrow the set."""
+    import glob
+    import os
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    p = torch.cuda.get_device_properties(0)
+    bdf = f'{getattr(p, "pci_domain_id", 0):04x}:{getattr(p, "pci_bus_id", 0):02x}:{getattr(p, "pci_device_id", 0):02x}.0'
+    try:
+        node = int(open(f'/sys/bus/pci/devices/{bdf}/numa_node').read())
+        local = _cpulist(open(f'/sys/devices/system/node/node{node}/cpulist').read())
+    except (OSError, ValueError):
+        pytest.skip('no NUMA information for the GPU')
+    allowed = os.sched_getaffinity(0)
+    want = local & allowed
+    if node < 0 or not want or want == allowed:
+        pytest.skip('binding would not narrow the CPU set here')
+    assert lib.ddl_get_config(b'host_numa_bind') == 1
+    old = lib.ddl_get_config(b'one_rank_shortcut')
+    try:
+        assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
+        xs = [torch.randn(300_001) for _ in range(3)]  # host tensors: the copy threads run
+        for h in allreduce_async_batch(xs, [f'numa_{i}' for i in range(3)], world):
+            h.wait(timeout=60)
+    finally:
+        lib.ddl_set_config(b'one_rank_shortcut', old)
+    bound = 0
+    for st in glob.glob(f'/proc/{os.getpid()}/task/*/status'):
+        try:
+            line = [x for x in open(st) if x.startswith('Cpus_allowed_list:')][0]
+        except (OSError, IndexError):
+            continue
+        if _cpulist(line.split(':', 1)[1]) == want:
+            bound += 1
+    # the engine thread, plus the copy threads (host_copy_threads, default 7)
+    assert bound >= 1 + lib.ddl_get_config(b'host_copy_threads'), (bound, sorted(want)[:4])
