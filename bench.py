@@ -616,7 +616,7 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
         step()
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
-        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us')
+        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us', b'host_check_us', b'host_plan_us')
         tl0 = [lib.ddl_get_config(kk) for kk in tl_keys]
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -627,8 +627,12 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
         # for a slot's DMA / device work, unpacking staged results; the rest is negotiation,
         # planning and posting
         tl = [(lib.ddl_get_config(kk) - v) / steps / 1e3 for kk, v in zip(tl_keys, tl0)]
+        # plan_ms: the allreduce plans' staging loops (pack + slot waits + unpack + posting);
+        # outside them: the pinned-output checks (check_ms), and the rest — submission,
+        # negotiation, planning, the last chunks' device work after the loop, done() (rest_ms)
         timeline = {'pack_ms': round(tl[0], 3), 'slot_wait_ms': round(tl[1], 3), 'unpack_ms': round(tl[2], 3),
-                    'other_ms': round(dt * 1e3 - sum(tl), 3)}
+                    'other_ms': round(dt * 1e3 - sum(tl[:3]), 3), 'check_ms': round(tl[3], 3),
+                    'plan_ms': round(tl[4], 3), 'rest_ms': round(dt * 1e3 - tl[3] - tl[4], 3)}
         registered = {'host_registered_bytes': int(lib.ddl_get_config(b'host_registered_bytes')),
                       'host_register_failures': int(lib.ddl_get_config(b'host_register_failures'))}
     finally:

@@ -397,6 +397,8 @@ long long ddl_get_config(const char *key) {
     if (k == "host_pack_us") return c.host_pack_ns / 1000;      // statistic, not settable
     if (k == "host_wait_us") return c.host_wait_ns / 1000;      // statistic, not settable
     if (k == "host_unpack_us") return c.host_unpack_ns / 1000;  // statistic, not settable
+    if (k == "host_check_us") return c.host_check_ns / 1000;    // statistic, not settable
+    if (k == "host_plan_us") return c.host_plan_ns / 1000;      // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;

@@ -73,6 +73,10 @@ struct Config {
     std::atomic<long long> host_pack_ns{0};  // read as microseconds (host_pack_us, ...)
     std::atomic<long long> host_wait_ns{0};
     std::atomic<long long> host_unpack_ns{0};
+    // keyed host allreduce plans: the pinned-output check before each plan, and the whole of
+    // each plan's staging loop (pack, slot waits, posting, unpack; host_plan_us)
+    std::atomic<long long> host_check_ns{0};
+    std::atomic<long long> host_plan_ns{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};

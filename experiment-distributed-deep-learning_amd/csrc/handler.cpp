@@ -894,7 +894,20 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     const size_t chunk = host_slots_(total);
     pool_for_config_();
     if (device_unpack) config().host_zero_copy_plans.fetch_add(1);
-    const size_t nchunks = (total + chunk - 1) / chunk;
+    // chunk boundaries (multiples of 256, the same on every rank: the per-chunk collectives must
+    // match): whole chunks, and the last two chunks' worth of a plan longer than that in quarter
+    // chunks — the device work still in flight when the loop ends (the pipeline's drain, ~3 ms of
+    // the pinned C5 batch with 32 MiB chunks) is then a quarter as long
+    std::vector<size_t> cut{0};
+    {
+        const size_t piece = std::max<size_t>(256, (chunk / 4) & ~size_t(255));
+        while (cut.back() < total) {
+            const size_t left = total - cut.back();
+            const size_t n = (total <= 2 * chunk || left > 2 * chunk) ? std::min(chunk, left) : std::min(piece, left);
+            cut.push_back(cut.back() + n);
+        }
+    }
+    const size_t nchunks = cut.size() - 1;
     std::vector<CopyPool::Piece> pieces;
     // timeline statistics (config "host_pack_us" / "host_wait_us" / "host_unpack_us"): where the
     // engine thread spends a host plan — packing chunks, waiting for a slot's DMA / device work,
@@ -909,9 +922,9 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         DDL_HIP(hipEventSynchronize(hev_[3 * k + 2]));  // D2H of chunk j landed
         config().host_wait_ns.fetch_add(ns_since(t0));
         t0 = clk::now();
-        const size_t off = j * chunk;
+        const size_t off = cut[j];
         pieces.clear();
-        host_pieces_(segs, starts, off, std::min(chunk, total - off), static_cast<char *>(pin_[k]), false, pieces);
+        host_pieces_(segs, starts, off, cut[j + 1] - off, static_cast<char *>(pin_[k]), false, pieces);
         pool_->run(pieces);
         config().host_unpack_ns.fetch_add(ns_since(t0));
     };
@@ -931,7 +944,7 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     for (size_t i = 0; i < nchunks; ++i) {
         const int k = (int)(i % kHostSlots);
         if (i >= (size_t)kHostSlots && !device_unpack) unpack(i - kHostSlots);  // frees slot k (pinned and device)
-        const size_t off = i * chunk, n = std::min(chunk, total - off);
+        const size_t off = cut[i], n = cut[i + 1] - off;
         // the device slot's last user may still be in flight (a device unpack)
         if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
         if (upload) {
@@ -1157,8 +1170,15 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     auto coll = [&](void *d, size_t elems) {
                         data_->allreduce(d, d, elems, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
                     };
-                    host_staged_(segs, es, true, coll, true,
-                                 config().host_zero_copy.load() && mapped_host_dsts_(segs));
+                    const auto t_check = std::chrono::steady_clock::now();
+                    const bool mapped = config().host_zero_copy.load() && mapped_host_dsts_(segs);
+                    const auto t_plan = std::chrono::steady_clock::now();
+                    config().host_check_ns.fetch_add(
+                        std::chrono::duration_cast<std::chrono::nanoseconds>(t_plan - t_check).count());
+                    host_staged_(segs, es, true, coll, true, mapped);
+                    config().host_plan_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                        std::chrono::steady_clock::now() - t_plan)
+                                                        .count());
                 }
             } else if (data_->size() == 1 && config().one_rank_shortcut.load()) {
                 // a one-rank world: the sum is the input; move bytes only where out != in
