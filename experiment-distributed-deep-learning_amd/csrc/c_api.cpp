@@ -334,6 +334,9 @@ int ddl_set_config(const char *key, long long value) {
         else if (k == "host_chunk_bytes") {
             DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
             c.host_chunk_bytes = value;
+        } else if (k == "host_taper") {
+            DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT, "host_taper must be 0, 1 or 2");
+            c.host_taper = value;
         } else if (k == "host_copy_threads") {
             DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
             c.host_copy_threads = value;
@@ -385,6 +388,7 @@ long long ddl_get_config(const char *key) {
     if (k == "log_level") return c.log_level;
     if (k == "cycle_time_us") return c.cycle_time_us;
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
+    if (k == "host_taper") return c.host_taper;
     if (k == "tune") return c.tune;
     if (k == "host_copy_threads") return c.host_copy_threads;
     if (k == "host_zero_copy") return c.host_zero_copy;
@@ -872,6 +876,17 @@ int ddl_testing_compute_stream_cus(int every, int *enabled, int *total) {
         for (int c = 0; c < ncu; ++c) on += (mask[(size_t)c / 32] >> (c % 32)) & 1u;
         *enabled = on;
         *total = ncu;
+    });
+}
+
+int ddl_testing_host_chunk_cuts(size_t total_bytes, size_t chunk_bytes, size_t *cuts, size_t cap, size_t *count) {
+    return guarded([&] {
+        DDL_REQUIRE(count && (cuts || cap == 0), DDL_STATUS_INVALID_ARGUMENT, "null output");
+        DDL_REQUIRE(chunk_bytes >= 256 && chunk_bytes % 256 == 0, DDL_STATUS_INVALID_ARGUMENT,
+                    "chunk_bytes " << chunk_bytes << " is not a positive multiple of 256");
+        const std::vector<size_t> cut = host_chunk_cuts(total_bytes, chunk_bytes, (int)config().host_taper.load());
+        for (size_t i = 0; i < cut.size() && i < cap; ++i) cuts[i] = cut[i];
+        *count = cut.size();
     });
 }
 

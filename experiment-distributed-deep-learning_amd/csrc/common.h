@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <string>
@@ -142,9 +143,10 @@ enum ReduceVariant : int {
 };
 int default_variant(size_t bytes);  // standalone reduce (ddl_reduce_local / ddl_reduce_sum2), by bucket size
 int ring_variant();     // reduce-scatter step of the ring
-// Form of the N-input fold (config "fold_form"): 0 auto (the run form above 8 MiB chunks), 1 the
-// tile form always, 2 the run form always (the binomial order is always tiled). Local: it changes
-// no collective's program, only the kernel (the same sums either way).
+// Form of the N-input fold (config "fold_form"): 0 auto (the run form for chunks of at least 4 MiB
+// and at least 7 inputs), 1 the tile form always, 2 the run form always (the binomial order is
+// always tiled). Local: it changes no collective's program, only the kernel (the same sums either
+// way).
 void set_fold_form(int form);
 int get_fold_form();
 
@@ -158,6 +160,28 @@ int device_cu_count();
 // captured node yet, once that stream has captured nodes since (tools/capture_replay.hip bisected
 // the engine's own program to that wait; profiles/r03/graph/).
 void launch_capture_anchor(hipStream_t stream);
+
+// Chunk boundaries [cut[i], cut[i + 1]) of a host-staged transfer of `total` bytes through
+// `chunk`-byte slots (chunk a multiple of 256): whole chunks (taper 0, config "host_taper"
+// default); with taper 1 the last two chunks' worth of a transfer longer than two chunks, and with
+// taper 2 also the first chunk's worth of one longer than three, are cut in quarter chunks. That
+// shortens the pipeline's fill (the first chunk's pack and upload, before any other engine has
+// work) and drain (the device work and download still in flight when the host loop ends), but
+// quarter chunks keep a quarter as many bytes in the slots in flight: measured on one box,
+// interleaved, whole chunks were as fast or faster. Boundaries are multiples of 256
+// that depend only on (total, chunk, taper) — a shared tunable — so every rank cuts the same
+// chunks (the per-chunk collectives must match).
+inline std::vector<size_t> host_chunk_cuts(size_t total, size_t chunk, int taper) {
+    std::vector<size_t> cut{0};
+    const size_t piece = std::max<size_t>(256, (chunk / 4) & ~size_t(255));
+    while (cut.back() < total) {
+        const size_t at = cut.back(), left = total - at;
+        const bool quarter = (taper >= 1 && total > 2 * chunk && left <= 2 * chunk) ||
+                             (taper >= 2 && total > 3 * chunk && at < chunk);
+        cut.push_back(at + std::min(quarter ? piece : chunk, left));
+    }
+    return cut;
+}
 
 // Gather (dir 0: segments -> flat) / scatter (dir 1: flat -> segments) between tensors and a
 // fusion buffer in one launch (pack.hip). Segment i sits at the running sum of the 256-byte-

@@ -39,7 +39,7 @@ Config &config() {
 uint64_t Config::shared_hash() const {
     const long long v[] = {algo.load(), slice_bytes.load(), rings.load(), max_slices.load(),
                            fusion_threshold_bytes.load(), tune.load(), fusion_pipeline_bytes.load(),
-                           reference_order.load(), host_chunk_bytes.load()};
+                           reference_order.load(), host_chunk_bytes.load(), host_taper.load()};
     uint64_t h = 1469598103934665603ull;  // FNV-1a over the values' bytes
     for (long long x : v)
         for (int b = 0; b < 8; ++b) {
@@ -187,7 +187,7 @@ void check_config_agreement(int rank, const std::vector<uint64_t> &hashes) {
     if (same) return;
     std::ostringstream os;
     os << "shared tunables differ between ranks (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, "
-          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes must be set alike on every rank); "
+          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes, host_taper must be set alike on every rank); "
           "config hash per rank:";
     for (size_t q = 0; q < hashes.size(); ++q)
         os << " " << q << (q == (size_t)rank ? "*" : "") << "=" << std::hex << hashes[q] << std::dec;
@@ -512,11 +512,14 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
         }
         RingConfig cfg = ring_config(chunk / es, dtype, ring_);
         cfg.order_bytes = total;  // the reference reduces the whole host buffer in one call
-        const size_t nchunks = (total + chunk - 1) / chunk;
+        // whole chunks, or quarter chunks at the ends ("host_taper": the first H2D runs alone
+        // before any D2H can overlap it, and so does the last D2H; measured no faster)
+        const std::vector<size_t> cut = host_chunk_cuts(total, chunk, (int)config().host_taper.load());
+        const size_t nchunks = cut.size() - 1;
         for (size_t i = 0; i < nchunks; ++i) {
             const int s = (int)(i % kHostSlots);
             hipEvent_t &h2d_done = ev[3 * s], &ring_done = ev[3 * s + 1], &d2h_done = ev[3 * s + 2];
-            const size_t off = i * chunk, bytes = total - off < chunk ? total - off : chunk;
+            const size_t off = cut[i], bytes = cut[i + 1] - off;
             if (i >= (size_t)kHostSlots) DDL_HIP(hipStreamWaitEvent(h2d_, d2h_done, 0));  // slot free again
             DDL_HIP(hipMemcpyAsync(slots_[s], static_cast<const char *>(send) + off, bytes, hipMemcpyHostToDevice, h2d_));
             DDL_HIP(hipEventRecord(h2d_done, h2d_));

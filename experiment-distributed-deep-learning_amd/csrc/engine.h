@@ -36,6 +36,10 @@ struct Config {
     std::atomic<long long> cycle_time_us{0};
     // host-resident pipeline chunk (ddl_allreduce_host, keyed host requests)
     std::atomic<long long> host_chunk_bytes{32ll << 20};
+    // quarter chunks at the ends of a long host-staged transfer (host_chunk_cuts): 0 whole chunks
+    // only (default: fastest in the interleaved A/B, profiles/r03/host/host_taper_ab.jsonl), 1 the
+    // last two chunks' worth, 2 that and the first chunk's worth
+    std::atomic<long long> host_taper{0};
     // memcpy workers of the keyed host-staging pipeline (pageable <-> pinned), besides the
     // engine thread itself
     std::atomic<long long> host_copy_threads{7};
@@ -116,7 +120,8 @@ struct Config {
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'
     // programs, the fusion plans and the host chunks): algo, slice_bytes, rings, max_slices,
-    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes.
+    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes,
+    // host_taper.
     // Never 0 or kCfgMismatch. Local tunables (log_level, cycle_time_us, host_copy_threads,
     // host_zero_copy, pipeline_rounds, one_rank_shortcut) are not in it.
     uint64_t shared_hash() const;

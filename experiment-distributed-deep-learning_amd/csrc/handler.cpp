@@ -894,19 +894,9 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     const size_t chunk = host_slots_(total);
     pool_for_config_();
     if (device_unpack) config().host_zero_copy_plans.fetch_add(1);
-    // chunk boundaries (multiples of 256, the same on every rank: the per-chunk collectives must
-    // match): whole chunks, and the last two chunks' worth of a plan longer than that in quarter
-    // chunks — the device work still in flight when the loop ends (the pipeline's drain, ~3 ms of
-    // the pinned C5 batch with 32 MiB chunks) is then a quarter as long
-    std::vector<size_t> cut{0};
-    {
-        const size_t piece = std::max<size_t>(256, (chunk / 4) & ~size_t(255));
-        while (cut.back() < total) {
-            const size_t left = total - cut.back();
-            const size_t n = (total <= 2 * chunk || left > 2 * chunk) ? std::min(chunk, left) : std::min(piece, left);
-            cut.push_back(cut.back() + n);
-        }
-    }
+    // chunk boundaries (the same on every rank): whole chunks, or quarter chunks at the ends of a
+    // long plan ("host_taper")
+    const std::vector<size_t> cut = host_chunk_cuts(total, chunk, (int)config().host_taper.load());
     const size_t nchunks = cut.size() - 1;
     std::vector<CopyPool::Piece> pieces;
     // timeline statistics (config "host_pack_us" / "host_wait_us" / "host_unpack_us"): where the

@@ -117,7 +117,10 @@ int ddl_is_initialized(void);
 /* Tunables: "algo" (0 multi-ring, 1 direct all-to-all, 2 one-shot, 3 gather-fold: one
  * ncclAllGather then the rank-order fold, 4 direct-gather: the direct reduce-scatter then one
  * in-place ncclAllGather of the reduced chunks when they are equal), "slice_bytes", "rings", "max_slices",
- * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "tune",
+ * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "host_taper" (0,
+ * default: whole chunks; 2: quarter chunks for the first chunk's worth and the last two chunks'
+ * worth of a long host-staged transfer, a shorter pipeline fill and drain but less in flight —
+ * measured no faster; 1: the last two only), "tune",
  * "host_copy_threads" (memcpy workers of the keyed host staging), "host_zero_copy" (1, default:
  * a keyed host allreduce plan whose outputs are all pinned and mapped on the device — torch
  * pin_memory, hipHostMalloc, hipHostRegister — is unpacked by the fusion kernel straight into
@@ -157,7 +160,7 @@ int ddl_is_initialized(void);
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
  * The shared tunables (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, tune,
- * fusion_pipeline_bytes, reference_order, host_chunk_bytes) must be equal on every rank of a
+ * fusion_pipeline_bytes, reference_order, host_chunk_bytes, host_taper) must be equal on every rank of a
  * communicator: the ranks agree on a hash of them at a communicator's first collective and
  * whenever this rank's values changed since (change them on every rank between the same two
  * collectives), and every keyed round carries the hash; on a mismatch the collective or round

@@ -142,6 +142,10 @@ int ddl_testing_drop_wait(int tick);
 /* The CUs enabled on an executor compute stream created with every `every`-th CU masked off
  * (config "compute_cu_mask"; 0 = unmasked), read back with hipExtStreamGetCUMask. */
 int ddl_testing_compute_stream_cus(int every, int *enabled, int *total);
+/* The chunk boundaries of a host-staged transfer (ddl_allreduce_host, the keyed handler's host
+ * plans) under the current "host_taper": writes min(count, cap) boundaries cut[0] = 0 < ... < cut[count - 1] = total_bytes into
+ * cuts and sets *count. Pure host arithmetic (no device). */
+int ddl_testing_host_chunk_cuts(size_t total_bytes, size_t chunk_bytes, size_t *cuts, size_t cap, size_t *count);
 
 /* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
  * A one-rank RCCL communicator (ncclGetUniqueId + ncclCommInitRank, the calls ddl_init makes at

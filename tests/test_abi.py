@@ -122,6 +122,9 @@ def test_config_roundtrip(lib):
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
     assert lib.ddl_set_config(b'fold_form', 3) == 3
+    # host-staged transfers cut whole chunks by default (1: quarter chunks at the tail, 2: both ends)
+    assert lib.ddl_get_config(b'host_taper') == 0
+    assert lib.ddl_set_config(b'host_taper', 3) == 3
 
 
 def test_product_does_not_reference_oracle():
@@ -156,3 +159,50 @@ def test_library_is_built_from_these_sources(lib):
     lib.ddl_build_info.restype = ctypes.c_char_p
     info = lib.ddl_build_info().decode()
     assert info == f'src={conftest.source_hash()} arch=gfx950', info
+
+
+def _host_cuts(lib, total, chunk):
+    n = ctypes.c_size_t(0)
+    assert lib.ddl_testing_host_chunk_cuts(ctypes.c_size_t(total), ctypes.c_size_t(chunk), None,
+                                           ctypes.c_size_t(0), ctypes.byref(n)) == 0, lib.ddl_last_error()
+    buf = (ctypes.c_size_t * n.value)()
+    assert lib.ddl_testing_host_chunk_cuts(ctypes.c_size_t(total), ctypes.c_size_t(chunk), buf, ctypes.c_size_t(n.value),
+                                           ctypes.byref(n)) == 0, lib.ddl_last_error()
+    return list(buf)
+
+
+@pytest.mark.parametrize('taper', [2, 1, 0])
+@pytest.mark.parametrize('chunk', [4096, 1 << 20, 32 << 20, 768])
+def test_host_chunk_cuts(lib, chunk, taper):
+    """Host-staged transfers (ddl_allreduce_host, keyed host plans) cut whole chunks, with quarter
+    chunks ("host_taper" 2) for the first chunk's worth of a transfer longer than three
+    chunks and the last two chunks' worth of one longer than two (1: the tail only). Every boundary
+    but the end is a multiple of 256 (the dtype size divides 256), so every element lies in one
+    chunk and ranks cut alike."""
+    assert lib.ddl_set_config(b'host_taper', taper) == 0
+    try:
+        _check_cuts(lib, chunk, taper)
+    finally:
+        assert lib.ddl_set_config(b'host_taper', 0) == 0
+
+
+def _check_cuts(lib, chunk, taper):
+    lib.ddl_testing_host_chunk_cuts.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.c_void_p]
+    piece = max(256, (chunk // 4) & ~255)
+    for total in [1, 256, chunk - 8, chunk, chunk + 256, 2 * chunk, 2 * chunk + 256, 3 * chunk, 3 * chunk + 1024,
+                  8 * chunk, 8 * chunk + 4, 73 * chunk + 12345]:
+        cuts = _host_cuts(lib, total, chunk)
+        assert cuts[0] == 0 and cuts[-1] == total
+        sizes = [b - a for a, b in zip(cuts, cuts[1:])]
+        assert all(s > 0 for s in sizes)
+        assert all(c % 256 == 0 for c in cuts[:-1])
+        for a, s in zip(cuts, sizes):
+            left = total - a
+            tail = taper >= 1 and total > 2 * chunk and left <= 2 * chunk
+            head = taper >= 2 and total > 3 * chunk and a < chunk
+            assert s == min(piece if (head or tail) else chunk, left), (total, a, s)
+    head = _host_cuts(lib, 256 << 20, 32 << 20)[:3]
+    assert head == ([0, 8 << 20, 16 << 20] if taper == 2 else [0, 32 << 20, 64 << 20])
+    assert lib.ddl_testing_host_chunk_cuts(ctypes.c_size_t(1024), ctypes.c_size_t(100), None, ctypes.c_size_t(0),
+                                           ctypes.byref(ctypes.c_size_t())) != 0
