@@ -212,28 +212,29 @@ def check_keyed_host_requests(ctx):
     xs = [[h.random_input(dts[i], n, 900 + 31 * i + q) for q in range(P)] for i, n in enumerate(sizes)]
     gb = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
     dev_x = [h.random_input(h.DT_FLOAT, 4099, 4000 + q) for q in range(P)]
-    with h.config(lib, host_chunk_bytes=64 << 10, reference_order=1):
-        for rnd in range(4):
-            pin = rnd == 3 or (rnd == 2 and r % 2 == 0)
-            ts = [torch.from_numpy(xs[i][r].copy()) for i in range(len(sizes))]
-            if pin:
-                ts = [t.pin_memory() for t in ts]
-            order = np.random.default_rng(5 * rnd + r).permutation(len(sizes))
-            tensors = [ts[i] for i in order] + [torch.from_numpy(dev_x[r]).cuda()]
-            names = [f'host_{i}' for i in order] + ['dev_0']
-            outs = [t if (rnd % 2 == 1 and not t.is_cuda) else None for t in tensors]  # odd rounds: in place
-            plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
-            hs = allreduce_async_batch(tensors, names, comm,
-                                       outputs=[o if o is not None else torch.empty_like(t, pin_memory=pin and not t.is_cuda)
-                                                for o, t in zip(outs, tensors)])
-            for hd, i in zip(hs, order):
-                got = hd.wait(timeout=120)
-                assert not got.is_cuda
-                want = ora.fold_ref_order(dts[i], xs[i], gb[dts[i]])
-                assert got.numpy().tobytes() == want.tobytes(), (rnd, i)
-            assert hs[-1].wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, dev_x).tobytes()
-            # three host dtype groups, one plan each
-            assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == (3 if pin else 0), rnd
+    for taper in (0, 2):  # whole chunks (default) and quarter chunks at both ends
+        with h.config(lib, host_chunk_bytes=64 << 10, reference_order=1, host_taper=taper):
+            for rnd in range(4):
+                pin = rnd == 3 or (rnd == 2 and r % 2 == 0)
+                ts = [torch.from_numpy(xs[i][r].copy()) for i in range(len(sizes))]
+                if pin:
+                    ts = [t.pin_memory() for t in ts]
+                order = np.random.default_rng(5 * rnd + r).permutation(len(sizes))
+                tensors = [ts[i] for i in order] + [torch.from_numpy(dev_x[r]).cuda()]
+                names = [f'host_{i}' for i in order] + ['dev_0']
+                outs = [t if (rnd % 2 == 1 and not t.is_cuda) else None for t in tensors]  # odd rounds: in place
+                plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
+                hs = allreduce_async_batch(tensors, names, comm,
+                                           outputs=[o if o is not None else torch.empty_like(t, pin_memory=pin and not t.is_cuda)
+                                                    for o, t in zip(outs, tensors)])
+                for hd, i in zip(hs, order):
+                    got = hd.wait(timeout=120)
+                    assert not got.is_cuda
+                    want = ora.fold_ref_order(dts[i], xs[i], gb[dts[i]])
+                    assert got.numpy().tobytes() == want.tobytes(), (taper, rnd, i)
+                assert hs[-1].wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, dev_x).tobytes()
+                # three host dtype groups, one plan each
+                assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == (3 if pin else 0), (taper, rnd)
         hs, want = [], []
         for i in range(9):
             root, dt = i % P, [torch.float32, torch.int64, torch.float64][i % 3]
@@ -352,16 +353,18 @@ def check_keyed_broadcast_allgather(ctx):
 
 
 def check_host_resident(ctx):
-    """allreduce of a CPU tensor: the chunked H2D -> ring -> D2H pipeline (4 slots), many chunks."""
+    """allreduce of a CPU tensor: the chunked H2D -> ring -> D2H pipeline (4 slots), many chunks,
+    whole or tapered ("host_taper" 2: quarter chunks at both ends, cut alike on every rank)."""
     import _helpers as h
     torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
     from ddl.torch.tensor_communicate import allreduce
     n = 1_000_003
     base = torch.randint(-1000, 1000, (n,), generator=torch.Generator().manual_seed(9))
-    with h.config(lib, host_chunk_bytes=256 << 10):
-        got = allreduce((base + r).to(torch.float32), comm)
-    assert not got.is_cuda
-    assert torch.equal(got, (base * P + P * (P - 1) // 2).to(torch.float32))
+    for taper in (0, 2):  # whole chunks (default) and quarter chunks at both ends
+        with h.config(lib, host_chunk_bytes=256 << 10, host_taper=taper):
+            got = allreduce((base + r).to(torch.float32), comm)
+        assert not got.is_cuda
+        assert torch.equal(got, (base * P + P * (P - 1) // 2).to(torch.float32)), taper
 
 
 def check_dp_training(ctx):

@@ -36,15 +36,18 @@ def test_allreduce_host_tensor(world):
     assert not y.is_cuda and torch.equal(x, y)
 
 
+@pytest.mark.parametrize('taper', [0, 2])
 @pytest.mark.parametrize('chunk', [4096, 1 << 20, 32 << 20])
 @pytest.mark.parametrize('n,dtype', [(1, torch.float32), (1000, torch.float16), (3_000_001, torch.float32),
                                      (777_777, torch.int64)])
-def test_allreduce_host_pipeline(world, lib, chunk, n, dtype):
-    """Chunked H2D -> ring -> D2H pipeline (pageable input registered for the call)."""
+def test_allreduce_host_pipeline(world, lib, chunk, n, dtype, taper):
+    """Chunked H2D -> ring -> D2H pipeline (pageable input registered for the call), in whole
+    chunks or with quarter chunks at both ends ("host_taper" 2)."""
     from ddl.torch.cpp_backend import check
     from ddl.torch.util import ddl_dtype
     old = lib.ddl_get_config(b'host_chunk_bytes')
     assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
+    assert lib.ddl_set_config(b'host_taper', taper) == 0
     try:
         x = (torch.randn(n) * 1000).to(dtype)
         y = torch.zeros_like(x)
@@ -55,6 +58,7 @@ def test_allreduce_host_pipeline(world, lib, chunk, n, dtype):
         assert torch.equal(x, z)
     finally:
         lib.ddl_set_config(b'host_chunk_bytes', old)
+        lib.ddl_set_config(b'host_taper', 0)
 
 
 def test_allreduce_gradient_mean(world):
@@ -413,6 +417,17 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     finally:
         for k, v in old.items():
             lib.ddl_set_config(k, v)
+
+
+@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'mixed', 'registered'])
+def test_keyed_host_requests_tapered(world, lib, memory):
+    """The keyed host plans with quarter chunks at both ends ("host_taper" 2; 4 KiB chunks, so
+    1 KiB quarters at both ends of every group's plan): same outputs, same paths."""
+    assert lib.ddl_set_config(b'host_taper', 2) == 0
+    try:
+        test_keyed_host_requests_data_plane(world, lib, 4096, memory)
+    finally:
+        lib.ddl_set_config(b'host_taper', 0)
 
 
 def _cpulist(text):
