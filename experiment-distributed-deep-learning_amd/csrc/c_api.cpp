@@ -861,8 +861,48 @@ int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *co
     });
 }
 
+int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const *srcs, void *const *dsts,
+                                       const size_t *bytes, int dtype, void *hip_stream, size_t *subplans) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && count >= 1 && srcs && dsts && bytes, DDL_STATUS_INVALID_ARGUMENT,
+                    "bad thread fused allreduce");
+        const size_t es = dtype_size(dtype);
+        DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+        for (int i = 0; i < count; ++i)
+            DDL_REQUIRE(bytes[i] % es == 0, DDL_STATUS_INVALID_ARGUMENT, "segment " << i << " is not whole elements");
+        const size_t j = thread_world(nranks).fused_allreduce(srcs, dsts, bytes, count, dtype, as_stream(hip_stream),
+                                                              config().ring(),
+                                                              (size_t)config().fusion_pipeline_bytes.load());
+        if (subplans) *subplans = j;
+    });
+}
+
 int ddl_testing_drop_wait(int tick) {
     return guarded([&] { set_testing_drop_wait(tick); });
+}
+
+int ddl_testing_dep_trace(int on) {
+    return guarded([&] {
+        if (on) dep::start();
+        else dep::stop();
+    });
+}
+
+int ddl_testing_dep_check(long long *counts, char *report, size_t len) {
+    return guarded([&] {
+        DDL_REQUIRE(counts, DDL_STATUS_INVALID_ARGUMENT, "null counts");
+        const dep::Report r = dep::check();
+        counts[0] = r.ops;
+        counts[1] = r.conflicts;
+        counts[2] = r.ordered;
+        counts[3] = r.ordered_reduce;
+        counts[4] = r.races;
+        if (report && len) {
+            const size_t k = std::min(len - 1, r.first.size());
+            std::memcpy(report, r.first.data(), k);
+            report[k] = 0;
+        }
+    });
 }
 
 int ddl_testing_compute_stream_cus(int every, int *enabled, int *total) {

@@ -1,6 +1,8 @@
 // executor.cpp — see executor.h.
 #include "executor.h"
 
+#include "deptrace.h"
+
 #include <algorithm>
 #include <map>
 #include <thread>
@@ -42,10 +44,17 @@ void RcclTransport::group(const std::vector<P2POp> &ops, hipStream_t stream) {
     ncclResult_t e = api.GroupEnd();
     rccl_check(first_err, "ncclSend/ncclRecv");
     rccl_check(e, "ncclGroupEnd");
+    if (dep::on()) {
+        std::vector<dep::Access> acc;
+        for (const P2POp &op : ops) acc.push_back(op.send ? dep::rd(op.ptr, op.bytes) : dep::wr(op.ptr, op.bytes));
+        dep::op(stream, "rccl group", std::move(acc));
+    }
 }
 
 void RcclTransport::allgather(const GatherOp &g, hipStream_t stream) {
     rccl_check(rccl().AllGather(g.send, g.recv, g.bytes, ncclInt8, comm_, stream), "ncclAllGather");
+    // (the other ranks' blocks are written too; their extent is the communicator's size)
+    if (dep::on()) dep::op(stream, "rccl allgather", {dep::rd(g.send, g.bytes), dep::wr(g.recv, g.bytes)});
 }
 
 void CallbackTransport::allgather(const GatherOp &g, hipStream_t stream) {
@@ -200,6 +209,31 @@ double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream) {
     return 3.0 * elems * es;
 }
 
+std::vector<dep::Access> tick_reduce_access(const Tick &tk, int dtype) {
+    const size_t es = dtype_size(dtype);
+    std::vector<dep::Access> acc;
+    if (tk.multi) {
+        for (const SegTableN &f : tk.folds) {
+            acc.push_back(dep::rd(f.a, f.n * es));
+            for (int i = 0; i < f.nb; ++i) acc.push_back(dep::rd(f.b[i], f.n * es));
+            acc.push_back(dep::wr(f.out, f.n * es));
+        }
+    } else {
+        for (int s = 0; s < tk.reduce.count; ++s) {
+            acc.push_back(dep::rd(tk.reduce.a[s], tk.reduce.n[s] * es));
+            acc.push_back(dep::rd(tk.reduce.b[s], tk.reduce.n[s] * es));
+            acc.push_back(dep::wr(tk.reduce.out[s], tk.reduce.n[s] * es));
+        }
+    }
+    return acc;
+}
+
+std::string dep_label(const char *what, int rank, size_t tick) {
+    std::ostringstream os;
+    os << what << " rank " << rank << " tick " << tick;
+    return os.str();
+}
+
 int last_reduce_at_or_before(const RingProgram &p, int w) {
     for (int t = w; t >= 0; --t)
         if (p.ticks[t].has_reduce) return t;
@@ -304,14 +338,19 @@ void Poster::posted(hipStream_t s) {
 
 void Poster::record(hipEvent_t e, hipStream_t s) {
     DDL_TRACE("record ev " << (void *)e << " on " << (void *)s);
-    if (m_ == kStreams) DDL_HIP(hipEventRecord(e, s));
-    else if (m_ == kDag) ev_[e] = tail_[s];
+    if (m_ == kStreams) {
+        DDL_HIP(hipEventRecord(e, s));
+        dep::record(e, s);
+    } else if (m_ == kDag) {
+        ev_[e] = tail_[s];
+    }
 }
 
 void Poster::wait(hipStream_t s, hipEvent_t e) {
     DDL_TRACE("wait " << (void *)s << " on ev " << (void *)e);
     if (m_ == kStreams) {
         DDL_HIP(hipStreamWaitEvent(s, e, 0));
+        dep::wait(s, e);
     } else if (m_ == kDag) {
         std::vector<hipGraphNode_t> &t = tail_[s];
         for (hipGraphNode_t n : ev_[e])
@@ -355,8 +394,10 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
             if (w >= 0) p.wait(comm, res_.red_ev[w]);
         }
         for (const CopyOp &c : tk.copies) {
-            DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, p.on(comm)));
+            const hipStream_t s = p.on(comm);
+            DDL_HIP(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s));
             p.posted(comm);
+            if (dep::on()) dep::op(s, dep_label("copy", rank_, t), {dep::rd(c.src, c.bytes), dep::wr(c.dst, c.bytes)});
         }
         if (transport_) {
             if (tk.gather.bytes) {
@@ -384,8 +425,10 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
                 }
                 DDL_HIP(hipEventRecord(tp.first, compute));
             }
-            const double bytes = launch_tick_reduce(tk, dtype, p.on(compute));
+            const hipStream_t cs = p.on(compute);
+            const double bytes = launch_tick_reduce(tk, dtype, cs);
             p.posted(compute);
+            if (dep::on()) dep::op(cs, dep_label(tk.multi ? "fold" : "reduce", rank_, t), tick_reduce_access(tk, dtype));
             if (timing) {
                 DDL_HIP(hipEventRecord(tp.second, compute));
                 timed_.push_back(tp);
@@ -440,6 +483,7 @@ void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t st
     // 1) post every send: the send buffers are ready at this point of `stream`
     hipEvent_t ready = event_();
     DDL_HIP(hipEventRecord(ready, stream));
+    dep::record(ready, stream);
     std::vector<std::shared_ptr<Send>> mine;
     {
         std::lock_guard<std::mutex> g(mu_);
@@ -471,9 +515,16 @@ void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t st
         DDL_TRACE("fabric rank " << rank << " recv " << op.bytes << " B from " << op.peer << " tag " << op.tag << " "
                                   << sd->ptr << " -> " << op.ptr);
         DDL_HIP(hipStreamWaitEvent(stream, sd->ready, 0));
+        dep::wait(stream, sd->ready);
         if (op.bytes) DDL_HIP(hipMemcpyAsync(op.ptr, sd->ptr, op.bytes, hipMemcpyDeviceToDevice, stream));
+        if (dep::on()) {
+            std::ostringstream os;
+            os << "recv rank " << rank << " <- " << op.peer << " tag " << op.tag;
+            dep::op(stream, os.str(), {dep::rd(sd->ptr, op.bytes), dep::wr(op.ptr, op.bytes)});
+        }
         hipEvent_t copied = event_();
         DDL_HIP(hipEventRecord(copied, stream));
+        dep::record(copied, stream);
         {
             std::lock_guard<std::mutex> g(mu_);
             sd->copied = copied;
@@ -491,14 +542,19 @@ void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t st
             copied = sd->copied;
         }
         DDL_HIP(hipStreamWaitEvent(stream, copied, 0));
+        dep::wait(stream, copied);
     }
 }
 
 void ThreadTransport::allgather(const GatherOp &g, hipStream_t stream) {
     const int P = fab_->size();
     char *recv = static_cast<char *>(g.recv);
-    if (recv + (size_t)rank_ * g.bytes != g.send)
+    if (recv + (size_t)rank_ * g.bytes != g.send) {
         DDL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * g.bytes, g.send, g.bytes, hipMemcpyDeviceToDevice, stream));
+        if (dep::on())
+            dep::op(stream, dep_label("gather own block", rank_, 0),
+                    {dep::rd(g.send, g.bytes), dep::wr(recv + (size_t)rank_ * g.bytes, g.bytes)});
+    }
     std::vector<P2POp> ops;
     for (int d = 1; d < P; ++d) {
         const int to = (rank_ + d) % P, from = (rank_ + P - d) % P;
@@ -532,7 +588,11 @@ ThreadWorld::~ThreadWorld() {
 
 void ThreadWorld::run_(hipStream_t user, const std::function<void(int, hipStream_t)> &body) {
     DDL_HIP(hipEventRecord(fork_, user));
-    for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(streams_[r], fork_, 0));
+    dep::record(fork_, user);
+    for (int r = 0; r < P_; ++r) {
+        DDL_HIP(hipStreamWaitEvent(streams_[r], fork_, 0));
+        dep::wait(streams_[r], fork_);
+    }
     std::vector<std::thread> th;
     std::vector<Error> errs;
     std::mutex emu;
@@ -542,6 +602,7 @@ void ThreadWorld::run_(hipStream_t user, const std::function<void(int, hipStream
                 DDL_HIP(hipSetDevice(device_));
                 body(r, streams_[r]);
                 DDL_HIP(hipEventRecord(done_[r], streams_[r]));
+                dep::record(done_[r], streams_[r]);
             } catch (const Error &e) {
                 std::lock_guard<std::mutex> g(emu);
                 errs.push_back(e);
@@ -556,7 +617,10 @@ void ThreadWorld::run_(hipStream_t user, const std::function<void(int, hipStream
             ex_[r].reset(new RingExecutor(r, P_, device_, std::unique_ptr<Transport>(new ThreadTransport(fab_, r))));
         throw errs.front();
     }
-    for (int r = 0; r < P_; ++r) DDL_HIP(hipStreamWaitEvent(user, done_[r], 0));
+    for (int r = 0; r < P_; ++r) {
+        DDL_HIP(hipStreamWaitEvent(user, done_[r], 0));
+        dep::wait(user, done_[r]);
+    }
     fab_->recycle();
 }
 
@@ -572,6 +636,22 @@ void ThreadWorld::broadcast(void *const *bufs, size_t n, int dtype, int root, hi
 void ThreadWorld::allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
                              int dtype, hipStream_t user) {
     run_(user, [&](int r, hipStream_t s) { ex_[r]->allgatherv(sends[r], recvs[r], counts, displs, dtype, s); });
+}
+
+size_t ThreadWorld::fused_allreduce(const void *const *srcs, void *const *dsts, const size_t *bytes, int count,
+                                    int dtype, hipStream_t user, const RingConfig &cfg, size_t cap) {
+    while (pipes_.size() < (size_t)P_) pipes_.emplace_back(new FusionPipe);
+    const std::vector<size_t> b(bytes, bytes + count);
+    run_(user, [&](int r, hipStream_t s) {
+        const std::vector<const void *> src(srcs + (size_t)r * count, srcs + (size_t)(r + 1) * count);
+        const std::vector<void *> dst(dsts + (size_t)r * count, dsts + (size_t)(r + 1) * count);
+        pipes_[r]->run(src, dst, b, dtype, cap, s, [&](void *buf, size_t elems, size_t message) {
+            RingConfig c = cfg;
+            c.order_bytes = message;
+            ex_[r]->allreduce(buf, buf, elems, dtype, s, c);
+        });
+    });
+    return pipes_[0]->subplans();
 }
 
 LocalWorld::LocalWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks) {
@@ -655,8 +735,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
     auto wait = [&](hipStream_t st, hipEvent_t e) { p.wait(st, e); };
     auto copy = [&](void *dst, const void *src, size_t bytes, hipStream_t st) {
         DDL_TRACE("copy " << bytes << " B on " << (void *)st);
-        DDL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, p.on(st)));
+        const hipStream_t s = p.on(st);
+        DDL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
         p.posted(st);
+        if (dep::on()) dep::op(s, "local copy", {dep::rd(src, bytes), dep::wr(dst, bytes)});
     };
     DDL_TRACE("local world run: P " << P_ << " ticks " << T << " mode " << (int)p.mode() << " user " << (void *)user);
     hipEvent_t fork = res_[0]->fork_ev;
@@ -753,8 +835,11 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
                     const P2POp &match = match_(r, t, op, seen);
                     wait(comm(r), res_[op.peer]->pre_ev[t]);
                     DDL_TRACE("recv copy " << op.bytes << " B on " << (void *)comm(r));
-                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, p.on(comm(r))));
+                    const hipStream_t s = p.on(comm(r));
+                    DDL_HIP(hipMemcpyAsync(op.ptr, match.ptr, op.bytes, hipMemcpyDeviceToDevice, s));
                     p.posted(comm(r));
+                    if (dep::on())
+                        dep::op(s, dep_label("local recv", r, t), {dep::rd(match.ptr, op.bytes), dep::wr(op.ptr, op.bytes)});
                 }
                 record(rr.post_ev[t], comm(r));
             }
@@ -772,8 +857,10 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
             record(rr.comm_ev[t], comm(r));
             wait(compute(r), rr.comm_ev[t]);
             DDL_TRACE("reduce launch on " << (void *)compute(r));
-            launch_tick_reduce(tk, dtype, p.on(compute(r)));
+            const hipStream_t cs = p.on(compute(r));
+            launch_tick_reduce(tk, dtype, cs);
             p.posted(compute(r));
+            if (dep::on()) dep::op(cs, dep_label(tk.multi ? "fold" : "reduce", r, t), tick_reduce_access(tk, dtype));
             record(rr.red_ev[t], compute(r));
         }
     }

@@ -17,6 +17,8 @@
 #include <mutex>
 #include <vector>
 
+#include "deptrace.h"
+#include "fusion.h"
 #include "rccl_api.h"
 #include "schedule.h"
 
@@ -306,12 +308,19 @@ public:
     void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
     void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
                     int dtype, hipStream_t user);
+    // The keyed path's multi-request plan on every rank (FusionPipe::run, what the handler runs:
+    // pack -> allreduce -> unpack, sub-plans above `cap` bytes), each sub-plan's allreduce through
+    // the rank's RingExecutor with the whole plan's message size. srcs[r * count + i] /
+    // dsts[r * count + i]: rank r's segment i of bytes[i] bytes. Returns the sub-plans per rank.
+    size_t fused_allreduce(const void *const *srcs, void *const *dsts, const size_t *bytes, int count, int dtype,
+                           hipStream_t user, const RingConfig &cfg, size_t cap);
 
 private:
     void run_(hipStream_t user, const std::function<void(int, hipStream_t)> &body);
     int P_, device_;
     std::shared_ptr<ThreadFabric> fab_;
     std::vector<std::unique_ptr<RingExecutor>> ex_;
+    std::vector<std::unique_ptr<FusionPipe>> pipes_;  // one per rank (fused_allreduce)
     std::vector<hipStream_t> streams_;
     std::vector<hipEvent_t> done_;
     hipEvent_t fork_ = nullptr;
@@ -323,5 +332,8 @@ int last_reduce_at_or_before(const RingProgram &p, int w);
 // Launches a tick's reduce (2-input ring step or N-input direct fold) on `stream`; returns its
 // algorithmic HBM bytes.
 double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream);
+// The byte ranges a tick's reduce reads and writes, and a trace label (deptrace.h).
+std::vector<dep::Access> tick_reduce_access(const Tick &tk, int dtype);
+std::string dep_label(const char *what, int rank, size_t tick);
 
 }  // namespace ddl

@@ -300,10 +300,6 @@ RequestHandler::~RequestHandler() {
     if (done_thread_.joinable()) done_thread_.join();
     fail_all_(DDL_STATUS_COMM_ERROR);
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
-    for (hipEvent_t e : pipe_events_) (void)hipEventDestroy(e);
-    if (fusion_) (void)hipFree(fusion_);
-    if (fusion2_) (void)hipFree(fusion2_);
-    if (side_) (void)hipStreamDestroy(side_);
     if (gather_) (void)hipFree(gather_);
     if (dims_) (void)hipFree(dims_);
     if (pin_gather_) (void)hipHostFree(pin_gather_);
@@ -1005,7 +1001,7 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
                 len.push_back(hi - lo);
                 flat += round256(hi - lo);
             }
-            copier_.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
+            fp_.copier.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
         } else {
             DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
         }
@@ -1198,7 +1194,10 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
                     dsts.push_back(static_cast<char *>(r.out) + b * es);
                     bytes.push_back((e - b) * es);
                 }
-                fused_allreduce_(srcs, dsts, bytes, dt);
+                fp_.run(srcs, dsts, bytes, dt, (size_t)config().fusion_pipeline_bytes.load(), stream_,
+                        [&](void *buf, size_t elems, size_t message) {
+                            data_->allreduce(buf, buf, elems, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
+                        });
             }
             const size_t plan = record_plan_(nplans);
             for (size_t q = p.req_begin; q <= p.req_end; ++q) {
@@ -1208,98 +1207,6 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
             }
         }
     }
-}
-
-hipEvent_t RequestHandler::pipe_event_(size_t i) {
-    while (pipe_events_.size() <= i) {
-        hipEvent_t e;
-        DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        pipe_events_.push_back(e);
-    }
-    return pipe_events_[i];
-}
-
-// The reference copies every request of a plan into one MPI buffer, reduces it and copies it
-// back (executeCommunicatePlan_, MPIRingTokenCommunication.cc:548-733). Here the copies are the
-// pack / unpack kernels, and a plan above fusion_pipeline_bytes is cut into sub-plans J of at
-// most that size (segments split at 256-byte multiples) over two fusion buffers:
-//   side_:   pack 0, pack 1, unpack 0, pack 2, unpack 1, ...   (unpack j waits allreduce j)
-//   stream_:         ar 0,   ar 1,     ar 2, ...               (ar j waits pack j)
-// so the pack of j+1 and the unpack of j-1 run under the allreduce of j. Buffer j%2 is reused
-// by pack j+2, issued on side_ after unpack j. Each sub-plan is an allreduce of its own (its
-// ring chunks follow the sub-plan); with reference_order each sub-plan folds in the order MPICH
-// uses for the whole plan's message, so the cut changes no bit.
-void RequestHandler::fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
-                                      const std::vector<size_t> &bytes, int dt) {
-    const size_t es = dtype_size(dt);
-    const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
-    // the reference's MPI buffer holds the requests back to back (no padding): its byte count
-    // picks MPICH's summation order (reference_order)
-    size_t message = 0;
-    for (size_t b : bytes) message += b;
-    size_t cap = (size_t)config().fusion_pipeline_bytes.load();
-    cap &= ~size_t(255);
-    if (cap == 0 || total <= cap) {
-        ensure_(fusion_, fusion_bytes_, total);
-        copier_.run(0, fusion_, const_cast<void *const *>(reinterpret_cast<const void *const *>(srcs.data())),
-                    bytes.data(), (int)srcs.size(), stream_);
-        data_->allreduce(fusion_, fusion_, total / es, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
-        copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
-        return;
-    }
-    struct Sub {
-        std::vector<const void *> src;
-        std::vector<void *> dst;
-        std::vector<size_t> bytes;
-        size_t flat = 0;
-    };
-    std::vector<Sub> subs(1);
-    for (size_t i = 0; i < bytes.size(); ++i) {
-        size_t off = 0;
-        do {
-            Sub *cur = &subs.back();
-            if (cur->flat >= cap) {
-                subs.emplace_back();
-                cur = &subs.back();
-            }
-            // a piece fills the sub-plan up to cap; every cut is a multiple of 256 bytes (and so of
-            // the element size) from the segment start
-            const size_t room = cap - cur->flat, left = bytes[i] - off;
-            const size_t len = left <= room ? left : room;
-            cur->src.push_back(static_cast<const char *>(srcs[i]) + off);
-            cur->dst.push_back(static_cast<char *>(dsts[i]) + off);
-            cur->bytes.push_back(len);
-            cur->flat += (len + 255) & ~size_t(255);
-            off += len;
-        } while (off < bytes[i]);
-    }
-    size_t maxflat = 0;
-    for (const Sub &sb : subs) maxflat = sb.flat > maxflat ? sb.flat : maxflat;
-    void *buf[2] = {ensure_(fusion_, fusion_bytes_, maxflat), ensure_(fusion2_, fusion2_bytes_, maxflat)};
-    if (!side_) DDL_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    const size_t J = subs.size();
-    // events: [0] fork, [1 + 2j] pack j done, [2 + 2j] allreduce j done, [1 + 2J] join
-    hipEvent_t fork = pipe_event_(0);
-    for (size_t k = 1; k <= 2 * J + 1; ++k) pipe_event_(k);
-    DDL_HIP(hipEventRecord(fork, stream_));  // inputs ready (wait_inputs_ ran on stream_)
-    DDL_HIP(hipStreamWaitEvent(side_, fork, 0));
-    auto unpack = [&](size_t j) {
-        DDL_HIP(hipStreamWaitEvent(side_, pipe_events_[2 + 2 * j], 0));
-        copier_.run(1, buf[j % 2], subs[j].dst.data(), subs[j].bytes.data(), (int)subs[j].dst.size(), side_);
-    };
-    for (size_t j = 0; j < J; ++j) {
-        Sub &sb = subs[j];
-        copier_.run(0, buf[j % 2], const_cast<void *const *>(reinterpret_cast<const void *const *>(sb.src.data())),
-                    sb.bytes.data(), (int)sb.src.size(), side_);
-        DDL_HIP(hipEventRecord(pipe_events_[1 + 2 * j], side_));
-        DDL_HIP(hipStreamWaitEvent(stream_, pipe_events_[1 + 2 * j], 0));
-        data_->allreduce(buf[j % 2], buf[j % 2], sb.flat / es, dt, DDL_ALLREDUCE_OP_SUM, stream_, message);
-        DDL_HIP(hipEventRecord(pipe_events_[2 + 2 * j], stream_));
-        if (j >= 1) unpack(j - 1);
-    }
-    unpack(J - 1);
-    DDL_HIP(hipEventRecord(pipe_events_[1 + 2 * J], side_));
-    DDL_HIP(hipStreamWaitEvent(stream_, pipe_events_[1 + 2 * J], 0));
 }
 
 // broadcastRequests (MPIRingTokenCommunication.cc:367-419): dtype groups, plans, broadcast of
@@ -1366,12 +1273,12 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
                     bytes.push_back((e - b) * es);
                 }
                 const size_t total = SegmentCopier::flat_bytes(bytes.data(), (int)bytes.size());
-                ensure_(fusion_, fusion_bytes_, total);
+                void *fb = fp_.ensure(0, total, stream_);
                 if (me == root)
-                    copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(),
-                                stream_);
-                data_->broadcast(fusion_, total / es, dt, root, stream_);
-                copier_.run(1, fusion_, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
+                    fp_.copier.run(0, fb, const_cast<void *const *>(srcs.data()), bytes.data(), (int)srcs.size(),
+                                   stream_);
+                data_->broadcast(fb, total / es, dt, root, stream_);
+                fp_.copier.run(1, fb, dsts.data(), bytes.data(), (int)dsts.size(), stream_);
             }
             const size_t plan = record_plan_(nplans);
             for (size_t q = p.req_begin; q <= p.req_end; ++q) {
@@ -1435,7 +1342,7 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
                 all += blk[q];
             }
             if (all) {
-                ensure_(fusion_, fusion_bytes_, std::max<size_t>(blk[me], 256));
+                void *fb = fp_.ensure(0, std::max<size_t>(blk[me], 256), stream_);
                 ensure_(gather_, gather_bytes_, all);
                 if (pin_gather_bytes_ < all) {
                     if (pin_gather_) DDL_HIP(hipHostFree(pin_gather_));
@@ -1452,8 +1359,8 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
                     std::memcpy(pin + off, r.in, b);
                     off += b;
                 }
-                DDL_HIP(hipMemcpyAsync(fusion_, pin, blk[me], hipMemcpyHostToDevice, stream_));
-                data_->allgatherv(fusion_, gather_, cnt.data(), dsp.data(), dt, stream_);
+                DDL_HIP(hipMemcpyAsync(fb, pin, blk[me], hipMemcpyHostToDevice, stream_));
+                data_->allgatherv(fb, gather_, cnt.data(), dsp.data(), dt, stream_);
                 DDL_HIP(hipMemcpyAsync(pin, gather_, all, hipMemcpyDeviceToHost, stream_));
                 DDL_HIP(hipStreamSynchronize(stream_));
                 std::vector<size_t> row_off(m, 0);
@@ -1494,13 +1401,13 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
                 all += blk[q];
             }
             if (all) {
-                ensure_(fusion_, fusion_bytes_, std::max<size_t>(blk[me], 256));
+                void *fb = fp_.ensure(0, std::max<size_t>(blk[me], 256), stream_);
                 ensure_(gather_, gather_bytes_, all);
                 std::vector<const void *> srcs(m);
                 for (size_t j = 0; j < m; ++j) srcs[j] = reqs[g.second[j]].in;
-                copier_.run(0, fusion_, const_cast<void *const *>(srcs.data()), seg_bytes.data() + me * m, (int)m,
-                            stream_);
-                data_->allgatherv(fusion_, gather_, cnt.data(), dsp.data(), dt, stream_);
+                fp_.copier.run(0, fb, const_cast<void *const *>(srcs.data()), seg_bytes.data() + me * m, (int)m,
+                               stream_);
+                data_->allgatherv(fb, gather_, cnt.data(), dsp.data(), dt, stream_);
                 std::vector<void *> dsts(P * m);
                 std::vector<size_t> row_off(m, 0);  // rows of request j written so far
                 for (int q = 0; q < P; ++q)
@@ -1509,7 +1416,7 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
                         dsts[q * m + j] = static_cast<char *>(r.out) + row_off[j] * r.row_elems * es;
                         row_off[j] += fd[q * m + j];
                     }
-                copier_.run(1, gather_, dsts.data(), seg_bytes.data(), (int)(P * m), stream_);
+                fp_.copier.run(1, gather_, dsts.data(), seg_bytes.data(), (int)(P * m), stream_);
             }
         }
         const size_t plan = record_plan_(nplans);

@@ -33,6 +33,7 @@
 
 #include "control.h"
 #include "engine.h"
+#include "fusion.h"
 
 namespace ddl {
 
@@ -223,11 +224,6 @@ private:
     void wait_inputs_(const Request &r, std::vector<hipEvent_t> &waited);
     void *ensure_(void *&buf, size_t &cap, size_t need);
     void allreduce_reqs_(std::vector<Request> &reqs, std::vector<Done> &dones, size_t &nplans);
-    // pack -> allreduce -> unpack of one multi-request plan's segments (src[i] -> dst[i], bytes[i]);
-    // above fusion_pipeline_bytes as a two-buffer pipeline of sub-plans (pack / unpack on side_)
-    void fused_allreduce_(const std::vector<const void *> &srcs, const std::vector<void *> &dsts,
-                          const std::vector<size_t> &bytes, int dtype);
-    hipEvent_t pipe_event_(size_t i);
     // Host-resident requests (the reference's deployment case, MPIRingTokenCommunication.cc:
     // 548-733 copies CPU tensors into its MPI buffer): the plan's segments are staged through
     // pinned slots in chunks — host pack (CopyPool) -> H2D -> `coll` on the device slot
@@ -269,17 +265,13 @@ private:
     ControlChannel *ch_ = nullptr;        // the owner's token ring (size > 1)
     std::shared_ptr<Communicator> data_;  // private data-plane communicator
     hipStream_t stream_ = nullptr;
-    void *fusion_ = nullptr;  // packed requests (allreduce / broadcast / allgather send side)
-    size_t fusion_bytes_ = 0;
-    void *fusion2_ = nullptr;  // second buffer of the fusion pipeline
-    size_t fusion2_bytes_ = 0;
-    hipStream_t side_ = nullptr;  // pack / unpack of the fusion pipeline
-    std::vector<hipEvent_t> pipe_events_;
+    // multi-request plans: pack -> allreduce -> unpack, pipelined in sub-plans above
+    // fusion_pipeline_bytes (fusion.h); its buffer 0 also packs broadcast / allgather plans
+    FusionPipe fp_;
     void *gather_ = nullptr;  // allgather receive side
     size_t gather_bytes_ = 0;
     void *dims_ = nullptr;    // allgather first-dim exchange
     size_t dims_bytes_ = 0;
-    SegmentCopier copier_;
     std::vector<hipEvent_t> round_events_;  // plan events of the round being enqueued (engine thread)
     static constexpr int kHostSlots = 4;
     void *pin_[kHostSlots] = {};    // pinned host staging slots

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "common.h"
+#include "deptrace.h"
 
 namespace ddl {
 
@@ -259,6 +260,13 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     }
     DDL_HIP(hipGetLastError());
     DDL_HIP(hipEventRecord(sl.ready, stream));
+    if (dep::on()) {  // happens-before trace (deptrace.h): the segments and the flat buffer
+        std::vector<dep::Access> acc;
+        acc.push_back(dir == 0 ? dep::wr(flat, off) : dep::rd(flat, off));
+        for (int i = 0; i < count; ++i)
+            if (bytes[i]) acc.push_back(dir == 0 ? dep::rd(segs[i], bytes[i]) : dep::wr(segs[i], bytes[i]));
+        dep::op(stream, dir == 0 ? "pack" : "unpack", std::move(acc));
+    }
 }
 
 }  // namespace ddl

@@ -139,6 +139,10 @@ class CPPBackend:
         sig('ddl_testing_thread_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
             ctypes.POINTER(sz), ci, vp)
         sig('ddl_testing_drop_wait', ci, ci)
+        sig('ddl_testing_dep_trace', ci, ci)
+        sig('ddl_testing_thread_fused_allreduce', ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp),
+            ctypes.POINTER(sz), ci, vp, ctypes.POINTER(sz))
+        sig('ddl_testing_dep_check', ci, lp, ctypes.c_char_p, sz)
         sig('ddl_rccl_loopback_init', ci, ci)
         sig('ddl_rccl_loopback_split', ci, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci))
         sig('ddl_rccl_loopback_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, vp)

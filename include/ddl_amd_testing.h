@@ -136,9 +136,25 @@ int ddl_testing_thread_broadcast(int nranks, int root, void *const *bufs, size_t
                                  void *hip_stream);
 int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,
                                   const size_t *displs, int dtype, void *hip_stream);
+/* The keyed path's multi-request plan on every virtual rank (the handler's FusionPipe: pack ->
+ * allreduce -> unpack, cut into sub-plans above config "fusion_pipeline_bytes", two fusion buffers,
+ * pack / unpack on a side stream), each sub-plan's allreduce through the rank's RingExecutor in the
+ * whole plan's MPICH order. srcs[r * count + i] / dsts[r * count + i] are rank r's segment i of
+ * bytes[i] bytes (whole elements of dtype); *subplans (may be NULL) = the sub-plans per rank. */
+int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const *srcs, void *const *dsts,
+                                       const size_t *bytes, int dtype, void *hip_stream, size_t *subplans);
 /* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
  * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
 int ddl_testing_drop_wait(int tick);
+/* Happens-before tracing of the work the executors post (deptrace.h): _trace(1) clears the log
+ * and starts it, _trace(0) stops it. _check replays the log with vector clocks (stream order plus
+ * event record -> stream wait edges) and compares every pair of ops on different streams whose
+ * byte ranges overlap, one of them writing: counts[0..4] = {ops, such conflicting pairs, pairs
+ * ordered by the posted dependencies, ordered pairs with a reduce / fold on one side, unordered
+ * pairs = races}; `report` gets the first races, one per line. Independent of timing and of how
+ * streams share hardware queues. */
+int ddl_testing_dep_trace(int on);
+int ddl_testing_dep_check(long long *counts, char *report, size_t len);
 /* The CUs enabled on an executor compute stream created with every `every`-th CU masked off
  * (config "compute_cu_mask"; 0 = unmasked), read back with hipExtStreamGetCUMask. */
 int ddl_testing_compute_stream_cus(int every, int *enabled, int *total);

@@ -10,8 +10,12 @@ wait corrupts the sums here, where the host-synchronising test transport would h
 Bar: every rank bit-exact vs MPICH's order (ddlo_fold_ref_order) — or the ring-order / left-fold
 restatements with reference_order 0 — on the MPICH golden vectors, the oracle cases and C3 at
 full size (8 x 256 MiB), for every schedule; broadcast / allgatherv vs MPI_Bcast / MPI_Allgatherv
-restatements. The mutation test drops ONE reduce wait (ddl_testing_drop_wait) and must see wrong
-data (reference semantics: MPIRingTokenCommunication.cc:548-733, MPICommunicator.cc:14-28)."""
+restatements. Beside the data, the happens-before trace (deptrace.h) checks what the executor
+POSTS: every conflicting pair of ops on different streams must be ordered by stream order and
+event waits — a check that does not depend on timing or on how the streams share the hardware
+queues. The mutation test drops ONE reduce wait (ddl_testing_drop_wait) and must see every
+receive of a forwarded chunk race with its fold (reference semantics:
+MPIRingTokenCommunication.cc:548-733, MPICommunicator.cc:14-28)."""
 import ctypes
 import json
 import os
@@ -20,7 +24,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import DT_DOUBLE, DT_FLOAT, DT_INT32, NAME, config, random_input, ring_perms, ring_shape
+from _helpers import DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, config, random_input, ring_perms, ring_shape
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -114,6 +118,140 @@ def test_thread_world_c3_full_size(lib, oracle, gpu, algo):
     torch.cuda.empty_cache()
 
 
+def test_thread_world_c4_fp16_full_size(lib, oracle, gpu):
+    """C4 through the production executor: 64 buckets of 16 MiB fp16 per rank (1 GiB), P = 8, each
+    bucket one asynchronous thread-world allreduce in place, back to back with no host
+    synchronisation in between (as a DDP bucket stream issues them). Every rank within the stated
+    fp16 bound |y - sum| <= (P-1) * 2^-11 * sum|x| + ulp16(sum)/2 of the exact (fp64) sum, all ranks
+    identical; and bucket 0 bit-exact vs the oracle's fp16 fold (rank order in fp32, one rounding)."""
+    P, nb, buckets = 8, (16 << 20) // 2, 64
+    g = torch.Generator(device=gpu).manual_seed(44)
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=2 << 20):
+        sets = []
+        for b in range(buckets):
+            ins = [(torch.randn(nb, device=gpu, generator=g) * 0.1).half() for _ in range(P)]
+            x64 = torch.stack(ins).double()
+            sets.append((ins, x64.sum(0), x64.abs().sum(0)))
+            del x64
+            if b == 0:
+                xs0 = [t.cpu().numpy() for t in ins]
+        torch.cuda.synchronize()
+        for ins, _, _ in sets:
+            _thread_allreduce(lib, ins, ins, nb, DT_HALF)
+        torch.cuda.synchronize()
+    want0 = oracle.fold_ref_order(DT_HALF, xs0)
+    assert sets[0][0][0].cpu().numpy().tobytes() == want0.tobytes()
+    worst = 0.0
+    for b, (ins, exact, mag) in enumerate(sets):
+        _, e = torch.frexp(exact.half().abs().double())  # |round16(sum)| = m * 2^e, m in [0.5, 1)
+        ulp = torch.exp2((e - 11).double()).clamp_min(2.0 ** -24)
+        bound = (P - 1) * 2.0 ** -11 * mag + ulp / 2
+        err = (ins[0].double() - exact).abs()
+        assert bool((err <= bound).all()), b
+        worst = max(worst, float((err / bound.clamp_min(1e-30)).max()))
+        for t in ins[1:]:
+            assert torch.equal(t, ins[0]), b
+    assert worst <= 1.0
+    del sets
+    torch.cuda.empty_cache()
+
+
+def _c5_buckets(k, seed=5, max_bytes=4 << 20):
+    """BASELINE C5's bucket set (as test_configs_gpu.py): sizes log-uniform in 4 KiB .. max_bytes,
+    256-byte multiples, fp16 or fp32 at random."""
+    rng = np.random.default_rng(seed)
+    sizes = (np.exp(rng.uniform(np.log(4096), np.log(max_bytes), size=k)).astype(np.int64) // 256) * 256
+    half = rng.random(k) < 0.5
+    return [(int(sizes[i]) // (2 if half[i] else 4), DT_HALF if half[i] else DT_FLOAT) for i in range(k)]
+
+
+def _thread_fused(lib, per_rank, outs, buckets, P):
+    """The keyed data plane per dtype group (ascending enum, key order = index order) through the
+    handler's FusionPipe on every rank, the allreduces through the ranks' RingExecutors
+    (ddl_testing_thread_fused_allreduce). Returns the sub-plans per group."""
+    s = torch.cuda.current_stream().cuda_stream
+    subs = {}
+    for dt in sorted({d for _, d in buckets}):
+        idx = [i for i, (_, d) in enumerate(buckets) if d == dt]
+        es = 2 if dt == DT_HALF else 4
+        nbytes = [buckets[i][0] * es for i in idx]
+        assert sum(nbytes) <= (1 << 31) - 1  # one plan at the reference's fusion threshold
+        m = len(idx)
+        S = (ctypes.c_void_p * (P * m))(*[per_rank[r][i].data_ptr() for r in range(P) for i in idx])
+        D = (ctypes.c_void_p * (P * m))(*[outs[r][i].data_ptr() for r in range(P) for i in idx])
+        J = ctypes.c_size_t()
+        assert lib.ddl_testing_thread_fused_allreduce(P, m, S, D, (ctypes.c_size_t * m)(*nbytes), dt, s,
+                                                      ctypes.byref(J)) == 0, lib.ddl_last_error()
+        subs[dt] = J.value
+    return subs
+
+
+def test_thread_world_c5_full_4096_buckets_exact(lib, gpu):
+    """C5 through the production executor and the handler's fusion pipeline: 4096 mixed fp32 /
+    fp16 buckets (2.4 GB per rank), 8 ranks, per dtype group one plan packed into the fusion
+    buffers in fusion_pipeline_bytes (256 MiB) sub-plans, each sub-plan reduced asynchronously by
+    the ranks' RingExecutors, unpacked. Integer-valued data (|x| <= 8: every sum exact in fp16 and
+    fp32), so every rank must equal the exact sum bit for bit."""
+    P = 8
+    buckets = _c5_buckets(4096)
+    g = torch.Generator(device=gpu).manual_seed(55)
+    tdt = {DT_FLOAT: torch.float32, DT_HALF: torch.float16}
+    per_rank = [[torch.randint(-8, 9, (n,), device=gpu, generator=g).to(tdt[dt]) for n, dt in buckets]
+                for _ in range(P)]
+    outs = [[torch.empty_like(t) for t in row] for row in per_rank]
+    torch.cuda.synchronize()
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=2 << 20, fusion_pipeline_bytes=256 << 20):
+        subs = _thread_fused(lib, per_rank, outs, buckets, P)
+    torch.cuda.synchronize()
+    assert all(j >= 4 for j in subs.values()), subs  # ~1.2 GB per group: the pipeline ran
+    for i in range(len(buckets)):
+        want = torch.stack([per_rank[r][i] for r in range(P)]).float().sum(0).to(per_rank[0][i].dtype)
+        for r in range(P):
+            assert torch.equal(outs[r][i], want), (i, r)
+    del per_rank, outs
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize('cap', [0, 1 << 20])
+def test_thread_world_c5_sample_random_vs_oracle(lib, oracle, gpu, cap):
+    """512 buckets of the C5 distribution (capped at 256 KiB) with random data, unpipelined and cut
+    into 1 MiB sub-plans: every rank equals the oracle's MPICH order for the whole group's message
+    (the sub-plan cut changes no bit), fp16 folded in fp32 in rank order."""
+    P = 8
+    buckets = _c5_buckets(512, seed=6, max_bytes=256 << 10)
+    xs = [[random_input(dt, n, 10_000 * r + i) for i, (n, dt) in enumerate(buckets)] for r in range(P)]
+    per_rank = [[_dev(x.view(np.int16) if x.dtype == np.float16 else x, gpu) for x in row] for row in xs]
+    per_rank = [[t.view(torch.float16) if t.dtype == torch.int16 else t for t in row] for row in per_rank]
+    outs = [[torch.full_like(t, float('nan')) for t in row] for row in per_rank]
+    torch.cuda.synchronize()
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=64 << 10, fusion_pipeline_bytes=cap):
+        subs = _thread_fused(lib, per_rank, outs, buckets, P)
+    torch.cuda.synchronize()
+    assert all((j > 1) == (cap > 0) for j in subs.values()), subs
+    message = {dt: sum(n * (2 if d == DT_HALF else 4) for n, d in buckets if d == dt) for dt in subs}
+    for i, (n, dt) in enumerate(buckets):
+        want = oracle.fold_ref_order(dt, [xs[r][i] for r in range(P)], message[dt]).tobytes()
+        for r in range(P):
+            assert outs[r][i].cpu().numpy().tobytes() == want, (i, r)
+
+
+def test_thread_world_fused_pipeline_has_no_race(lib, gpu):
+    """What the fusion pipeline posts around the executors (pack / unpack on the side stream, two
+    buffers, sub-plan allreduces, unpack of j-1 under allreduce j) is race-free: 96 buckets cut
+    into 64 KiB sub-plans at P = 5, traced (deptrace.h)."""
+    P = 5
+    buckets = _c5_buckets(96, seed=7, max_bytes=64 << 10)
+    per_rank = [[torch.randn(n, device=gpu).to(torch.float16 if dt == DT_HALF else torch.float32)
+                 for n, dt in buckets] for _ in range(P)]
+    outs = [[torch.empty_like(t) for t in row] for row in per_rank]
+    torch.cuda.synchronize()
+    with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=16 << 10, fusion_pipeline_bytes=64 << 10):
+        res, lines = _traced(lib, lambda: _thread_fused(lib, per_rank, outs, buckets, P))
+    torch.cuda.synchronize()
+    assert res['races'] == 0, (res, lines)
+    assert res['ordered'] > 0 and res['ordered_reduce'] > 0, res
+
+
 @pytest.mark.parametrize('P', [3, 8])
 def test_thread_world_broadcast_allgatherv(lib, oracle, gpu, P):
     """RingExecutor::broadcast / allgatherv asynchronously (their programs have no reduce: the
@@ -163,34 +301,122 @@ def test_thread_world_repeated_calls_reuse_events(lib, oracle, gpu):
             assert all(o.cpu().numpy().tobytes() == want for o in outs)
 
 
+def _traced(lib, fn):
+    """Runs fn() with the happens-before trace on (deptrace.h) and returns the check's counts and
+    its first race lines. The check replays what was POSTED — stream order plus event record ->
+    stream wait edges — so its verdict does not depend on timing or on how the streams share the
+    hardware queues."""
+    assert lib.ddl_testing_dep_trace(1) == 0, lib.ddl_last_error()
+    try:
+        fn()
+    finally:
+        assert lib.ddl_testing_dep_trace(0) == 0, lib.ddl_last_error()
+    counts = (ctypes.c_longlong * 5)()
+    buf = ctypes.create_string_buffer(1 << 14)
+    assert lib.ddl_testing_dep_check(counts, buf, len(buf)) == 0, lib.ddl_last_error()
+    return dict(zip(('ops', 'conflicts', 'ordered', 'ordered_reduce', 'races'), counts)), buf.value.decode()
+
+
 def test_dropping_one_reduce_wait_is_caught(lib, oracle, gpu):
-    """The mutation: RingExecutor skips the wait of the allgather tick on the fold it forwards
-    (executor.cpp, tick.wait_reduce). Over the asynchronous transport the allgather's copies then
-    read the output before the fold has written it, and the test sees wrong data; with the wait
-    restored the same call is bit-exact again. (P = 8, one 32 MiB slice per chunk: the fold runs
-    ~50 us, the copy starts at once.)"""
-    P, n = 8, 64 << 20
+    """The mutation, checked DETERMINISTICALLY: RingExecutor skips the wait of the allgather tick
+    on the fold it forwards (executor.cpp, tick.wait_reduce; ddl_testing_drop_wait). The posted
+    dependency graph then has no path from rank q's fold to the receives that read q's reduced
+    chunk — every one of the P(P-1) receives races with a fold, whatever the box's stream-to-queue
+    mapping (r03's data-based form of this test saw 0 wrong outputs on one box: DESIGN §8.6). With
+    the wait restored the same call has no race and is bit-exact. Reference semantics guarded:
+    the memcpy-out only after the reduce (MPIRingTokenCommunication.cc:548-733)."""
+    P, n = 8, (1 << 20) + 5
     xs = [random_input(DT_FLOAT, n, 5150 + r) for r in range(P)]
     want = oracle.fold_ref_order(DT_FLOAT, xs).tobytes()
     ins = [torch.from_numpy(x).to(gpu) for x in xs]
+    outs = [torch.full_like(t, float('nan')) for t in ins]
     with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=64 << 20):
-        wrong = 0
+        torch.cuda.synchronize()
         try:
             assert lib.ddl_testing_drop_wait(1) == 0  # tick 0 = reduce-scatter + fold, tick 1 = allgather
-            for _ in range(3):
-                outs = [torch.full_like(t, float('nan')) for t in ins]
-                _thread_allreduce(lib, ins, outs, n, DT_FLOAT)
-                torch.cuda.synchronize()
-                wrong += sum(o.cpu().numpy().tobytes() != want for o in outs)
+            dropped, lines = _traced(lib, lambda: _thread_allreduce(lib, ins, outs, n, DT_FLOAT))
+            torch.cuda.synchronize()
         finally:
             assert lib.ddl_testing_drop_wait(-1) == 0
-        assert wrong > 0, 'dropping the allgather\'s wait on the fold went unnoticed'
+        assert dropped['races'] >= P * (P - 1), (dropped, lines)
+        for line in lines.strip().splitlines():  # every race: a fold against a receive of its chunk
+            a, b = line.split(' || ')
+            fold, recv = (a, b) if a.startswith('fold') else (b, a)
+            assert fold.startswith('fold rank ') and fold.endswith(' tick 0'), line
+            assert recv.startswith('recv rank ') and recv.split(' <- ')[1].split()[0] == fold.split()[2], line
         outs = [torch.full_like(t, float('nan')) for t in ins]
-        _thread_allreduce(lib, ins, outs, n, DT_FLOAT)
         torch.cuda.synchronize()
-        assert all(o.cpu().numpy().tobytes() == want for o in outs)
-    del ins, outs
-    torch.cuda.empty_cache()
+        kept, lines = _traced(lib, lambda: _thread_allreduce(lib, ins, outs, n, DT_FLOAT))
+        torch.cuda.synchronize()
+    assert kept['races'] == 0, lines
+    assert kept['ordered_reduce'] >= 2 * P * (P - 1), kept  # fold <- its inputs' receives, receives <- fold
+    assert all(o.cpu().numpy().tobytes() == want for o in outs)
+
+
+@pytest.mark.parametrize('P', [2, 3, 5, 8])
+@pytest.mark.parametrize('algo,ref', [(0, 0), (1, 0), (2, 0), (3, 0), (1, 1), (4, 1)])
+def test_posted_dependencies_have_no_race(lib, gpu, P, algo, ref):
+    """Every schedule of the production executor, several slices per chunk (64 KiB), in and out of
+    place, two calls back to back on the caller's stream (staging and events reused, no host
+    synchronisation between them): every pair of posted ops on different streams that touch the
+    same bytes, one writing, is ordered by the posted dependencies."""
+    s = torch.cuda.current_stream()
+    with config(lib, algo=algo, reference_order=ref, tune=0, slice_bytes=64 << 10):
+        for n in (300, 128 * 840 + 3):
+            ins = [torch.randn(n, device=gpu) for _ in range(P)]
+            outs = [torch.empty_like(t) for t in ins]
+            torch.cuda.synchronize()
+
+            def two_calls():
+                _thread_allreduce(lib, ins, outs, n, DT_FLOAT)  # out of place
+                _thread_allreduce(lib, outs, outs, n, DT_FLOAT)  # in place, reading the first's output
+            res, lines = _traced(lib, two_calls)
+            s.synchronize()
+            assert res['races'] == 0, (n, res, lines)
+            assert res['ordered'] > 0 and (P == 1 or res['ordered_reduce'] > 0), res
+
+
+@pytest.mark.parametrize('P', [3, 8])
+def test_posted_dependencies_broadcast_allgatherv(lib, gpu, P):
+    """RingExecutor::broadcast / allgatherv: no race in what they post."""
+    s = torch.cuda.current_stream().cuda_stream
+    n, root = 300_007, P - 2
+    bufs = [torch.randn(n, device=gpu) for _ in range(P)]
+    counts = [10_000 * (r + 1) + 3 for r in range(P)]
+    displs = list(np.cumsum([0] + counts[:-1]))
+    sends = [torch.randn(c, device=gpu) for c in counts]
+    recvs = [torch.empty(sum(counts), device=gpu) for _ in range(P)]
+    torch.cuda.synchronize()
+    with config(lib, slice_bytes=64 << 10):
+        arr = (ctypes.c_void_p * P)(*[b.data_ptr() for b in bufs])
+        res, lines = _traced(lib, lambda: lib.ddl_testing_thread_broadcast(P, root, arr, n, DT_FLOAT, s))
+        torch.cuda.synchronize()
+        assert res['races'] == 0 and res['ordered'] > 0, (res, lines)
+        S = (ctypes.c_void_p * P)(*[t.data_ptr() for t in sends])
+        R = (ctypes.c_void_p * P)(*[t.data_ptr() for t in recvs])
+        C = (ctypes.c_size_t * P)(*counts)
+        D = (ctypes.c_size_t * P)(*[int(d) for d in displs])
+        res, lines = _traced(lib, lambda: lib.ddl_testing_thread_allgatherv(P, S, R, C, D, DT_FLOAT, s))
+        torch.cuda.synchronize()
+        assert res['races'] == 0 and res['ops'] >= P * (P - 1), (res, lines)  # disjoint blocks: no conflicts at all
+
+
+@pytest.mark.parametrize('P', [3, 8])
+@pytest.mark.parametrize('algo', [0, 1, 2])
+def test_posted_dependencies_local_world(lib, gpu, P, algo):
+    """The one-GPU harness's scheduler (LocalWorld::run_, what the RCCL loopback and
+    ddl_local_ring_allreduce run) posts a race-free program too."""
+    n = 128 * 840 + 3
+    ins = [torch.randn(n, device=gpu) for _ in range(P)]
+    outs = [torch.empty_like(t) for t in ins]
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream().cuda_stream
+    send = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+    recv = (ctypes.c_void_p * P)(*[t.data_ptr() for t in outs])
+    with config(lib, algo=algo, reference_order=0, tune=0, slice_bytes=64 << 10):
+        res, lines = _traced(lib, lambda: lib.ddl_local_ring_allreduce(P, send, recv, n, DT_FLOAT, 0, s))
+    torch.cuda.synchronize()
+    assert res['races'] == 0 and res['ordered_reduce'] > 0, (res, lines)
 
 
 @pytest.mark.parametrize('every,want', [(0, 256), (8, 224), (4, 192), (2, 128)])
