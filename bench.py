@@ -275,13 +275,23 @@ def single_gpu(args):
         # once) instead of the run form (one input at a time over 16 KiB runs)
         extra['fold_kernel_tile_form'] = fold_roofline(lib, dev, sh, S, form=1)
         # C4's fold: one 16 MiB fp16 bucket at P = 8 -> 2 MiB chunk, 7 received inputs (cache-resident
-        # operands, as RCCL has just written them)
-        # (measured twice on fresh buffers, the better kept: the process's first fp16 graph reads
-        # 3.2 -> 4.6 us on some boxes whatever the form, tools/c4_form_ab.py)
+        # operands, as RCCL has just written them). Measured twice on fresh buffers; `us` is the MEAN
+        # of every replay round of both (the process's first fp16 graph reads slower on some boxes:
+        # that is part of the mean)
         c4a = fold_roofline(lib, dev, sh, 16 << 20, half=True)
         c4b = fold_roofline(lib, dev, sh, 16 << 20, half=True)
-        extra['fold_kernel_fp16_c4'] = dict(min((c4a, c4b), key=lambda r: r['us']),
-                                            measurements_us=[c4a['us'], c4b['us']])
+        rounds = c4a['rounds_us'] + c4b['rounds_us']
+        mean_us = sum(rounds) / len(rounds)
+        extra['fold_kernel_fp16_c4'] = dict(c4a, us=round(mean_us, 2), rounds_us=rounds,
+                                            achieved_GBs=round(c4a['algorithmic_bytes_per_launch'] / mean_us / 1e3, 1),
+                                            frac_of_peak=round(c4a['algorithmic_bytes_per_launch'] / mean_us / 1e3
+                                                               / HBM_PEAK_GBS, 4),
+                                            timing='mean of 2 x 3 replay rounds, 20 launches each, captured into '
+                                                   'a hipGraph, HIP events on the replay stream')
+        # ... and C4's 64 buckets folded the way the grouped allreduce folds them (ddl_allreduce_batch):
+        # 8 buckets' chunks per launch (FoldBatch), 8 launches over the 64 buckets (1.2 GB of
+        # operands: HBM, not the Infinity Cache)
+        extra['fold_kernel_fp16_c4_batch'] = fold_batch_roofline(lib, dev, sh)
         extra['reduce_half_dtypes_achieved_GBs'] = half_dtypes(lib, dev, sh, S)
 
     traffic = pmc_traffic(f'reduce_fp32_{args.bucket_mib}MiB')
@@ -317,10 +327,6 @@ def single_gpu(args):
         if not args.no_host:
             out['keyed_host_c5'] = keyed_host_c5(lib, Communicator.world(), steps=3)
             out['keyed_host_c5_pinned'] = keyed_host_c5(lib, Communicator.world(), steps=3, pinned=True)
-            # A/B: the large pinned inputs uploaded by DMA straight from the tensors (host_direct_dma,
-            # off by default) instead of packed by the copy threads into the pinned slots
-            out['keyed_host_c5_pinned_direct_dma'] = keyed_host_c5(
-                lib, Communicator.world(), steps=3, pinned=True, settings={'host_direct_dma': 1})
             # pageable tensors with the opt-in registration cache: registered on the first batch,
             # then the pinned paths
             out['keyed_host_c5_registered'] = keyed_host_c5(
@@ -343,6 +349,8 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
     es = 2 if half else 4
     n = S // 8 // es
     run_form = form == 2 or (form == 0 and n * es >= (4 << 20) and nb + 1 >= 7)
+    vec = n * es // 16
+    grid = (vec + 1024) // 1024 if run_form else (vec + 128) // 128  # workgroups (rocprof's grid / 128)
     old_form = lib.ddl_get_config(b'fold_form')
     check(lib.ddl_set_config(b'fold_form', form), 'ddl_set_config fold_form')
     sets = [[torch.rand(n, device=dev).to(torch.float16 if half else torch.float32) for _ in range(nb + 2)]
@@ -367,7 +375,7 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
             check(lib.ddl_reduce_fold_ordered(b[-1].data_ptr(), b[0].data_ptr(),
                                               P(*[t.data_ptr() for t in b[1:-1]]), nb, n, 19 if half else DT_FLOAT,
                                               order, sh_g), 'ddl_reduce_fold_ordered (captured)')
-    best = float('inf')
+    rounds = []
     for _ in range(3):
         with torch.cuda.stream(gs):
             graph.replay()
@@ -376,19 +384,74 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
             graph.replay()
             e1.record(gs)
         torch.cuda.synchronize()
-        best = min(best, e0.elapsed_time(e1) / 20 / 1e3)
+        rounds.append(e0.elapsed_time(e1) / 20 / 1e3)
+    best = sum(rounds) / len(rounds)  # the mean of the rounds (not the best)
     del graph
     check(lib.ddl_set_config(b'fold_form', old_form), 'ddl_set_config fold_form')
     byts = (nb + 2) * n * es
     kname = 'k_sumN_run' if run_form else 'k_sumN_tile'
     return {'kernel': f'{kname}<{"DDL_HALF" if half else "DDL_FLOAT"},{nb},order {order}>', 'chunk_bytes': n * es,
-            'timing': '20 launches captured into a hipGraph, replayed between HIP events on the replay stream',
-            'us': round(best * 1e6, 1),
+            'timing': '20 launches captured into a hipGraph, replayed between HIP events on the replay stream; '
+                      'mean of 3 rounds',
+            'us': round(best * 1e6, 2), 'rounds_us': [round(r * 1e6, 2) for r in rounds], 'grid_workgroups': grid,
             'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / best / 1e9, 1),
             'frac_of_peak': round(byts / best / 1e9 / HBM_PEAK_GBS, 4),
             'traffic': (pmc_traffic('fold_fp16_P8_C4_chunk') if half else
                         pmc_traffic('fold_fp32_P8_chunk_run' if run_form else 'fold_fp32_P8_chunk'))
             if order == 0 and ((S == 256 << 20 and not half) or (S == 16 << 20 and half)) else None}
+
+
+def fold_batch_roofline(lib, dev, sh, buckets=64, per_launch=8, bucket_bytes=16 << 20, P=8):
+    """C4's folds as the grouped allreduce launches them: `buckets` fp16 buckets of `bucket_bytes`
+    at P ranks -> one chunk of bucket_bytes / P per bucket with P - 1 received inputs; the chunks of
+    `per_launch` buckets share one launch (ddl_reduce_fold_batch, FoldBatch: blockIdx.y = bucket).
+    All buckets' operands live at once (64 x 9 x 2 MiB = 1.2 GB: HBM, not the Infinity Cache). The
+    launches of one pass over the buckets are captured into a hipGraph and replayed between HIP
+    events; `us` is the mean per launch over 3 rounds."""
+    import torch
+    from ddl.torch.cpp_backend import check
+    nb, es = P - 1, 2
+    n = bucket_bytes // P // es
+    sets = [[torch.rand(n, device=dev).half() for _ in range(nb + 2)] for _ in range(buckets)]  # in, inputs, out
+    V = ctypes.c_void_p
+    launches = []
+    for k in range(0, buckets, per_launch):
+        grp = sets[k:k + per_launch]
+        launches.append(((V * len(grp))(*[b[-1].data_ptr() for b in grp]), (V * len(grp))(*[b[0].data_ptr() for b in grp]),
+                         (V * (len(grp) * nb))(*[t.data_ptr() for b in grp for t in b[1:-1]]),
+                         (ctypes.c_size_t * len(grp))(*[n] * len(grp)), len(grp)))
+
+    def run(stream):
+        for outs, as_, ins, ns, c in launches:
+            check(lib.ddl_reduce_fold_batch(c, outs, as_, ins, nb, ns, 19, 0, stream), 'ddl_reduce_fold_batch')
+    run(sh)
+    torch.cuda.synchronize()
+    gs = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=gs):
+        run(gs.cuda_stream)
+    rounds = []
+    for _ in range(3):
+        with torch.cuda.stream(gs):
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(gs)
+            graph.replay()
+            e1.record(gs)
+        torch.cuda.synchronize()
+        rounds.append(e0.elapsed_time(e1) / len(launches) / 1e3)
+    del graph
+    t = sum(rounds) / len(rounds)
+    byts = (nb + 2) * n * es * per_launch
+    return {'kernel': f'k_sumN_tile<DDL_HALF,{nb},order 0> x {per_launch} problems (blockIdx.y)',
+            'chunk_bytes': n * es, 'problems_per_launch': per_launch, 'launches_per_pass': len(launches),
+            'grid_workgroups': ((n * es // 16 + 128) // 128) * per_launch,
+            'timing': f'{len(launches)} launches (all {buckets} buckets) captured into a hipGraph, replayed between HIP '
+                      'events on the replay stream; mean of 3 rounds',
+            'us': round(t * 1e6, 2), 'rounds_us': [round(r * 1e6, 2) for r in rounds],
+            'algorithmic_bytes_per_launch': byts, 'achieved_GBs': round(byts / t / 1e9, 1),
+            'frac_of_peak': round(byts / t / 1e9 / HBM_PEAK_GBS, 4),
+            'traffic': pmc_traffic('fold_fp16_P8_C4_batch8')}
 
 
 def half_dtypes(lib, dev, sh, S):
@@ -624,8 +687,9 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
         dt = (time.perf_counter() - t0) / steps
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
         # the engine thread's timeline per step: packing chunks into the pinned slots, waiting
-        # for a slot's DMA / device work, unpacking staged results; the rest is negotiation,
-        # planning and posting
+        # for a slot's DMA / device work, waiting for the unpack lane (staged results are unpacked
+        # by their own copy threads while the next chunks are packed, r04); the rest is
+        # negotiation, planning and posting
         tl = [(lib.ddl_get_config(kk) - v) / steps / 1e3 for kk, v in zip(tl_keys, tl0)]
         # plan_ms: the allreduce plans' staging loops (pack + slot waits + unpack + posting);
         # outside them: the pinned-output checks (check_ms), and the rest — submission,
@@ -646,8 +710,6 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
             'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path, 'engine_thread': timeline,
-            'host_direct_dma': int(lib.ddl_get_config(b'host_direct_dma')) if 'host_direct_dma' not in settings
-            else settings['host_direct_dma'],
             'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},
             **(registered if 'host_register_cache_bytes' in settings else {})}
 
@@ -723,6 +785,12 @@ def multi_gpu(args):
     if tranks.value != world:
         sys.stderr.write(f'[bench rank {rank}] the transport sees {tranks.value} ranks, the launcher {world}\n')
         sys.exit(2)
+    # which executor and transport each leg's collectives ran on
+    executor_path = ('RingExecutor::run_ over ' + {'rccl': 'RcclTransport (ncclSend/ncclRecv groups, ncclAllGather)',
+                                                     'test_transport_gloo': 'CallbackTransport (gloo host copies)',
+                                                     'none': 'no transport (one rank)'}[transport['kind']])
+    keyed_path = ('RequestHandler (star negotiation over TCP) -> FusionPipe -> the private keyed communicator\'s '
+                  + executor_path)
     dev = torch.device('cuda', local)
     S = args.bucket_mib << 20
     n = S // 4
@@ -812,6 +880,11 @@ def multi_gpu(args):
                    'reference_order': lib.ddl_get_config(b'reference_order')},
         'value_is': 'allreduce algbw: bucket bytes / max-over-ranks time per allreduce (GiB/s)',
         'transport': transport,
+        'legs_path': {'headline, parity, schedule_sweep, c4, size_sweep, broadcast_allgather': executor_path,
+                      'host_resident': 'ddl_allreduce_host: H2D / D2H chunks around ' + executor_path,
+                      'fusion_c5, keyed_bucket_stream, keyed_c1_latency, keyed_host_c5_pinned': keyed_path,
+                      'rccl_allreduce_comparator': "RCCL's own ncclAllReduce on the world's communicator",
+                      'compute_cu_mask_ab': 'a split communicator: ' + executor_path},
         'algbw_GiBs': round(algbw, 2),
         'busbw_GBs': round(busbw_gbs, 2),
         'link_roofline': (None if ceiling is None else
@@ -913,7 +986,22 @@ def multi_gpu(args):
             t = timed_fn(c4_step, 3, 1)
             out['c4_fp16_64x16MiB'] = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
                                        'algbw_GiBs': round((1 << 30) / GiB / t, 2),
-                                       'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2)}
+                                       'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2),
+                                       'path': 'one ddl_allreduce per bucket: ' + executor_path}
+            # the same 64 buckets as ONE grouped call (ddl_allreduce_batch): one RCCL group per tick for
+            # every bucket, the folds of 8 buckets per launch; bit-identical sums
+            V = ctypes.c_void_p * 64
+            ptrs = V(*[b.data_ptr() for b in c4_bufs])
+            counts = (ctypes.c_size_t * 64)(*[nb] * 64)
+
+            def c4_batch_step():
+                check(lib.ddl_allreduce_batch(comm.id, 64, ptrs, ptrs, counts, 19, 0, stream.cuda_stream),
+                      'ddl_allreduce_batch')
+            t = timed_fn(c4_batch_step, 3, 1)
+            out['c4_fp16_64x16MiB_batch'] = {'buckets': 64, 'bucket_bytes': 16 << 20, 'ms': round(t * 1e3, 3),
+                                             'algbw_GiBs': round((1 << 30) / GiB / t, 2),
+                                             'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2),
+                                             'path': 'one ddl_allreduce_batch of 64 buckets: ' + executor_path}
             del c4_bufs
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['c4'] = repr(e)[:400]

@@ -334,14 +334,10 @@ int ddl_set_config(const char *key, long long value) {
         else if (k == "host_chunk_bytes") {
             DDL_REQUIRE(value >= 4096, DDL_STATUS_INVALID_ARGUMENT, "host_chunk_bytes must be >= 4096");
             c.host_chunk_bytes = value;
-        } else if (k == "host_taper") {
-            DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT, "host_taper must be 0, 1 or 2");
-            c.host_taper = value;
         } else if (k == "host_copy_threads") {
             DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
             c.host_copy_threads = value;
         } else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
-        else if (k == "host_direct_dma") c.host_direct_dma = value ? 1 : 0;
         else if (k == "host_numa_bind") c.host_numa_bind = value ? 1 : 0;
         else if (k == "host_register_cache_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "host_register_cache_bytes must be >= 0");
@@ -388,11 +384,9 @@ long long ddl_get_config(const char *key) {
     if (k == "log_level") return c.log_level;
     if (k == "cycle_time_us") return c.cycle_time_us;
     if (k == "host_chunk_bytes") return c.host_chunk_bytes;
-    if (k == "host_taper") return c.host_taper;
     if (k == "tune") return c.tune;
     if (k == "host_copy_threads") return c.host_copy_threads;
     if (k == "host_zero_copy") return c.host_zero_copy;
-    if (k == "host_direct_dma") return c.host_direct_dma;
     if (k == "host_register_cache_bytes") return c.host_register_cache_bytes;
     if (k == "host_numa_bind") return c.host_numa_bind;
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
@@ -455,6 +449,13 @@ void py_error(const char *s) { DDL_LOG(0, "[py]: " << (s ? s : "")); }
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements, int dtype,
                   int op, void *hip_stream) {
     return guarded([&] { Registry::get().find(id)->allreduce(send, recv, elements, dtype, op, as_stream(hip_stream)); });
+}
+
+int ddl_allreduce_batch(ddl_communicator_id id, int count, const void *const *sends, void *const *recvs,
+                        const size_t *elements, int dtype, int op, void *hip_stream) {
+    return guarded([&] {
+        Registry::get().find(id)->allreduce_batch(sends, recvs, elements, count, dtype, op, as_stream(hip_stream));
+    });
 }
 
 int ddl_broadcast(ddl_communicator_id id, void *buf, size_t elements, int dtype, int root, void *hip_stream) {
@@ -774,6 +775,25 @@ int ddl_reduce_fold_ordered(void *out, const void *a, const void *const *ins, in
     });
 }
 
+int ddl_reduce_fold_batch(int count, void *const *outs, const void *const *as, const void *const *ins, int nb,
+                          const size_t *elements, int dtype, int order, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(count >= 1 && count <= kMaxFoldBatch && outs && as && ins && elements, DDL_STATUS_INVALID_ARGUMENT,
+                    "fold batch of " << count << " (1.." << kMaxFoldBatch << ")");
+        DDL_REQUIRE(nb >= 1 && nb <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "fold inputs " << nb);
+        std::vector<SegTableN> t(count);
+        for (int p = 0; p < count; ++p) {
+            t[p].a = as[p];
+            t[p].out = outs[p];
+            t[p].n = elements[p];
+            t[p].nb = nb;
+            t[p].order = order;
+            for (int i = 0; i < nb; ++i) t[p].b[i] = ins[(size_t)p * nb + i];
+        }
+        launch_sumN_batch(t.data(), count, dtype, as_stream(hip_stream));
+    });
+}
+
 int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
                     void *hip_stream) {
     return ddl_reduce_fold_ordered(out, a, ins, nb, elements, dtype, kFoldLeft, hip_stream);
@@ -814,6 +834,16 @@ int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *
     });
 }
 
+int ddl_local_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                              const size_t *elements, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && count >= 0 && (count == 0 || (sends && recvs && elements)),
+                    DDL_STATUS_INVALID_ARGUMENT, "bad local allreduce batch");
+        (void)current_device();
+        local_world(nranks).allreduce_batch(sends, recvs, elements, count, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
 int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream) {
     return guarded([&] {
         DDL_REQUIRE(nranks >= 1 && nranks <= 64, DDL_STATUS_INVALID_ARGUMENT, "nranks " << nranks);
@@ -840,6 +870,16 @@ int ddl_testing_thread_allreduce(int nranks, const void *const *sends, void *con
     return guarded([&] {
         DDL_REQUIRE(nranks >= 1 && nranks <= 64 && sends && recvs, DDL_STATUS_INVALID_ARGUMENT, "bad thread allreduce");
         thread_world(nranks).allreduce(sends, recvs, elements, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_testing_thread_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                                       const size_t *elements, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && count >= 0 && (count == 0 || (sends && recvs && elements)),
+                    DDL_STATUS_INVALID_ARGUMENT, "bad thread allreduce batch");
+        thread_world(nranks).allreduce_batch(sends, recvs, elements, count, dtype, as_stream(hip_stream),
+                                             config().ring());
     });
 }
 
@@ -924,7 +964,7 @@ int ddl_testing_host_chunk_cuts(size_t total_bytes, size_t chunk_bytes, size_t *
         DDL_REQUIRE(count && (cuts || cap == 0), DDL_STATUS_INVALID_ARGUMENT, "null output");
         DDL_REQUIRE(chunk_bytes >= 256 && chunk_bytes % 256 == 0, DDL_STATUS_INVALID_ARGUMENT,
                     "chunk_bytes " << chunk_bytes << " is not a positive multiple of 256");
-        const std::vector<size_t> cut = host_chunk_cuts(total_bytes, chunk_bytes, (int)config().host_taper.load());
+        const std::vector<size_t> cut = host_chunk_cuts(total_bytes, chunk_bytes);
         for (size_t i = 0; i < cut.size() && i < cap; ++i) cuts[i] = cut[i];
         *count = cut.size();
     });
@@ -967,6 +1007,17 @@ int ddl_rccl_loopback_allreduce(int nranks, const void *const *sends, void *cons
         RcclLoopback &l = rccl_loopback();
         std::lock_guard<std::mutex> g(l.mu);
         l.world(nranks).allreduce(sends, recvs, elements, dtype, as_stream(hip_stream), config().ring());
+    });
+}
+
+int ddl_rccl_loopback_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                                      const size_t *elements, int dtype, void *hip_stream) {
+    return guarded([&] {
+        DDL_REQUIRE(nranks >= 1 && nranks <= 64 && count >= 0 && (count == 0 || (sends && recvs && elements)),
+                    DDL_STATUS_INVALID_ARGUMENT, "bad loopback allreduce batch");
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> g(l.mu);
+        l.world(nranks).allreduce_batch(sends, recvs, elements, count, dtype, as_stream(hip_stream), config().ring());
     });
 }
 

@@ -130,6 +130,16 @@ struct SegTableN {
 // fp32/fp64/int: one rounding per add in `order`; fp16/bf16 (no reference order: the reference
 // rejects them): accumulate in fp32 and round once at the end, whatever the order.
 void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream);
+// Up to kMaxFoldBatch independent folds with the same input count and order in ONE launch
+// (blockIdx.y = problem): the grouped allreduce folds every bucket's slice of a tick together, so
+// 64 back-to-back 2 MiB fp16 chunks (C4) become 8 launches of 8 chunks instead of 64 latency-bound
+// ones. No problem may read what another writes. Misaligned problems are launched one by one.
+constexpr int kMaxFoldBatch = 8;
+struct FoldBatch {
+    SegTableN t[kMaxFoldBatch];
+    int count;
+};
+void launch_sumN_batch(const SegTableN *t, int count, int dtype, hipStream_t stream);
 
 // Reduce-kernel cache-policy / staging flags (bit set). kVariantDefault is what the engine uses;
 // the others exist for measurement (ddl_reduce_sum2_variant, bench.py, tools/reduce_tune.hip).
@@ -162,24 +172,14 @@ int device_cu_count();
 void launch_capture_anchor(hipStream_t stream);
 
 // Chunk boundaries [cut[i], cut[i + 1]) of a host-staged transfer of `total` bytes through
-// `chunk`-byte slots (chunk a multiple of 256): whole chunks (taper 0, config "host_taper"
-// default); with taper 1 the last two chunks' worth of a transfer longer than two chunks, and with
-// taper 2 also the first chunk's worth of one longer than three, are cut in quarter chunks. That
-// shortens the pipeline's fill (the first chunk's pack and upload, before any other engine has
-// work) and drain (the device work and download still in flight when the host loop ends), but
-// quarter chunks keep a quarter as many bytes in the slots in flight: measured on one box,
-// interleaved, whole chunks were as fast or faster. Boundaries are multiples of 256
-// that depend only on (total, chunk, taper) — a shared tunable — so every rank cuts the same
-// chunks (the per-chunk collectives must match).
-inline std::vector<size_t> host_chunk_cuts(size_t total, size_t chunk, int taper) {
+// `chunk`-byte slots (chunk a multiple of 256): whole chunks, the last one short. They depend
+// only on (total, chunk) — host_chunk_bytes is a shared tunable — so every rank cuts the same
+// chunks (the per-chunk collectives must match). (r03 measured quarter chunks at the ends of a
+// transfer — a shorter fill and drain — against whole chunks on two boxes: never faster, DESIGN §7;
+// that option is gone.)
+inline std::vector<size_t> host_chunk_cuts(size_t total, size_t chunk) {
     std::vector<size_t> cut{0};
-    const size_t piece = std::max<size_t>(256, (chunk / 4) & ~size_t(255));
-    while (cut.back() < total) {
-        const size_t at = cut.back(), left = total - at;
-        const bool quarter = (taper >= 1 && total > 2 * chunk && left <= 2 * chunk) ||
-                             (taper >= 2 && total > 3 * chunk && at < chunk);
-        cut.push_back(at + std::min(quarter ? piece : chunk, left));
-    }
+    while (cut.back() < total) cut.push_back(cut.back() + std::min(chunk, total - cut.back()));
     return cut;
 }
 

@@ -39,7 +39,7 @@ Config &config() {
 uint64_t Config::shared_hash() const {
     const long long v[] = {algo.load(), slice_bytes.load(), rings.load(), max_slices.load(),
                            fusion_threshold_bytes.load(), tune.load(), fusion_pipeline_bytes.load(),
-                           reference_order.load(), host_chunk_bytes.load(), host_taper.load()};
+                           reference_order.load(), host_chunk_bytes.load()};
     uint64_t h = 1469598103934665603ull;  // FNV-1a over the values' bytes
     for (long long x : v)
         for (int b = 0; b < 8; ++b) {
@@ -187,7 +187,7 @@ void check_config_agreement(int rank, const std::vector<uint64_t> &hashes) {
     if (same) return;
     std::ostringstream os;
     os << "shared tunables differ between ranks (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, "
-          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes, host_taper must be set alike on every rank); "
+          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes must be set alike on every rank); "
           "config hash per rank:";
     for (size_t q = 0; q < hashes.size(); ++q)
         os << " " << q << (q == (size_t)rank ? "*" : "") << "=" << std::hex << hashes[q] << std::dec;
@@ -230,6 +230,23 @@ void Communicator::allreduce(const void *send, void *recv, size_t n, int dtype, 
     RingConfig cfg = ring_config(n, dtype, stream);
     cfg.order_bytes = order_bytes;
     exec_->allreduce(send, recv, n, dtype, stream, cfg);
+}
+
+void Communicator::allreduce_batch(const void *const *send, void *const *recv, const size_t *n, int count, int dtype,
+                                   int op, hipStream_t stream) {
+    DDL_REQUIRE(op == DDL_ALLREDUCE_OP_SUM, DDL_STATUS_INVALID_ARGUMENT, "only SUM is supported (op " << op << ")");
+    DDL_REQUIRE(dtype_size(dtype) != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    DDL_REQUIRE(count >= 0 && (count == 0 || (send && recv && n)), DDL_STATUS_INVALID_ARGUMENT, "null bucket arrays");
+    size_t largest = 0;
+    for (int b = 0; b < count; ++b) {
+        DDL_REQUIRE(n[b] == 0 || (send[b] && recv[b]), DDL_STATUS_INVALID_ARGUMENT, "null buffer in bucket " << b);
+        largest = std::max(largest, n[b]);
+    }
+    UserCollective uc(*this);
+    std::lock_guard<std::mutex> g(mu_);
+    DeviceGuard dg(device_);
+    const RingConfig cfg = ring_config(largest, dtype, stream);
+    exec_->allreduce_batch(send, recv, n, count, dtype, stream, cfg);
 }
 
 void Communicator::rccl_allreduce(const void *send, void *recv, size_t n, int dtype, hipStream_t stream) {
@@ -512,9 +529,7 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
         }
         RingConfig cfg = ring_config(chunk / es, dtype, ring_);
         cfg.order_bytes = total;  // the reference reduces the whole host buffer in one call
-        // whole chunks, or quarter chunks at the ends ("host_taper": the first H2D runs alone
-        // before any D2H can overlap it, and so does the last D2H; measured no faster)
-        const std::vector<size_t> cut = host_chunk_cuts(total, chunk, (int)config().host_taper.load());
+        const std::vector<size_t> cut = host_chunk_cuts(total, chunk);
         const size_t nchunks = cut.size() - 1;
         for (size_t i = 0; i < nchunks; ++i) {
             const int s = (int)(i % kHostSlots);

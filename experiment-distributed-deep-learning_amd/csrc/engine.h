@@ -36,10 +36,6 @@ struct Config {
     std::atomic<long long> cycle_time_us{0};
     // host-resident pipeline chunk (ddl_allreduce_host, keyed host requests)
     std::atomic<long long> host_chunk_bytes{32ll << 20};
-    // quarter chunks at the ends of a long host-staged transfer (host_chunk_cuts): 0 whole chunks
-    // only (default: fastest in the interleaved A/B, profiles/r03/host/host_taper_ab.jsonl), 1 the
-    // last two chunks' worth, 2 that and the first chunk's worth
-    std::atomic<long long> host_taper{0};
     // memcpy workers of the keyed host-staging pipeline (pageable <-> pinned), besides the
     // engine thread itself
     std::atomic<long long> host_copy_threads{7};
@@ -47,11 +43,6 @@ struct Config {
     // address space (torch pin_memory, hipHostMalloc, hipHostRegister): the unpack kernel writes
     // them over PCIe in place of the D2H copy and the host unpack memcpy (1 on, 0 always stage)
     std::atomic<long long> host_zero_copy{1};
-    // keyed host plans: input segments in pinned memory of >= 256 KiB are uploaded by DMA straight
-    // from the tensor instead of host memcpy into the pinned slot + one DMA per chunk (1 on, 0 off,
-    // default: measured slower on the C5 set, 111 vs 62 ms — the many small DMAs of one chunk
-    // serialise on the upload stream; bench keyed_host_c5_pinned_direct_dma)
-    std::atomic<long long> host_direct_dma{0};
     // keyed host requests: pageable tensors are hipHostRegister'ed once and the registration kept
     // (up to this many bytes, least recently used out), so repeated allreduce(cpu_tensor) calls take
     // the pinned paths. 0 (default) = off: a registered range must stay allocated while cached —
@@ -120,8 +111,7 @@ struct Config {
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'
     // programs, the fusion plans and the host chunks): algo, slice_bytes, rings, max_slices,
-    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes,
-    // host_taper.
+    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes.
     // Never 0 or kCfgMismatch. Local tunables (log_level, cycle_time_us, host_copy_threads,
     // host_zero_copy, pipeline_rounds, one_rank_shortcut) are not in it.
     uint64_t shared_hash() const;
@@ -176,6 +166,10 @@ public:
     // Host-resident buckets (the reference's deployment case: framework CPU tensors behind the
     // MPI buffers): chunked pinned H2D -> device ring -> D2H pipeline; returns when recv holds
     // the result.
+    // `count` buckets of one dtype in one grouped program (RingExecutor::allreduce_batch); the
+    // schedule is the one tuned for the largest bucket's size class
+    void allreduce_batch(const void *const *send, void *const *recv, const size_t *n, int count, int dtype, int op,
+                         hipStream_t stream);
     void allreduce_host(const void *send, void *recv, size_t n, int dtype, int op);
     // Communicator::broadcast (reference Communicator.h:81-92): root's n elements of `buf` into
     // every rank's `buf`, stream-ordered.

@@ -195,12 +195,33 @@ void *RankResources::ensure_staging(size_t bytes, bool capturing) {
 
 double launch_tick_reduce(const Tick &tk, int dtype, hipStream_t stream) {
     const double es = (double)dtype_size(dtype);
-    if (tk.multi) {  // fold steps in order on the compute stream
+    if (tk.multi) {
+        // fold steps in order on the compute stream; consecutive independent steps of one shape
+        // (a grouped allreduce's buckets) share a launch, kMaxFoldBatch at a time
         double bytes = 0;
+        std::vector<SegTableN> batch;
+        auto flush = [&] {
+            if (!batch.empty()) launch_sumN_batch(batch.data(), (int)batch.size(), dtype, stream);
+            batch.clear();
+        };
+        auto meets = [es](const void *p, uint64_t pn, const void *q, uint64_t qn) {
+            const uintptr_t a = (uintptr_t)p, b = (uintptr_t)q;
+            return a < b + qn * es && b < a + pn * es;
+        };
         for (const SegTableN &f : tk.folds) {
-            launch_sumN(f, dtype, stream);
+            bool joins = !batch.empty() && (int)batch.size() < kMaxFoldBatch && f.nb == batch[0].nb &&
+                         f.order == batch[0].order;
+            for (size_t i = 0; joins && i < batch.size(); ++i) {  // no step reads or writes another's output
+                const SegTableN &g = batch[i];
+                joins = !meets(f.out, f.n, g.out, g.n) && !meets(f.a, f.n, g.out, g.n) && !meets(g.a, g.n, f.out, f.n);
+                for (int k = 0; joins && k < f.nb; ++k) joins = !meets(f.b[k], f.n, g.out, g.n);
+                for (int k = 0; joins && k < g.nb; ++k) joins = !meets(g.b[k], g.n, f.out, f.n);
+            }
+            if (!joins) flush();
+            batch.push_back(f);
             bytes += (f.nb + 2.0) * (double)f.n * es;
         }
+        flush();
         return bytes;
     }
     launch_sum2(tk.reduce, dtype, stream, ring_variant());
@@ -280,6 +301,21 @@ void RingExecutor::allreduce(const void *in, void *out, size_t n, int dtype, hip
     }
     void *staging = res_.ensure_staging(program_staging_elems(n, es, size_, cfg) * es, stream_capturing(user));
     build_program(prog_, rank_, size_, in, out, staging, n, dtype, cfg);
+    run_(dtype, user);
+}
+
+void RingExecutor::allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                                   hipStream_t user, const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (size_ == 1) {
+        for (int b = 0; b < count; ++b)
+            if (n[b] && in[b] != out[b]) DDL_HIP(hipMemcpyAsync(out[b], in[b], n[b] * es, hipMemcpyDeviceToDevice, user));
+        return;
+    }
+    void *staging = res_.ensure_staging(std::max<size_t>(1, batch_staging_elems(n, count, es, size_, cfg)) * es,
+                                        stream_capturing(user));
+    build_batch_program(prog_, rank_, size_, in, out, n, count, staging, dtype, cfg);
     run_(dtype, user);
 }
 
@@ -638,6 +674,13 @@ void ThreadWorld::allgatherv(const void *const *sends, void *const *recvs, const
     run_(user, [&](int r, hipStream_t s) { ex_[r]->allgatherv(sends[r], recvs[r], counts, displs, dtype, s); });
 }
 
+void ThreadWorld::allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                                  hipStream_t user, const RingConfig &cfg) {
+    run_(user, [&](int r, hipStream_t s) {
+        ex_[r]->allreduce_batch(in + (size_t)r * count, out + (size_t)r * count, n, count, dtype, s, cfg);
+    });
+}
+
 size_t ThreadWorld::fused_allreduce(const void *const *srcs, void *const *dsts, const size_t *bytes, int count,
                                     int dtype, hipStream_t user, const RingConfig &cfg, size_t cap) {
     while (pipes_.size() < (size_t)P_) pipes_.emplace_back(new FusionPipe);
@@ -695,6 +738,24 @@ void LocalWorld::allreduce(const void *const *in, void *const *out, size_t n, in
     for (int r = 0; r < P_; ++r) {
         void *st = res_[r]->ensure_staging(program_staging_elems(n, es, P_, cfg) * es, capture);
         build_program(progs_[r], r, P_, in[r], out[r], st, n, dtype, cfg);
+    }
+    run_(dtype, user);
+}
+
+void LocalWorld::allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                                 hipStream_t user, const RingConfig &cfg) {
+    const size_t es = dtype_size(dtype);
+    DDL_REQUIRE(es != 0, DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype " << dtype);
+    if (P_ == 1) {
+        for (int b = 0; b < count; ++b)
+            if (n[b] && in[b] != out[b]) DDL_HIP(hipMemcpyAsync(out[b], in[b], n[b] * es, hipMemcpyDeviceToDevice, user));
+        return;
+    }
+    const bool capture = stream_capturing(user);
+    const size_t elems = std::max<size_t>(1, batch_staging_elems(n, count, es, P_, cfg));
+    for (int r = 0; r < P_; ++r) {
+        void *st = res_[r]->ensure_staging(elems * es, capture);
+        build_batch_program(progs_[r], r, P_, in + (size_t)r * count, out + (size_t)r * count, n, count, st, dtype, cfg);
     }
     run_(dtype, user);
 }

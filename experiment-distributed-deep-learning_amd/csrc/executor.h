@@ -239,6 +239,10 @@ public:
     ~RingExecutor();
     void allreduce(const void *in, void *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
+    // `count` buckets of one dtype as one grouped program (build_batch_program): one group and
+    // batched folds per tick instead of a program per bucket
+    void allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                         hipStream_t user, const RingConfig &cfg);
     void broadcast(void *buf, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
     void allgatherv(const void *send, void *recv, const size_t *counts, const size_t *displs, int dtype,
                     hipStream_t user);
@@ -275,6 +279,9 @@ public:
     ~LocalWorld();
     void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
+    // in[r * count + b] / out[r * count + b]: rank r's bucket b (RingExecutor::allreduce_batch)
+    void allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                         hipStream_t user, const RingConfig &cfg);
     void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
     void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
                     int dtype, hipStream_t user);
@@ -305,6 +312,9 @@ public:
     ~ThreadWorld();
     void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
+    // in[r * count + b] / out[r * count + b]: rank r's bucket b (RingExecutor::allreduce_batch)
+    void allreduce_batch(const void *const *in, void *const *out, const size_t *n, int count, int dtype,
+                         hipStream_t user, const RingConfig &cfg);
     void broadcast(void *const *bufs, size_t n, int dtype, int root, hipStream_t user, const RingConfig &cfg);
     void allgatherv(const void *const *sends, void *const *recvs, const size_t *counts, const size_t *displs,
                     int dtype, hipStream_t user);

@@ -164,6 +164,79 @@ void bind_this_thread(const std::vector<int> &cpus) {
 }
 }  // namespace
 
+AsyncLane::AsyncLane(std::vector<int> cpus) : cpus_(std::move(cpus)) {
+    thread_ = std::thread(&AsyncLane::worker_, this);
+}
+
+AsyncLane::~AsyncLane() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    if (thread_.joinable()) thread_.join();
+}
+
+uint64_t AsyncLane::submit(std::function<void()> job) {
+    uint64_t seq;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        q_.push_back(std::move(job));
+        seq = ++submitted_;
+    }
+    cv_.notify_one();
+    return seq;
+}
+
+void AsyncLane::wait(uint64_t seq) {
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return done_ >= seq; });
+    if (failed_) {
+        failed_ = false;
+        throw err_;
+    }
+}
+
+void AsyncLane::drain() noexcept {
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return done_ >= submitted_; });
+    failed_ = false;
+}
+
+void AsyncLane::worker_() {
+    bind_this_thread(cpus_);
+    for (;;) {
+        std::function<void()> job;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;  // stop_, nothing left
+            job = std::move(q_.front());
+            q_.pop_front();
+        }
+        bool bad = false;
+        Error e{0, ""};
+        try {
+            job();
+        } catch (const Error &x) {
+            bad = true;
+            e = x;
+        } catch (const std::exception &x) {
+            bad = true;
+            e = Error{DDL_STATUS_ERROR_UNKNOWN, x.what()};
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (bad && !failed_) {
+                failed_ = true;
+                err_ = e;
+            }
+            ++done_;
+        }
+        done_cv_.notify_all();
+    }
+}
+
 CopyPool::CopyPool(int threads, std::vector<int> cpus) : cpus_(std::move(cpus)) {
     for (int i = 0; i < threads; ++i) threads_.emplace_back(&CopyPool::worker_, this);
 }
@@ -299,6 +372,7 @@ RequestHandler::~RequestHandler() {
     done_cv_.notify_all();
     if (done_thread_.joinable()) done_thread_.join();
     fail_all_(DDL_STATUS_COMM_ERROR);
+    if (lane_) lane_->drain();  // unpack jobs read the pinned download slots freed below
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     if (gather_) (void)hipFree(gather_);
     if (dims_) (void)hipFree(dims_);
@@ -307,6 +381,7 @@ RequestHandler::~RequestHandler() {
         if (st) (void)hipStreamSynchronize(st);
     for (int k = 0; k < kHostSlots; ++k) {
         if (pin_[k]) (void)hipHostFree(pin_[k]);
+        if (pout_[k]) (void)hipHostFree(pout_[k]);
         if (dslot_[k]) (void)hipFree(dslot_[k]);
     }
     for (hipEvent_t e : hev_)
@@ -852,13 +927,15 @@ size_t RequestHandler::host_slots_(size_t total) {
             if (st) DDL_HIP(hipStreamSynchronize(st));
         for (int k = 0; k < kHostSlots; ++k) {
             if (pin_[k]) DDL_HIP(hipHostFree(pin_[k]));
+            if (pout_[k]) DDL_HIP(hipHostFree(pout_[k]));
             if (dslot_[k]) DDL_HIP(hipFree(dslot_[k]));
-            pin_[k] = dslot_[k] = nullptr;
+            pin_[k] = pout_[k] = dslot_[k] = nullptr;
             slot_used_[k] = false;
         }
         host_slot_bytes_ = 0;
         for (int k = 0; k < kHostSlots; ++k) {
             DDL_HIP(hipHostMalloc(&pin_[k], chunk, hipHostMallocDefault));
+            DDL_HIP(hipHostMalloc(&pout_[k], chunk, hipHostMallocDefault));
             DDL_HIP(hipMalloc(&dslot_[k], chunk));
         }
         host_slot_bytes_ = chunk;
@@ -876,9 +953,13 @@ CopyPool &RequestHandler::pool_for_config_() {
     // using the old pool here); r02's thread-count sweep ran every setting on the first pool
     const int want = (int)std::max(0ll, config().host_copy_threads.load());
     if (!pool_ || pool_->threads() != want) {
+        if (lane_) lane_->drain();  // no unpack job may still use out_pool_
         pool_.reset();
         pool_.reset(new CopyPool(want, local_cpus_));
+        out_pool_.reset();
+        out_pool_.reset(new CopyPool(want, local_cpus_));
     }
+    if (!lane_) lane_.reset(new AsyncLane(local_cpus_));
     return *pool_;
 }
 
@@ -890,9 +971,8 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     const size_t chunk = host_slots_(total);
     pool_for_config_();
     if (device_unpack) config().host_zero_copy_plans.fetch_add(1);
-    // chunk boundaries (the same on every rank): whole chunks, or quarter chunks at the ends of a
-    // long plan ("host_taper")
-    const std::vector<size_t> cut = host_chunk_cuts(total, chunk, (int)config().host_taper.load());
+    // chunk boundaries (the same on every rank)
+    const std::vector<size_t> cut = host_chunk_cuts(total, chunk);
     const size_t nchunks = cut.size() - 1;
     std::vector<CopyPool::Piece> pieces;
     // timeline statistics (config "host_pack_us" / "host_wait_us" / "host_unpack_us"): where the
@@ -902,34 +982,33 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     auto ns_since = [](clk::time_point t0) {  // summed in ns: a 4 KiB chunk's unpack is < 1 us
         return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
     };
-    auto unpack = [&](size_t j) {
+    // staged outputs: chunk j's D2H lands in the download slot pout_[j % kHostSlots] and its host
+    // unpack runs on the unpack lane (out_pool_'s copy threads) — concurrently with the engine
+    // thread's packs of the next chunks into the upload slots. Before the D2H of chunk j + kHostSlots
+    // reuses the download slot, the engine thread waits for chunk j's unpack (host_unpack_us).
+    std::vector<uint64_t> unpacked(nchunks, 0);  // lane job of chunk j
+    const int dev = owner_->device();
+    auto unpack_async = [&](size_t j) {
         const int k = (int)(j % kHostSlots);
-        clk::time_point t0 = clk::now();
-        DDL_HIP(hipEventSynchronize(hev_[3 * k + 2]));  // D2H of chunk j landed
-        config().host_wait_ns.fetch_add(ns_since(t0));
-        t0 = clk::now();
-        const size_t off = cut[j];
-        pieces.clear();
-        host_pieces_(segs, starts, off, cut[j + 1] - off, static_cast<char *>(pin_[k]), false, pieces);
-        pool_->run(pieces);
+        std::vector<CopyPool::Piece> pc;
+        host_pieces_(segs, starts, cut[j], cut[j + 1] - cut[j], static_cast<char *>(pout_[k]), false, pc);
+        const hipEvent_t landed = hev_[3 * k + 2];  // re-recorded only after this job (wait_unpack)
+        CopyPool *op = out_pool_.get();
+        unpacked[j] = lane_->submit([dev, landed, op, pc = std::move(pc)] {
+            DeviceGuard g(dev);
+            DDL_HIP(hipEventSynchronize(landed));  // D2H of chunk j landed
+            op->run(pc);
+        });
+    };
+    auto wait_unpack = [&](size_t j) {
+        const clk::time_point t0 = clk::now();
+        lane_->wait(unpacked[j]);
         config().host_unpack_ns.fetch_add(ns_since(t0));
     };
     std::vector<void *> dst;
     std::vector<size_t> len;
-    // inputs in pinned, device-mapped memory (torch pin_memory, hipHostMalloc, hipHostRegister):
-    // their large pieces are uploaded by DMA straight from the tensors
-    std::vector<char> direct;
-    if (upload && config().host_direct_dma.load()) {
-        bool any = false;
-        direct.assign(segs.size(), 0);
-        for (size_t i = 0; i < segs.size(); ++i)
-            if (segs[i].bytes >= kDirectDmaMin && mapped_host_range(segs[i].src, segs[i].bytes))
-                direct[i] = any = true;
-        if (!any) direct.clear();
-    }
     for (size_t i = 0; i < nchunks; ++i) {
         const int k = (int)(i % kHostSlots);
-        if (i >= (size_t)kHostSlots && !device_unpack) unpack(i - kHostSlots);  // frees slot k (pinned and device)
         const size_t off = cut[i], n = cut[i + 1] - off;
         // the device slot's last user may still be in flight (a device unpack)
         if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
@@ -940,43 +1019,10 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
             if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
             config().host_wait_ns.fetch_add(ns_since(t0));
             t0 = clk::now();
-            if (!direct.empty()) {
-                // pieces of pinned inputs (segments flagged in `direct`) go straight from the
-                // tensor to the device slot by DMA, no host memcpy; the others are packed into
-                // the pinned slot and uploaded as runs between them
-                pieces.clear();
-                std::vector<std::pair<size_t, size_t>> runs;  // [lo, hi) of the chunk, from pin_[k]
-                std::vector<CopyPool::Piece> dmas;             // straight from the tensors
-                char *pin = static_cast<char *>(pin_[k]);
-                char *dev = static_cast<char *>(dslot_[k]);
-                bool after_dma = true;
-                const size_t end = off + n;
-                for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
-                     j < segs.size() && starts[j] < end; ++j) {
-                    const size_t lo = std::max(off, starts[j]), hi = std::min(end, starts[j] + segs[j].bytes);
-                    if (hi <= lo) continue;
-                    const char *src = segs[j].src + (lo - starts[j]);
-                    if (direct[j]) {
-                        dmas.push_back(CopyPool::Piece{dev + (lo - off), src, hi - lo});
-                        after_dma = true;
-                        continue;
-                    }
-                    pieces.push_back(CopyPool::Piece{pin + (lo - off), src, hi - lo});
-                    if (after_dma) runs.emplace_back(lo - off, hi - off);
-                    else runs.back().second = hi - off;  // padding between pieces is harmless
-                    after_dma = false;
-                }
-                pool_->run(pieces);
-                for (const auto &r : runs)
-                    DDL_HIP(hipMemcpyAsync(dev + r.first, pin + r.first, r.second - r.first, hipMemcpyHostToDevice, h2d_));
-                for (const CopyPool::Piece &d : dmas)
-                    DDL_HIP(hipMemcpyAsync(d.dst, d.src, d.bytes, hipMemcpyHostToDevice, h2d_));
-            } else {
-                pieces.clear();
-                host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
-                pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
-                DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
-            }
+            pieces.clear();
+            host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
+            pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
+            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
             config().host_pack_ns.fetch_add(ns_since(t0));
         }
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
@@ -1003,17 +1049,19 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
             }
             fp_.copier.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
         } else {
-            DDL_HIP(hipMemcpyAsync(pin_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
+            if (i >= (size_t)kHostSlots) wait_unpack(i - kHostSlots);  // download slot k free again
+            DDL_HIP(hipMemcpyAsync(pout_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
         }
         DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
         slot_used_[k] = true;
+        if (!device_unpack) unpack_async(i);
     }
     if (device_unpack) {
         // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * ((nchunks - 1) % kHostSlots) + 2], 0));
         return;
     }
-    for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) unpack(j);
+    for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) wait_unpack(j);
 }
 
 void RequestHandler::release_registrations() {

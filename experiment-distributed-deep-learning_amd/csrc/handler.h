@@ -104,6 +104,33 @@ private:
     bool stop_ = false;
 };
 
+// One worker thread running jobs in submission order: the host unpack of staged chunks, so the
+// engine thread packs chunk i (CopyPool) while chunk i - kHostSlots is unpacked (its own CopyPool)
+// — the two host memcpys overlap instead of alternating on the engine thread. wait(seq) blocks
+// until job `seq` (1-based, from submit) has run; a job's Error is rethrown by the next wait.
+class AsyncLane {
+public:
+    explicit AsyncLane(std::vector<int> cpus = {});
+    ~AsyncLane();
+    AsyncLane(const AsyncLane &) = delete;
+    AsyncLane &operator=(const AsyncLane &) = delete;
+    uint64_t submit(std::function<void()> job);
+    void wait(uint64_t seq);
+    void drain() noexcept;  // every job submitted so far has run (errors dropped)
+
+private:
+    void worker_();
+    std::vector<int> cpus_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<std::function<void()>> q_;
+    uint64_t submitted_ = 0, done_ = 0;
+    bool stop_ = false;
+    bool failed_ = false;
+    Error err_{0, ""};
+    std::thread thread_;
+};
+
 // Request identity: (type, key), ordered as the reference's (typeName, key) pairs —
 // "Allgather" < "Allreduce" < "Broadcast", then the key bytewise. On the wire it is the string
 // "<TypeName>::<key>".
@@ -215,9 +242,6 @@ private:
     // a round of at most this many bytes, with no earlier round in flight, completes on the
     // engine thread even when pipelined (its data plane is microseconds: the hand-off costs more)
     static constexpr size_t kInlineRoundBytes = 256u << 10;
-    // host staging: a pinned input segment of at least this many bytes is uploaded by DMA straight
-    // from the tensor (config "host_direct_dma"); smaller ones are packed by the copy threads
-    static constexpr size_t kDirectDmaMin = 256u << 10;
     size_t record_plan_(size_t &nplans);  // records the round's next plan event on stream_
     void complete_(Round &rd);            // waits the plan events, fires done(), frees the events
     void completer_();                    // the completion thread
@@ -274,13 +298,19 @@ private:
     size_t dims_bytes_ = 0;
     std::vector<hipEvent_t> round_events_;  // plan events of the round being enqueued (engine thread)
     static constexpr int kHostSlots = 4;
-    void *pin_[kHostSlots] = {};    // pinned host staging slots
+    void *pin_[kHostSlots] = {};    // pinned host staging slots (uploads)
+    void *pout_[kHostSlots] = {};   // pinned download slots: a chunk's D2H lands here, apart from the
+                                    // upload slot, so its host unpack overlaps the next packs
     void *dslot_[kHostSlots] = {};  // device slots
     size_t host_slot_bytes_ = 0;
     hipStream_t h2d_ = nullptr, d2h_ = nullptr;
     hipEvent_t hev_[3 * kHostSlots] = {};  // per slot: input landed, collective done, output landed
     bool slot_used_[kHostSlots] = {};        // hev_[3k + 2] marks the slot's last device use
     std::unique_ptr<CopyPool> pool_;
+    // the host unpack of staged chunks (its own copy threads, host_copy_threads of them); the lane
+    // is destroyed first (its jobs use out_pool_)
+    std::unique_ptr<CopyPool> out_pool_;
+    std::unique_ptr<AsyncLane> lane_;
     // opt-in registration cache (config "host_register_cache_bytes"): pageable host tensors of
     // keyed requests are hipHostRegister'ed once and kept (least recently used out past the cap),
     // so a training loop's CPU gradients take the pinned paths (direct DMA in, device unpack out)

@@ -276,7 +276,8 @@ int fold_variant(size_t chunk_bytes) {
 // skip" per input makes hipcc wait vmcnt(0) per input).
 constexpr int kFoldThreads = 128;
 template <int DT, int NB, int FV, int ORDER>
-__global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(SegTableN t) {
+__global__ void __launch_bounds__(kFoldThreads) k_sumN_tile(FoldBatch fb) {
+    const SegTableN &t = fb.t[blockIdx.y];  // (uniform: the problem's table stays in the kernarg segment)
     constexpr uint64_t kTileVec = kFoldThreads;
     using A = Acc<DT>;
     using S = typename Add<DT>::S;
@@ -395,7 +396,8 @@ __device__ __forceinline__ void run_tree(RunVec<DT> &out, const SegTableN &t, ui
 }
 
 template <int DT, int NB, int FV, int ORDER>
-__global__ void __launch_bounds__(kFoldThreads) k_sumN_run(SegTableN t) {
+__global__ void __launch_bounds__(kFoldThreads) k_sumN_run(FoldBatch fb) {
+    const SegTableN &t = fb.t[blockIdx.y];
     using A = Acc<DT>;
     using S = typename Add<DT>::S;
     using T = typename A::T;
@@ -465,45 +467,53 @@ template <int DT>
 constexpr bool kHalfType = DT == DDL_HALF || DT == DDL_BFLOAT16;
 
 template <int DT, int NB, int FV>
-void launch_sumN_order(const SegTableN &t, hipStream_t stream, unsigned tiles) {
+void launch_sumN_order(const FoldBatch &b, hipStream_t stream) {
     constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
-    if (fold_run_form((size_t)t.n * sizeof(typename Add<DT>::S), t.order, NB + 1)) {
-        const uint64_t runs = ((uint64_t)t.n / V + kRunVec) / kRunVec;  // +1 vector of room for the tail
+    const SegTableN &t = b.t[0];  // nb and order are the batch's; the form and grid follow its largest problem
+    uint64_t max_n = 0;
+    for (int i = 0; i < b.count; ++i) max_n = b.t[i].n > max_n ? b.t[i].n : max_n;
+    if (fold_run_form((size_t)max_n * sizeof(typename Add<DT>::S), t.order, NB + 1)) {
+        const dim3 grid((unsigned)((max_n / V + kRunVec) / kRunVec), (unsigned)b.count);  // +1 vector for the tail
         if constexpr (!kHalfType<DT>) {
             if (t.order == kFoldMpichTree) {
-                hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldMpichTree>), dim3((unsigned)runs), dim3(kFoldThreads), 0,
-                                   stream, t);
+                hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldMpichTree>), grid, dim3(kFoldThreads), 0, stream, b);
                 return;
             }
         }
-        hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldLeft>), dim3((unsigned)runs), dim3(kFoldThreads), 0, stream, t);
+        hipLaunchKernelGGL((k_sumN_run<DT, NB, FV, kFoldLeft>), grid, dim3(kFoldThreads), 0, stream, b);
         return;
     }
+    const uint64_t tiles = (max_n / V + kFoldThreads) / kFoldThreads;
+    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << max_n << " elements");
+    const dim3 grid((unsigned)tiles, (unsigned)b.count);
     if constexpr (!kHalfType<DT>) {
         if (t.order == kFoldMpichTree) {
-            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldMpichTree>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
+            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldMpichTree>), grid, dim3(kFoldThreads), 0, stream, b);
             return;
         }
         if (t.order == kFoldBinomial) {
-            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldBinomial>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
+            hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldBinomial>), grid, dim3(kFoldThreads), 0, stream, b);
             return;
         }
     }
-    hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldLeft>), dim3(tiles), dim3(kFoldThreads), 0, stream, t);
+    hipLaunchKernelGGL((k_sumN_tile<DT, NB, FV, kFoldLeft>), grid, dim3(kFoldThreads), 0, stream, b);
 }
 
 template <int DT, int NB>
-void launch_sumN_nb(const SegTableN &t, hipStream_t stream, unsigned tiles) {
+void launch_sumN_nb(const FoldBatch &b, hipStream_t stream) {
     if constexpr (NB > kMaxInputs) {
         fail(DDL_STATUS_INVALID_ARGUMENT, "too many reduce inputs");
     } else {
-        if (t.nb == NB) {
-            // cache policy (fold_variant): 5 = non-temporal loads + write-through store (large
-            // chunks), 4 = plain loads + write-through store (chunks up to 8 MiB, in cache)
-            if (fold_variant((size_t)t.n * sizeof(typename Add<DT>::S)) == 4) launch_sumN_order<DT, NB, 4>(t, stream, tiles);
-            else launch_sumN_order<DT, NB, 5>(t, stream, tiles);
+        if (b.t[0].nb == NB) {
+            // cache policy (fold_variant, by the batch's bytes per input): 5 = non-temporal loads +
+            // write-through store (large chunks), 4 = plain loads + write-through store (up to
+            // 8 MiB, in cache)
+            uint64_t elems = 0;
+            for (int i = 0; i < b.count; ++i) elems += b.t[i].n;
+            if (fold_variant((size_t)elems * sizeof(typename Add<DT>::S)) == 4) launch_sumN_order<DT, NB, 4>(b, stream);
+            else launch_sumN_order<DT, NB, 5>(b, stream);
         } else {
-            launch_sumN_nb<DT, NB + 1>(t, stream, tiles);
+            launch_sumN_nb<DT, NB + 1>(b, stream);
         }
     }
 }
@@ -625,42 +635,65 @@ int device_cu_count() {
 }
 
 namespace {
-template <int DT>
-void launch_sumN_dt(const SegTableN &t, hipStream_t stream) {
-    constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
+bool fold_aligned(const SegTableN &t) {
     bool aligned = aligned16(t.a) && aligned16(t.out);
     for (int k = 0; k < t.nb; ++k) aligned = aligned && aligned16(t.b[k]);
-    if (!aligned) {
-        uint64_t blocks = (t.n + kThreads * 4 - 1) / (kThreads * 4);
-        const uint64_t cap = (uint64_t)device_cu_count() * 8;
-        blocks = blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
-        launch_sumN_scalar_nb<DT, 1>(t, stream, (unsigned)blocks);
+    return aligned;
+}
+
+template <int DT>
+void launch_sumN_scalar_dt(const SegTableN &t, hipStream_t stream) {
+    uint64_t blocks = (t.n + kThreads * 4 - 1) / (kThreads * 4);
+    const uint64_t cap = (uint64_t)device_cu_count() * 8;
+    blocks = blocks > cap ? cap : (blocks < 1 ? 1 : blocks);
+    launch_sumN_scalar_nb<DT, 1>(t, stream, (unsigned)blocks);
+}
+
+template <int DT>
+void launch_sumN_dt(const FoldBatch &b, hipStream_t stream) {
+    bool aligned = true;
+    for (int i = 0; i < b.count; ++i) aligned = aligned && fold_aligned(b.t[i]);
+    if (!aligned) {  // misaligned buffers: element-granular, one problem at a time
+        for (int i = 0; i < b.count; ++i) launch_sumN_scalar_dt<DT>(b.t[i], stream);
         return;
     }
-    const uint64_t tiles = (t.n / V + kFoldThreads) / kFoldThreads;
-    DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << t.n << " elements");
-    launch_sumN_nb<DT, 1>(t, stream, (unsigned)tiles);
+    launch_sumN_nb<DT, 1>(b, stream);
+}
+
+void check_fold(const SegTableN &t) {
+    DDL_REQUIRE(t.nb >= 1 && t.nb <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "reduce inputs " << t.nb);
+    DDL_REQUIRE(t.order >= kFoldLeft && t.order <= kFoldBinomial, DDL_STATUS_INVALID_ARGUMENT, "fold order " << t.order);
+    DDL_REQUIRE(t.a && t.out, DDL_STATUS_INVALID_ARGUMENT, "null reduce buffer");
+    for (int k = 0; k < t.nb; ++k) DDL_REQUIRE(t.b[k], DDL_STATUS_INVALID_ARGUMENT, "null reduce input " << k);
 }
 }  // namespace
 
-void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) {
-    DDL_REQUIRE(t.nb >= 1 && t.nb <= kMaxInputs, DDL_STATUS_INVALID_ARGUMENT, "reduce inputs " << t.nb);
-    DDL_REQUIRE(t.order >= kFoldLeft && t.order <= kFoldBinomial, DDL_STATUS_INVALID_ARGUMENT, "fold order " << t.order);
-    if (t.n == 0) return;
-    DDL_REQUIRE(t.a && t.out, DDL_STATUS_INVALID_ARGUMENT, "null reduce buffer");
-    for (int k = 0; k < t.nb; ++k) DDL_REQUIRE(t.b[k], DDL_STATUS_INVALID_ARGUMENT, "null reduce input " << k);
+void launch_sumN_batch(const SegTableN *t, int count, int dtype, hipStream_t stream) {
+    DDL_REQUIRE(count >= 0 && count <= kMaxFoldBatch, DDL_STATUS_INVALID_ARGUMENT, "fold batch of " << count);
+    FoldBatch b;
+    b.count = 0;
+    for (int i = 0; i < count; ++i) {
+        if (t[i].n == 0) continue;
+        check_fold(t[i]);
+        DDL_REQUIRE(b.count == 0 || (t[i].nb == b.t[0].nb && t[i].order == b.t[0].order), DDL_STATUS_INVALID_ARGUMENT,
+                    "a fold batch needs one input count and one order");
+        b.t[b.count++] = t[i];
+    }
+    if (b.count == 0) return;
     switch (dtype) {
-        case DDL_FLOAT: launch_sumN_dt<DDL_FLOAT>(t, stream); break;
-        case DDL_DOUBLE: launch_sumN_dt<DDL_DOUBLE>(t, stream); break;
-        case DDL_INT32: launch_sumN_dt<DDL_INT32>(t, stream); break;
-        case DDL_INT64: launch_sumN_dt<DDL_INT64>(t, stream); break;
-        case DDL_UINT64: launch_sumN_dt<DDL_UINT64>(t, stream); break;
-        case DDL_HALF: launch_sumN_dt<DDL_HALF>(t, stream); break;
-        case DDL_BFLOAT16: launch_sumN_dt<DDL_BFLOAT16>(t, stream); break;
+        case DDL_FLOAT: launch_sumN_dt<DDL_FLOAT>(b, stream); break;
+        case DDL_DOUBLE: launch_sumN_dt<DDL_DOUBLE>(b, stream); break;
+        case DDL_INT32: launch_sumN_dt<DDL_INT32>(b, stream); break;
+        case DDL_INT64: launch_sumN_dt<DDL_INT64>(b, stream); break;
+        case DDL_UINT64: launch_sumN_dt<DDL_UINT64>(b, stream); break;
+        case DDL_HALF: launch_sumN_dt<DDL_HALF>(b, stream); break;
+        case DDL_BFLOAT16: launch_sumN_dt<DDL_BFLOAT16>(b, stream); break;
         default: fail(DDL_STATUS_UNSUPPORTED_DTYPE, "unsupported dtype");
     }
     DDL_HIP(hipGetLastError());
 }
+
+void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) { launch_sumN_batch(&t, 1, dtype, stream); }
 
 // Standalone reduce (acc += in over whole buckets) of `bytes` per operand, by bucket size
 // (3 rotating buffer sets per size, profiles/r02/reduce_policy/):

@@ -517,6 +517,76 @@ void build_program(RingProgram &prog, int rank, int P, const void *in, void *out
     }
 }
 
+RingConfig batch_bucket_config(RingConfig cfg, int P) {
+    cfg = effective_config(cfg, P);
+    // a merged tick posts one group and one allgather at most: every bucket runs a p2p schedule
+    // whose reduce is a fold (direct; one-shot where picked) — the ring's two-input steps and the
+    // collective allgathers of gather-fold / direct-gather are not merged
+    if (cfg.algo != kAlgoOneShot) {
+        cfg.algo = kAlgoDirect;
+        cfg.rings = 1;
+    }
+    return cfg;
+}
+
+namespace {
+size_t batch_block_elems(size_t n, size_t es, int P, const RingConfig &cfg) {
+    const size_t e = program_staging_elems(n, es, P, cfg);
+    const size_t g = kGranuleBytes / es;  // every bucket's block starts 256-byte aligned
+    return (e + g - 1) / g * g;
+}
+}  // namespace
+
+size_t batch_staging_elems(const size_t *ns, int count, size_t es, int P, const RingConfig &cfg_in) {
+    const RingConfig cfg = batch_bucket_config(cfg_in, P);
+    size_t total = 0;
+    for (int b = 0; b < count; ++b)
+        if (ns[b]) total += batch_block_elems(ns[b], es, P, cfg);
+    return total;
+}
+
+void build_batch_program(RingProgram &prog, int rank, int P, const void *const *ins, void *const *outs,
+                         const size_t *ns, int count, void *staging, int dtype, const RingConfig &cfg_in) {
+    const RingConfig cfg = batch_bucket_config(cfg_in, P);
+    const size_t es = dtype_size(dtype);
+    prog.P = P;
+    prog.rank = rank;
+    prog.esize = es;
+    prog.algo = cfg.algo;
+    prog.R = 1;
+    prog.K = 0;
+    prog.n = 0;
+    prog.staging_stride = 0;
+    prog.staging_slots = 0;
+    prog.ticks.clear();
+    if (P <= 1) return;
+    RingProgram part;
+    char *st = static_cast<char *>(staging);
+    for (int b = 0; b < count; ++b) {
+        if (ns[b] == 0) continue;
+        build_program(part, rank, P, ins[b], outs[b], st, ns[b], dtype, cfg);
+        st += batch_block_elems(ns[b], es, P, cfg) * es;
+        prog.n += ns[b];
+        prog.K = std::max(prog.K, part.K);
+        if (prog.ticks.size() < part.ticks.size()) prog.ticks.resize(part.ticks.size());
+        for (size_t t = 0; t < part.ticks.size(); ++t) {
+            Tick &dst = prog.ticks[t];
+            Tick &src = part.ticks[t];
+            DDL_REQUIRE(!src.gather.bytes && (!src.has_reduce || src.multi), DDL_STATUS_ERROR_UNKNOWN,
+                        "grouped allreduce: tick " << t << " of bucket " << b << " cannot be merged");
+            dst.reduce.count = 0;
+            dst.copies.insert(dst.copies.end(), src.copies.begin(), src.copies.end());
+            dst.ops.insert(dst.ops.end(), src.ops.begin(), src.ops.end());
+            if (src.has_reduce) {
+                dst.has_reduce = true;
+                dst.multi = true;
+                dst.folds.insert(dst.folds.end(), src.folds.begin(), src.folds.end());
+            }
+            dst.wait_reduce = std::max(dst.wait_reduce, src.wait_reduce);
+        }
+    }
+}
+
 void build_broadcast(RingProgram &prog, int rank, int P, int root, void *buf, size_t n, int dtype,
                      const RingConfig &cfg) {
     const size_t es = dtype_size(dtype);

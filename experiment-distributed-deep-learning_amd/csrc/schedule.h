@@ -164,6 +164,19 @@ inline size_t gather_stride(size_t n, size_t esize) { return (n * esize) % 16 ==
 void build_program(RingProgram &prog, int rank, int P, const void *in, void *out, void *staging,
                    size_t n, int dtype, const RingConfig &cfg);
 
+// Grouped allreduce of `count` buckets of one dtype (ins[b] -> outs[b], ns[b] elements) as ONE
+// program: every bucket's own program (batch_bucket_config: the direct schedule, or one-shot where
+// the config picks it), merged tick by tick — tick t posts every bucket's tick-t copies and p2p ops
+// as one group and folds every bucket's tick-t slices in as few launches as kMaxFoldBatch allows
+// (launch_tick_reduce); the merged tick waits for the latest reduce any bucket's tick waits for
+// (the compute stream is in order, so that covers the others). Per element the sums are exactly the
+// buckets' own (same fold, same order; `cfg.order_bytes` 0: each bucket's own message size). Bucket
+// b's staging is its own block of batch_staging_elems' layout.
+RingConfig batch_bucket_config(RingConfig cfg, int P);
+size_t batch_staging_elems(const size_t *ns, int count, size_t esize, int P, const RingConfig &cfg);
+void build_batch_program(RingProgram &prog, int rank, int P, const void *const *ins, void *const *outs,
+                         const size_t *ns, int count, void *staging, int dtype, const RingConfig &cfg);
+
 // Broadcast of `root`'s n elements into every rank's `buf` (MPICommunicator.cc:77-90 is
 // MPI_Bcast): scatter (root sends chunk c to rank c) + direct allgather of the chunks, K
 // slices pipelined so the allgather of slice k shares a tick with the scatter of slice k+1.

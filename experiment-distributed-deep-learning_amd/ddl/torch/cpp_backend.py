@@ -92,6 +92,10 @@ class CPPBackend:
         sig('py_error', None, ctypes.c_char_p)
         # data plane
         sig('ddl_allreduce', ci, cid, vp, vp, sz, ci, ci, vp)
+        sig('ddl_allreduce_batch', ci, cid, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), ci, ci, vp)
+        for name in ('ddl_local_allreduce_batch', 'ddl_testing_thread_allreduce_batch',
+                     'ddl_rccl_loopback_allreduce_batch'):
+            sig(name, ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), ci, vp)
         sig('ddl_allreduce_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
         sig('ddl_allreduce_submit_batch', ci, cid, ci, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(vp),
             ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(ci), ci, vp, DONE_FN, ctypes.POINTER(vp))
@@ -129,6 +133,8 @@ class CPPBackend:
         sig('ddl_reduce_sum2_variant', ci, ci, vp, vp, vp, sz, ci, vp)
         sig('ddl_reduce_fold', ci, vp, vp, ctypes.POINTER(vp), ci, sz, ci, vp)
         sig('ddl_reduce_fold_ordered', ci, vp, vp, ctypes.POINTER(vp), ci, sz, ci, ci, vp)
+        sig('ddl_reduce_fold_batch', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ci,
+            ctypes.POINTER(sz), ci, ci, vp)
         sig('ddl_pack', ci, vp, ctypes.POINTER(vp), ctypes.POINTER(sz), ci, vp)
         sig('ddl_unpack', ci, ctypes.POINTER(vp), vp, ctypes.POINTER(sz), ci, vp)
         sig('ddl_local_ring_allreduce', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ci, ci, vp)

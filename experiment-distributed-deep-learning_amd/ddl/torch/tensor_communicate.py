@@ -11,6 +11,7 @@ Device tensors stay in HBM; the call is ordered on torch's current stream and do
 synchronise the host. A host (CPU) tensor — the reference's deployment case — is staged
 through pinned memory to the GPU, reduced there and copied back.
 """
+import ctypes
 import itertools
 import threading
 
@@ -57,6 +58,28 @@ def allreduce_(tensor: torch.Tensor, communicator: Communicator = None) -> torch
     communicator = _comm(communicator)
     _allreduce_device(tensor, tensor, communicator)
     return tensor
+
+
+def allreduce_batch_(tensors, communicator: Communicator = None):
+    """In-place SUM of every device tensor in `tensors` (one dtype) over the ranks, as ONE grouped
+    collective (ddl_allreduce_batch): a DDP-style bucket list reduced with one RCCL group per tick
+    and the folds of up to 8 buckets per kernel launch. Each result is bit for bit what
+    `allreduce_` gives that tensor alone. Every rank passes the same shapes in the same order."""
+    communicator = _comm(communicator)
+    tensors = list(tensors)
+    if not tensors:
+        return tensors
+    dt = ddl_dtype(tensors[0])
+    for t in tensors:
+        require_device_tensor(t, 'allreduce_batch_ tensor')
+        if ddl_dtype(t) != dt or not t.is_contiguous():
+            raise ValueError('allreduce_batch_ needs contiguous tensors of one dtype')
+    k = len(tensors)
+    ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in tensors])
+    counts = (ctypes.c_size_t * k)(*[t.numel() for t in tensors])
+    check(CPPBackend.c_api().ddl_allreduce_batch(communicator.id, k, ptrs, ptrs, counts, dt, cb.OP_SUM,
+                                                  current_stream_handle(tensors[0].device)), 'ddl_allreduce_batch')
+    return tensors
 
 
 def allreduce_gradient(tensor: torch.Tensor, communicator: Communicator = None,

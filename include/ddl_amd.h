@@ -102,10 +102,11 @@ int ddl_init(int rank, int size, int device, const void *unique_id, size_t len);
 
 /* Same, for a single-process world (size 1); no RCCL involved. */
 int ddl_init_single(int device);
-/* Optional control channel for keyed requests at size > 1 (ring of TCP links, replaces the
- * MPI p2p token ring, MPIRingTokenCommunication.cc:29-102). ddl_control_listen opens a
- * listener and returns "ip:port"; ddl_control_connect takes every rank's endpoint,
- * separated by ';', in rank order. */
+/* Optional control channel for keyed requests at size > 1: TCP links in a star around rank 0
+ * (3 hops per negotiation round at any size), replacing the MPI p2p token ring
+ * (MPIRingTokenCommunication.cc:29-102) with the same token header. ddl_control_listen opens a
+ * listener and returns "ip:port"; ddl_control_connect takes every rank's endpoint, separated by
+ * ';', in rank order. */
 int ddl_control_listen(char *endpoint_out, size_t len);
 int ddl_control_connect(const char *endpoints);
 /* Negotiation rounds so far by token form: ids as strings, or as indices into the table of ids
@@ -117,10 +118,8 @@ int ddl_is_initialized(void);
 /* Tunables: "algo" (0 multi-ring, 1 direct all-to-all, 2 one-shot, 3 gather-fold: one
  * ncclAllGather then the rank-order fold, 4 direct-gather: the direct reduce-scatter then one
  * in-place ncclAllGather of the reduced chunks when they are equal), "slice_bytes", "rings", "max_slices",
- * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes", "host_taper" (0,
- * default: whole chunks; 2: quarter chunks for the first chunk's worth and the last two chunks'
- * worth of a long host-staged transfer, a shorter pipeline fill and drain but less in flight —
- * measured no faster; 1: the last two only), "tune",
+ * "fusion_threshold_bytes", "log_level", "cycle_time_us", "host_chunk_bytes" (host-staged
+ * transfers move in chunks of this size, default 32 MiB), "tune",
  * "host_copy_threads" (memcpy workers of the keyed host staging), "host_zero_copy" (1, default:
  * a keyed host allreduce plan whose outputs are all pinned and mapped on the device — torch
  * pin_memory, hipHostMalloc, hipHostRegister — is unpacked by the fusion kernel straight into
@@ -128,15 +127,14 @@ int ddl_is_initialized(void);
  * read-only "host_zero_copy_plans" counts the plans that took that path),
  * "host_numa_bind" (1, default: the handler's engine thread and copy threads bind to the CPUs of
  * the GPU's NUMA node, where pinned host memory lives; 0: placement left to the OS),
- * "host_direct_dma" (0, default; 1: pinned input segments of >= 256 KiB of a keyed host plan are
- * uploaded by DMA straight from the tensors instead of through the copy threads — slower on the C5
- * set), "host_register_cache_bytes" (0, default = off; > 0: pageable host tensors of keyed requests
+ * "host_register_cache_bytes" (0, default = off; > 0: pageable host tensors of keyed requests
  * are hipHostRegister'ed once and the registrations kept, least recently used out past this many
  * bytes, so repeated allreduce(cpu_tensor) calls take the pinned paths — the caller keeps those
  * tensors allocated while cached; setting it to 0 unregisters every cached range at once, after
  * ddl_wait_all), the read-only timeline of keyed host plans "host_pack_us" / "host_wait_us" /
  * "host_unpack_us" (microseconds the engine thread spent packing chunks, waiting for a pinned
- * slot's DMA / device work, unpacking staged results), "capture_mode" (0, default: inside a
+ * slot's DMA / device work, waiting for the unpack lane — staged results are unpacked by their own
+ * copy threads while the next chunks are packed), "capture_mode" (0, default: inside a
  * hipGraph capture the program is posted serially on the captured stream — one chain; 2: as a
  * single-stream DAG, every op on the captured stream with its dependencies set explicitly, which
  * keeps the recv / reduce / send overlap in the graph; 1: on the forked comm / compute streams —
@@ -160,7 +158,7 @@ int ddl_is_initialized(void);
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
  * The shared tunables (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, tune,
- * fusion_pipeline_bytes, reference_order, host_chunk_bytes, host_taper) must be equal on every rank of a
+ * fusion_pipeline_bytes, reference_order, host_chunk_bytes) must be equal on every rank of a
  * communicator: the ranks agree on a hash of them at a communicator's first collective and
  * whenever this rank's values changed since (change them on every rank between the same two
  * collectives), and every keyed round carries the hash; on a mismatch the collective or round
@@ -184,10 +182,24 @@ void py_debug(const char *log_str);
 void py_error(const char *log_str);
 
 /* ---- data plane ---------------------------------------------------------------------- */
-/* recv = SUM over ranks of send (elementwise). Ring reduce-scatter + allgather over RCCL
- * send/recv with the HIP reduce kernel; recv may equal send (in place). Stream-ordered. */
+/* recv = SUM over ranks of send (elementwise), bit for bit the reference's MPI_Allreduce (MPICH
+ * 3.3.2's order) with reference_order 1. The schedule is the tuned one for the bucket's size
+ * class: by default at P > 2 the direct reduce-scatter (slices of every chunk to every peer over
+ * RCCL send/recv, one HIP fold per slice in MPICH's tree) + allgather; one-shot / gather-fold for
+ * small buckets; at P = 2 the ring. recv may equal send (in place). Stream-ordered: no host
+ * synchronisation (except the first bucket of a size class, which the autotuner times). */
 int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t elements,
                   int dtype, int op, void *hip_stream);
+
+/* Grouped form of ddl_allreduce for `count` buckets of one dtype (MI355X extension: a DDP-style
+ * bucket list in one call): recvs[b] = SUM over ranks of sends[b] (elements[b] each; in place when
+ * recvs[b] == sends[b]), bit for bit what ddl_allreduce gives each bucket on its own. One program
+ * for all buckets — tick by tick one RCCL group carries every bucket's slices and the folds of up
+ * to 8 buckets share a kernel launch — instead of a program, two or more groups and a fold launch
+ * per bucket. The schedule is the one tuned for the largest bucket (direct, or one-shot for small
+ * buckets). Stream-ordered; collective: every rank passes the same count and element counts. */
+int ddl_allreduce_batch(ddl_communicator_id id, int count, const void *const *sends, void *const *recvs,
+                        const size_t *elements, int dtype, int op, void *hip_stream);
 
 /* Communicator::broadcast (reference Communicator.h:81-92, MPI_Bcast at MPICommunicator.cc:77-90):
  * root's `elements` of `buf` into every rank's `buf`. Scatter + direct allgather over RCCL
@@ -216,22 +228,20 @@ int ddl_allreduce_host(ddl_communicator_id id, const void *send, void *recv, siz
  * ms[i] = mean time per allreduce (max over ranks). configs/ms may be NULL. */
 int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, int *count,
                     long long *configs, float *ms, int max_candidates);
-/* Order between the two (the reference's MPI_THREAD_MULTIPLE, MPIBackend.cc:77-86): a
- * communicator with a token ring reduces its keyed rounds on a private RCCL communicator, and
- * every round is placed after the same number of the communicator's direct collectives
- * (ddl_allreduce, ddl_broadcast, ddl_allgather[v], ddl_allreduce_host, split_communicator) on
- * every rank, so both RCCL communicators see their work in one order everywhere. A direct
- * collective issued while a round is being placed waits for the placement (one negotiation). */
 /* Keyed asynchronous request (TF op Allreduce semantics): registered under `key`,
  * negotiated across ranks, fused by dtype in lexicographic key order, then `done` fires.
  * `in`/`out` must stay valid until `done`. Work is ordered after `hip_stream`'s current
- * position; `done` fires once `out` is final. */
+ * position; `done` fires once `out` is final.
+ * Keyed rounds and direct collectives on one communicator (the reference's MPI_THREAD_MULTIPLE,
+ * MPIBackend.cc:77-86): a communicator with a token ring reduces its keyed rounds on a private
+ * RCCL communicator, and every round is placed after the same number of the communicator's
+ * direct collectives (ddl_allreduce[_batch], ddl_broadcast, ddl_allgather[v], ddl_allreduce_host,
+ * split_communicator) on every rank, so both RCCL communicators see their work in one order
+ * everywhere. A direct collective issued while a round is being placed waits for the placement
+ * (one negotiation). */
 int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
                          size_t elements, int dtype, int op, void *hip_stream,
                          ddl_done_fn done, void *user);
-/* Batch form: registers `count` keyed requests at once (one input-ready event on hip_stream,
- * one wake-up of the engine thread); users[i] (or NULL) is passed to done for request i.
- * All-or-nothing: a duplicate key rejects the whole batch. */
 /* Keyed broadcast (TF op Broadcast, op/tensorflow/BroadcastOp.cc; TensorBroadcastRequest.h:13-40):
  * `out` on every rank receives root's `in`. Negotiated and fused like allreduce requests
  * (dtype groups, plans, MPIRingTokenCommunication.cc:367-419); requests of different roots
@@ -246,6 +256,9 @@ int ddl_broadcast_submit(ddl_communicator_id id, const char *key, const void *in
 int ddl_allgather_submit(ddl_communicator_id id, const char *key, const void *in, size_t first_dim,
                          size_t row_elements, int dtype, void *hip_stream, ddl_alloc_fn alloc,
                          ddl_done_fn done, void *user);
+/* Batch form of ddl_allreduce_submit: registers `count` keyed requests at once (one input-ready
+ * event on hip_stream, one wake-up of the engine thread); users[i] (or NULL) is passed to done for
+ * request i. All-or-nothing: a duplicate key rejects the whole batch. */
 int ddl_allreduce_submit_batch(ddl_communicator_id id, int count, const char *const *keys,
                                const void *const *ins, void *const *outs, const size_t *elements,
                                const int *dtypes, int op, void *hip_stream, ddl_done_fn done,

@@ -105,6 +105,12 @@ int ddl_reduce_fold(void *out, const void *a, const void *const *ins, int nb, si
 int ddl_reduce_fold_ordered(void *out, const void *a, const void *const *ins, int nb, size_t elements, int dtype,
                             int order, void *hip_stream);
 
+/* Up to 8 such folds in ONE launch (the grouped allreduce's batched fold; blockIdx.y = problem):
+ * problem p computes outs[p] = as[p] + ins[p * nb + 0] + ... + ins[p * nb + nb - 1] over elements[p]
+ * in `order`. No problem may read another's output. */
+int ddl_reduce_fold_batch(int count, void *const *outs, const void *const *as, const void *const *ins, int nb,
+                          const size_t *elements, int dtype, int order, void *hip_stream);
+
 /* Fusion pack/unpack (device): gathers `count` segments into one contiguous buffer and
  * scatters it back (executeCommunicatePlan_'s memcpy in/out, MPIRingTokenCommunication.cc:548-733). */
 int ddl_pack(void *dst, const void *const *srcs, const size_t *bytes, int count, void *hip_stream);
@@ -117,6 +123,15 @@ int ddl_unpack(void *const *dsts, const void *src, const size_t *bytes, int coun
  * sends[r]/recvs[r] are rank r's buffers. Stream-ordered on hip_stream. */
 int ddl_local_ring_allreduce(int nranks, const void *const *sends, void *const *recvs,
                              size_t elements, int dtype, int op, void *hip_stream);
+
+/* ddl_allreduce_batch over P virtual ranks: sends[r * count + b] / recvs[r * count + b] are rank r's
+ * bucket b of elements[b]. _local: device copies for the moves (LocalWorld); _thread: the
+ * production executor per rank over the asynchronous thread fabric; _rccl_loopback: every matched
+ * pair through RCCL (declared with the loopback below). */
+int ddl_local_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                              const size_t *elements, int dtype, void *hip_stream);
+int ddl_testing_thread_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                                       const size_t *elements, int dtype, void *hip_stream);
 
 /* Broadcast / allgatherv of P virtual ranks on one GPU (as ddl_local_ring_allreduce). */
 int ddl_local_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype, void *hip_stream);
@@ -159,8 +174,9 @@ int ddl_testing_dep_check(long long *counts, char *report, size_t len);
  * (config "compute_cu_mask"; 0 = unmasked), read back with hipExtStreamGetCUMask. */
 int ddl_testing_compute_stream_cus(int every, int *enabled, int *total);
 /* The chunk boundaries of a host-staged transfer (ddl_allreduce_host, the keyed handler's host
- * plans) under the current "host_taper": writes min(count, cap) boundaries cut[0] = 0 < ... < cut[count - 1] = total_bytes into
- * cuts and sets *count. Pure host arithmetic (no device). */
+ * plans): whole chunks of chunk_bytes, the last one short. Writes min(count, cap) boundaries
+ * cut[0] = 0 < ... < cut[count - 1] = total_bytes into cuts and sets *count. Pure host arithmetic
+ * (no device). */
 int ddl_testing_host_chunk_cuts(size_t total_bytes, size_t chunk_bytes, size_t *cuts, size_t cap, size_t *count);
 
 /* ---- RCCL loopback: the production RCCL transport on one GPU (TEST / DIAGNOSTIC) ---------
@@ -176,6 +192,8 @@ int ddl_rccl_loopback_init(int device);
 int ddl_rccl_loopback_split(int color, int key, int *rank, int *size);
 int ddl_rccl_loopback_allreduce(int nranks, const void *const *sends, void *const *recvs, size_t elements,
                                 int dtype, void *hip_stream);
+int ddl_rccl_loopback_allreduce_batch(int nranks, int count, const void *const *sends, void *const *recvs,
+                                      const size_t *elements, int dtype, void *hip_stream);
 int ddl_rccl_loopback_broadcast(int nranks, int root, void *const *bufs, size_t elements, int dtype,
                                 void *hip_stream);
 int ddl_rccl_loopback_allgatherv(int nranks, const void *const *sends, void *const *recvs, const size_t *counts,

@@ -76,6 +76,30 @@ def check_schedules_vs_oracle(ctx):
                             assert got.tobytes() == want.tobytes(), (algo, ref, dt, n, in_place)
 
 
+def check_allreduce_batch(ctx):
+    """The grouped allreduce on the real engine (Communicator::allreduce_batch through the
+    allreduce_batch_ Python API): mixed bucket sizes (empty, ragged, both sides of 2048 B) of fp32
+    and fp16, the direct and one-shot schedules and the tuner's pick — every bucket on every rank
+    equals MPICH's order for its own message, bit for bit."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allreduce_batch_
+    ns = [300, 0, 4099, 65_537, 1, 300_001]
+    for dt in (h.DT_FLOAT, h.DT_HALF):
+        for settings in ({'tune': 0, 'algo': 1, 'slice_bytes': 64 << 10}, {'tune': 0, 'algo': 2}, {}):
+            xs = [[h.random_input(dt, n, 1000 * q + 17 * b + dt) for b, n in enumerate(ns)] for q in range(P)]
+            ts = [_dev(torch, x.view(np.uint16) if x.dtype == np.float16 else x, 'cuda') for x in xs[r]]
+            ts = [t.view(torch.float16) if dt == h.DT_HALF else t for t in ts]
+            with h.config(lib, **settings):
+                allreduce_batch_(ts, comm)
+            torch.cuda.synchronize()
+            for b, n in enumerate(ns):
+                if n:
+                    want = ora.fold_ref_order(dt, [xs[q][b] for q in range(P)])
+                    got = ts[b].view(torch.int16).cpu().numpy().view(np.float16) if dt == h.DT_HALF else ts[b].cpu().numpy()
+                    assert got.tobytes() == want.tobytes(), (dt, settings, b, n)
+
+
 def check_tuned_exact(ctx):
     """Autotuner on (collective timing, max over ranks through the transport): every rank picks
     the same schedule per size class, and exactly summable buckets come out exact."""
@@ -212,8 +236,8 @@ def check_keyed_host_requests(ctx):
     xs = [[h.random_input(dts[i], n, 900 + 31 * i + q) for q in range(P)] for i, n in enumerate(sizes)]
     gb = {d: sum(xs[i][0].nbytes for i in range(len(sizes)) if dts[i] == d) for d in set(dts)}
     dev_x = [h.random_input(h.DT_FLOAT, 4099, 4000 + q) for q in range(P)]
-    for taper in (0, 2):  # whole chunks (default) and quarter chunks at both ends
-        with h.config(lib, host_chunk_bytes=64 << 10, reference_order=1, host_taper=taper):
+    for chunk in (64 << 10,):  # many chunks: the 4 upload / download slots wrap
+        with h.config(lib, host_chunk_bytes=chunk, reference_order=1):
             for rnd in range(4):
                 pin = rnd == 3 or (rnd == 2 and r % 2 == 0)
                 ts = [torch.from_numpy(xs[i][r].copy()) for i in range(len(sizes))]
@@ -231,10 +255,10 @@ def check_keyed_host_requests(ctx):
                     got = hd.wait(timeout=120)
                     assert not got.is_cuda
                     want = ora.fold_ref_order(dts[i], xs[i], gb[dts[i]])
-                    assert got.numpy().tobytes() == want.tobytes(), (taper, rnd, i)
+                    assert got.numpy().tobytes() == want.tobytes(), (rnd, i)
                 assert hs[-1].wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, dev_x).tobytes()
                 # three host dtype groups, one plan each
-                assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == (3 if pin else 0), (taper, rnd)
+                assert lib.ddl_get_config(b'host_zero_copy_plans') - plans0 == (3 if pin else 0), rnd
         hs, want = [], []
         for i in range(9):
             root, dt = i % P, [torch.float32, torch.int64, torch.float64][i % 3]
@@ -353,18 +377,16 @@ def check_keyed_broadcast_allgather(ctx):
 
 
 def check_host_resident(ctx):
-    """allreduce of a CPU tensor: the chunked H2D -> ring -> D2H pipeline (4 slots), many chunks,
-    whole or tapered ("host_taper" 2: quarter chunks at both ends, cut alike on every rank)."""
+    """allreduce of a CPU tensor: the chunked H2D -> ring -> D2H pipeline (4 slots), many chunks."""
     import _helpers as h
     torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
     from ddl.torch.tensor_communicate import allreduce
     n = 1_000_003
     base = torch.randint(-1000, 1000, (n,), generator=torch.Generator().manual_seed(9))
-    for taper in (0, 2):  # whole chunks (default) and quarter chunks at both ends
-        with h.config(lib, host_chunk_bytes=256 << 10, host_taper=taper):
-            got = allreduce((base + r).to(torch.float32), comm)
-        assert not got.is_cuda
-        assert torch.equal(got, (base * P + P * (P - 1) // 2).to(torch.float32)), taper
+    with h.config(lib, host_chunk_bytes=256 << 10):
+        got = allreduce((base + r).to(torch.float32), comm)
+    assert not got.is_cuda
+    assert torch.equal(got, (base * P + P * (P - 1) // 2).to(torch.float32))
 
 
 def check_dp_training(ctx):
@@ -501,7 +523,8 @@ def check_keyed_round_order(ctx):
     assert mine[1] and mine[1] == sorted(mine[1]), mine
 
 
-CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_tuned_exact, check_keyed_fusion,
+CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,
+          check_keyed_fusion,
           check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
           check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model,
           check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]

@@ -22,7 +22,7 @@ DEPLOYMENT = {
     'ddl_version', 'ddl_build_info', 'ddl_last_error', 'ddl_dtype_name', 'ddl_dtype_size',
     'ddl_get_unique_id', 'ddl_init', 'ddl_init_single', 'ddl_control_listen', 'ddl_control_connect',
     'ddl_control_stats', 'ddl_finalize', 'ddl_is_initialized', 'ddl_set_config', 'ddl_get_config',
-    'ddl_comm_transport', 'ddl_allreduce', 'ddl_broadcast', 'ddl_allgatherv', 'ddl_allgather',
+    'ddl_comm_transport', 'ddl_allreduce', 'ddl_allreduce_batch', 'ddl_broadcast', 'ddl_allgatherv', 'ddl_allgather',
     'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit',
     'ddl_allgather_submit', 'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem',
     'ddl_allreduce_submit_batch_mem', 'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all',
@@ -122,9 +122,9 @@ def test_config_roundtrip(lib):
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
     assert lib.ddl_set_config(b'fold_form', 3) == 3
-    # host-staged transfers cut whole chunks by default (1: quarter chunks at the tail, 2: both ends)
-    assert lib.ddl_get_config(b'host_taper') == 0
-    assert lib.ddl_set_config(b'host_taper', 3) == 3
+    # the measured losers of r03 are gone: quarter-chunk tapers, direct DMA
+    for gone in (b'host_taper', b'host_direct_dma'):
+        assert lib.ddl_set_config(gone, 0) == 3 and lib.ddl_get_config(gone) == -1
 
 
 def test_product_does_not_reference_oracle():
@@ -171,25 +171,13 @@ def _host_cuts(lib, total, chunk):
     return list(buf)
 
 
-@pytest.mark.parametrize('taper', [2, 1, 0])
 @pytest.mark.parametrize('chunk', [4096, 1 << 20, 32 << 20, 768])
-def test_host_chunk_cuts(lib, chunk, taper):
-    """Host-staged transfers (ddl_allreduce_host, keyed host plans) cut whole chunks, with quarter
-    chunks ("host_taper" 2) for the first chunk's worth of a transfer longer than three
-    chunks and the last two chunks' worth of one longer than two (1: the tail only). Every boundary
-    but the end is a multiple of 256 (the dtype size divides 256), so every element lies in one
-    chunk and ranks cut alike."""
-    assert lib.ddl_set_config(b'host_taper', taper) == 0
-    try:
-        _check_cuts(lib, chunk, taper)
-    finally:
-        assert lib.ddl_set_config(b'host_taper', 0) == 0
-
-
-def _check_cuts(lib, chunk, taper):
+def test_host_chunk_cuts(lib, chunk):
+    """Host-staged transfers (ddl_allreduce_host, keyed host plans) cut whole chunks, the last one
+    short. Every boundary but the end is a multiple of 256 (the dtype size divides 256), so every
+    element lies in one chunk and ranks cut alike."""
     lib.ddl_testing_host_chunk_cuts.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                                 ctypes.c_void_p]
-    piece = max(256, (chunk // 4) & ~255)
     for total in [1, 256, chunk - 8, chunk, chunk + 256, 2 * chunk, 2 * chunk + 256, 3 * chunk, 3 * chunk + 1024,
                   8 * chunk, 8 * chunk + 4, 73 * chunk + 12345]:
         cuts = _host_cuts(lib, total, chunk)
@@ -198,11 +186,7 @@ def _check_cuts(lib, chunk, taper):
         assert all(s > 0 for s in sizes)
         assert all(c % 256 == 0 for c in cuts[:-1])
         for a, s in zip(cuts, sizes):
-            left = total - a
-            tail = taper >= 1 and total > 2 * chunk and left <= 2 * chunk
-            head = taper >= 2 and total > 3 * chunk and a < chunk
-            assert s == min(piece if (head or tail) else chunk, left), (total, a, s)
-    head = _host_cuts(lib, 256 << 20, 32 << 20)[:3]
-    assert head == ([0, 8 << 20, 16 << 20] if taper == 2 else [0, 32 << 20, 64 << 20])
+            assert s == min(chunk, total - a), (total, a, s)
+    assert _host_cuts(lib, 256 << 20, 32 << 20) == [k * (32 << 20) for k in range(9)]
     assert lib.ddl_testing_host_chunk_cuts(ctypes.c_size_t(1024), ctypes.c_size_t(100), None, ctypes.c_size_t(0),
                                            ctypes.byref(ctypes.c_size_t())) != 0

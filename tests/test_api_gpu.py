@@ -36,18 +36,15 @@ def test_allreduce_host_tensor(world):
     assert not y.is_cuda and torch.equal(x, y)
 
 
-@pytest.mark.parametrize('taper', [0, 2])
 @pytest.mark.parametrize('chunk', [4096, 1 << 20, 32 << 20])
 @pytest.mark.parametrize('n,dtype', [(1, torch.float32), (1000, torch.float16), (3_000_001, torch.float32),
                                      (777_777, torch.int64)])
-def test_allreduce_host_pipeline(world, lib, chunk, n, dtype, taper):
-    """Chunked H2D -> ring -> D2H pipeline (pageable input registered for the call), in whole
-    chunks or with quarter chunks at both ends ("host_taper" 2)."""
+def test_allreduce_host_pipeline(world, lib, chunk, n, dtype):
+    """Chunked H2D -> ring -> D2H pipeline (pageable input registered for the call), whole chunks."""
     from ddl.torch.cpp_backend import check
     from ddl.torch.util import ddl_dtype
     old = lib.ddl_get_config(b'host_chunk_bytes')
     assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
-    assert lib.ddl_set_config(b'host_taper', taper) == 0
     try:
         x = (torch.randn(n) * 1000).to(dtype)
         y = torch.zeros_like(x)
@@ -58,7 +55,6 @@ def test_allreduce_host_pipeline(world, lib, chunk, n, dtype, taper):
         assert torch.equal(x, z)
     finally:
         lib.ddl_set_config(b'host_chunk_bytes', old)
-        lib.ddl_set_config(b'host_taper', 0)
 
 
 def test_allreduce_gradient_mean(world):
@@ -354,7 +350,7 @@ def test_keyed_fusion_pipeline_large_segment(world, lib, data_plane_at_one_rank)
 
 
 @pytest.mark.parametrize('memory', ['pageable', 'pinned', 'pinned_outputs', 'mixed', 'pinned_misaligned',
-                                    'pinned_direct', 'registered'])
+                                    'registered'])
 @pytest.mark.parametrize('chunk', [4096, 64 << 10, 32 << 20])
 def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     """Keyed requests on host tensors with the one-rank shortcut off: every plan goes through the
@@ -363,25 +359,22 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     bit (one rank). Pageable outputs are staged back (D2H -> host unpack); when every output of a
     plan is pinned the unpack kernel writes them over PCIe — the plan counter says which path
     ran. A pinned output viewed at a 2-byte offset, or one pageable output in the dtype group,
-    sends its plan back to staging. 'pinned_direct': pinned inputs of >= 256 KiB uploaded by DMA
-    straight from the tensors (host_direct_dma 1); 'registered': pageable tensors with the opt-in
+    sends its plan back to staging. 'registered': pageable tensors with the opt-in
     registration cache take the pinned paths (the unpack kernel writes the registered outputs
     through their device mapping); switching the cache off unregisters them again."""
     from ddl.torch.tensor_communicate import allreduce_async_batch, broadcast_async
-    keys = (b'one_rank_shortcut', b'host_chunk_bytes', b'host_direct_dma', b'host_register_cache_bytes')
+    keys = (b'one_rank_shortcut', b'host_chunk_bytes', b'host_register_cache_bytes')
     old = {k: lib.ddl_get_config(k) for k in keys}
     try:
         assert lib.ddl_set_config(b'one_rank_shortcut', 0) == 0
         assert lib.ddl_set_config(b'host_chunk_bytes', chunk) == 0
-        if memory == 'pinned_direct':
-            assert lib.ddl_set_config(b'host_direct_dma', 1) == 0
         if memory == 'registered':
             assert lib.ddl_set_config(b'host_register_cache_bytes', 1 << 30) == 0
         g = torch.Generator().manual_seed(chunk)
         dts = [torch.float32, torch.float64, torch.int32, torch.float16, torch.bfloat16, torch.int64]
         xs = [(torch.randn(n, generator=g) * 100).to(dts[i % 6]) for i, n in enumerate([1, 7, 1000, 65_537, 300_001,
                                                                                        5, 2_000_003, 4096])]
-        if memory in ('pinned', 'mixed', 'pinned_misaligned', 'pinned_direct'):
+        if memory in ('pinned', 'mixed', 'pinned_misaligned'):
             xs = [x.pin_memory() for x in xs]
         if memory == 'pinned_misaligned':  # fp16 tensor 3 (in place) seen from its second element: 2-byte offset
             xs[3] = xs[3][1:]
@@ -406,7 +399,7 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
         # misaligned fp16 group
         device_unpacked = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
         assert device_unpacked == {'pageable': 0, 'pinned': 6, 'pinned_outputs': 6, 'mixed': 5,
-                                   'pinned_misaligned': 5, 'pinned_direct': 6, 'registered': 6}[memory]
+                                   'pinned_misaligned': 5, 'registered': 6}[memory]
         # the engine thread's timeline statistics moved: chunks were packed, and unpacked on the
         # host when every plan was staged back (microseconds: a tiny staged plan may read 0)
         pack, wait, unpack = [lib.ddl_get_config(k) - v for k, v in zip(tl_keys, tl0)]
@@ -417,17 +410,6 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
     finally:
         for k, v in old.items():
             lib.ddl_set_config(k, v)
-
-
-@pytest.mark.parametrize('memory', ['pageable', 'pinned', 'mixed', 'registered'])
-def test_keyed_host_requests_tapered(world, lib, memory):
-    """The keyed host plans with quarter chunks at both ends ("host_taper" 2; 4 KiB chunks, so
-    1 KiB quarters at both ends of every group's plan): same outputs, same paths."""
-    assert lib.ddl_set_config(b'host_taper', 2) == 0
-    try:
-        test_keyed_host_requests_data_plane(world, lib, 4096, memory)
-    finally:
-        lib.ddl_set_config(b'host_taper', 0)
 
 
 def _cpulist(text):
