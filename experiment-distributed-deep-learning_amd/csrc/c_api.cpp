@@ -391,6 +391,7 @@ long long ddl_get_config(const char *key) {
     if (k == "host_numa_bind") return c.host_numa_bind;
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
     if (k == "host_register_failures") return c.host_register_failures;  // statistic, not settable
+    if (k == "host_register_hits") return c.host_register_hits;          // statistic, not settable
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "host_pack_us") return c.host_pack_ns / 1000;      // statistic, not settable
     if (k == "host_wait_us") return c.host_wait_ns / 1000;      // statistic, not settable
@@ -915,6 +916,10 @@ int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const 
                                                               (size_t)config().fusion_pipeline_bytes.load());
         if (subplans) *subplans = j;
     });
+}
+
+int ddl_testing_control_fault(int on) {
+    return guarded([&] { set_testing_control_fault(on); });
 }
 
 int ddl_testing_drop_wait(int tick) {

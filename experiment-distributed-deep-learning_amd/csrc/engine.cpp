@@ -113,7 +113,11 @@ public:
     explicit UserCollective(Communicator &c) : c_(c) {
         if (c_.size_ <= 1 || !c_.keyed_data_) return;
         std::unique_lock<std::mutex> lk(c_.gate_mu_);
-        c_.gate_cv_.wait(lk, [&] { return !c_.frozen_ || c_.user_seq_ < c_.release_; });
+        c_.gate_cv_.wait(lk, [&] { return c_.aborted_ || !c_.frozen_ || c_.user_seq_ < c_.release_; });
+        DDL_REQUIRE(!c_.aborted_, c_.aborted_,
+                    "the communicator's keyed request handler stopped (" << c_.abort_msg_
+                                                                         << "): user collectives can no longer be "
+                                                                            "ordered against keyed rounds");
         ++c_.user_seq_;
         active_ = true;
     }
@@ -152,7 +156,8 @@ void Communicator::round_release(long long at) {
 
 void Communicator::round_enter(long long at) {
     std::unique_lock<std::mutex> g(gate_mu_);
-    gate_cv_.wait(g, [&] { return user_done_ >= at; });
+    gate_cv_.wait(g, [&] { return aborted_ || user_done_ >= at; });
+    DDL_REQUIRE(!aborted_, aborted_, "keyed round not entered: " << abort_msg_);
     DDL_REQUIRE(user_seq_ == at && user_done_ == at, DDL_STATUS_COMM_ERROR,
                 "keyed round placed after user collective " << at << " but " << user_seq_ << " have started");
 }
@@ -160,6 +165,18 @@ void Communicator::round_enter(long long at) {
 void Communicator::round_unfreeze() {
     {
         std::lock_guard<std::mutex> g(gate_mu_);
+        frozen_ = false;
+    }
+    gate_cv_.notify_all();
+}
+
+void Communicator::round_abort(int status, const std::string &why) {
+    {
+        std::lock_guard<std::mutex> g(gate_mu_);
+        if (!aborted_) {
+            aborted_ = status ? status : DDL_STATUS_COMM_ERROR;
+            abort_msg_ = why;
+        }
         frozen_ = false;
     }
     gate_cv_.notify_all();

@@ -58,6 +58,7 @@ struct Config {
     // read-only statistics of that cache (ddl_get_config): bytes registered now, failed registrations
     std::atomic<long long> host_registered_bytes{0};
     std::atomic<long long> host_register_failures{0};
+    std::atomic<long long> host_register_hits{0};  // tensors found inside a cached registration
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
     // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};
@@ -223,6 +224,11 @@ public:
     void round_release(long long at);    // handler: the round goes after user collective `at`
     void round_enter(long long at);      // handler: waits until `at` user collectives are enqueued
     void round_unfreeze();               // handler: the round is enqueued (or failed)
+    // handler: it stopped on an error (a control link lost mid-round, a token-protocol fault) or is
+    // shutting down. Clears the freeze, wakes every gate wait, and from then on every user
+    // collective on this communicator fails with `status` instead of blocking behind a round that
+    // can no longer be placed (the keyed / user collective order is no longer known).
+    void round_abort(int status, const std::string &why);
     long long user_collectives() const;  // issued so far (tests)
     // The round release points this rank used, most recent last (bounded log; tests compare
     // them across ranks).
@@ -232,8 +238,11 @@ public:
     // and whenever this rank's shared tunables changed since the last agreement, every rank's
     // Config::shared_hash() is allgathered over the data plane; a mismatch fails the collective on
     // every rank with DDL_STATUS_CONFIG_MISMATCH before any program is built (different slice
-    // sizes would otherwise build different programs and hang RCCL). Keyed rounds carry the hash
-    // in their tokens instead (every round).
+    // sizes would otherwise build different programs and hang RCCL). The exchange is collective:
+    // it is matched only when every rank changes its values between the same two collectives; a
+    // one-sided change after the first collective posts an unmatched exchange (unsupported, see
+    // ddl_set_config in ddl_amd.h). Keyed rounds carry the hash in their tokens instead (every
+    // round, so they see one-sided changes too).
     void agree_config(hipStream_t stream);
 
 private:
@@ -243,6 +252,8 @@ private:
     long long user_seq_ = 0;    // user collectives entered
     long long user_done_ = 0;   // user collectives enqueued (or failed)
     bool frozen_ = false;       // a keyed round is being placed
+    int aborted_ = 0;           // round_abort's status (0: the handler is healthy)
+    std::string abort_msg_;
     long long release_ = 0;     // while frozen: user collectives may run while user_seq_ < release_
     std::vector<long long> round_log_;
     uint64_t agreed_hash_ = 0;  // last shared-config hash all ranks agreed on (0: none yet)

@@ -364,6 +364,9 @@ RequestHandler::~RequestHandler() {
         stop_ = true;
     }
     cv_.notify_all();
+    // a round waiting in round_enter for user collectives that will never be issued now fails
+    // (the communicator is going away) instead of blocking the join below
+    owner_->round_abort(DDL_STATUS_NOT_INITIALIZED, "the communicator is being destroyed");
     if (thread_.joinable()) thread_.join();
     {  // the rounds already handed over complete (or fail) first, in order
         std::lock_guard<std::mutex> g(done_mu_);
@@ -476,6 +479,9 @@ void RequestHandler::wait_all() {
     idle_cv_.wait(lk, [this] { return (pending_.empty() && inflight_ == 0) || stop_; });
 }
 
+std::atomic<int> g_control_fault{0};
+void set_testing_control_fault(int on) { g_control_fault = on ? 1 : 0; }
+
 void RequestHandler::fail_all_(int status) {
     std::map<ReqId, Request> left;
     {
@@ -556,7 +562,18 @@ void RequestHandler::main_() {
         }
     } catch (const Error &e) {
         DDL_LOG(0, "request handler stopped: " << e.msg);
+        // a freeze taken by this round's snapshot is cleared here, and the user collectives waiting
+        // behind it (or issued later) fail instead of blocking: with the round's place unknown their
+        // order against the keyed data plane is no longer defined
+        owner_->round_abort(e.status, e.msg);
+        // the other ends see the link close (EOF) and stop as well, instead of waiting for a token
+        if (ch_) ch_->close_all();
         fail_all_(e.status);
+    } catch (const std::exception &e) {
+        DDL_LOG(0, "request handler stopped: " << e.what());
+        owner_->round_abort(DDL_STATUS_COMM_ERROR, e.what());
+        if (ch_) ch_->close_all();
+        fail_all_(DDL_STATUS_COMM_ERROR);
     }
     {
         std::lock_guard<std::mutex> g(mu_);
@@ -795,7 +812,13 @@ void RequestHandler::member_round_(Token &t) {
                 if (held(i)) mine.push_back(i);
             return mine;
         },
-        [this] { return owner_->round_freeze(); });
+        [this] {
+            const long long at = owner_->round_freeze();
+            // test hook (ddl_testing_control_fault): the control link is lost right after this
+            // rank froze its user collectives for the round — the answer below cannot be sent
+            if (g_control_fault.exchange(0)) ch_->close_all();
+            return at;
+        });
     run_agreed_(a);
 }
 
@@ -1095,6 +1118,7 @@ void RequestHandler::register_hosts_(const std::vector<std::pair<const void *, s
         auto it = reg_.upper_bound(lo);  // inside an entry already: touch it
         if (it != reg_.begin() && std::prev(it)->first <= lo && hi <= std::prev(it)->first + std::prev(it)->second.first) {
             std::prev(it)->second.second = ++reg_tick_;
+            config().host_register_hits.fetch_add(1);
             continue;
         }
         if (mapped_host_range(r.first, r.second)) continue;  // pinned already (the framework's own)
@@ -1169,8 +1193,12 @@ void RequestHandler::allreduce_reqs_(std::vector<Request> &reqs, std::vector<Don
             elems.push_back(reqs[i].n);
             esz.push_back(es);
         }
+        // a host group holds the registration lock while its plans are posted: release_registrations
+        // (ddl_set_config on the user's thread) then waits, and its stream sync covers every plan
+        // already posted with a device alias of a registered range
+        std::unique_lock<std::mutex> rg(reg_mu_, std::defer_lock);
+        if (host) rg.lock();
         if (host && config().host_register_cache_bytes.load() > 0) {
-            std::lock_guard<std::mutex> rg(reg_mu_);
             std::vector<std::pair<const void *, size_t>> ranges;  // pageable tensors used again and again
             for (size_t i : g.second) {
                 ranges.emplace_back(reqs[i].in, reqs[i].n * es);
@@ -1277,8 +1305,12 @@ void RequestHandler::broadcast_reqs_(std::vector<Request> &reqs, std::vector<Don
             elems.push_back(reqs[i].n);
             esz.push_back(es);
         }
+        // a host group holds the registration lock while its plans are posted: release_registrations
+        // (ddl_set_config on the user's thread) then waits, and its stream sync covers every plan
+        // already posted with a device alias of a registered range
+        std::unique_lock<std::mutex> rg(reg_mu_, std::defer_lock);
+        if (host) rg.lock();
         if (host && config().host_register_cache_bytes.load() > 0) {
-            std::lock_guard<std::mutex> rg(reg_mu_);
             std::vector<std::pair<const void *, size_t>> ranges;  // pageable tensors used again and again
             for (size_t i : g.second) {
                 ranges.emplace_back(reqs[i].in, reqs[i].n * es);

@@ -349,4 +349,8 @@ private:
     std::thread done_thread_;
 };
 
+// Test hook (ddl_testing_control_fault): the next keyed round a member joins closes that member's
+// control link right after its snapshot froze the user collectives (a link lost mid-round).
+void set_testing_control_fault(int on);
+
 }  // namespace ddl

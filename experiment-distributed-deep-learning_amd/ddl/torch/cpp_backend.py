@@ -145,6 +145,7 @@ class CPPBackend:
         sig('ddl_testing_thread_allgatherv', ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz),
             ctypes.POINTER(sz), ci, vp)
         sig('ddl_testing_drop_wait', ci, ci)
+        sig('ddl_testing_control_fault', ci, ci)
         sig('ddl_testing_dep_trace', ci, ci)
         sig('ddl_testing_thread_fused_allreduce', ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp),
             ctypes.POINTER(sz), ci, vp, ctypes.POINTER(sz))

@@ -159,10 +159,15 @@ int ddl_is_initialized(void);
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
  * The shared tunables (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, tune,
  * fusion_pipeline_bytes, reference_order, host_chunk_bytes) must be equal on every rank of a
- * communicator: the ranks agree on a hash of them at a communicator's first collective and
- * whenever this rank's values changed since (change them on every rank between the same two
- * collectives), and every keyed round carries the hash; on a mismatch the collective or round
- * fails on every rank with DDL_STATUS_CONFIG_MISMATCH instead of building different programs.
+ * communicator. Direct collectives: the ranks exchange a hash of them at a communicator's first
+ * collective and at the next collective after this rank's values changed; a mismatch found there
+ * fails that collective on every rank with DDL_STATUS_CONFIG_MISMATCH instead of building
+ * different programs. That exchange is itself collective, so it is only matched when EVERY rank
+ * changes its shared values between the same two collectives (to equal or different values);
+ * changing them on some ranks only, after the first collective, is unsupported — those ranks post
+ * an exchange the others never match, and the communicator hangs (there is no per-collective
+ * check: it would cost a host-synchronising exchange on every call). Keyed rounds carry each
+ * rank's hash in their tokens, so they detect any difference, one-sided included.
  * A change of the shared tunables drops the tuned choices; the other keys are per process. */
 int ddl_set_config(const char *key, long long value);
 long long ddl_get_config(const char *key);
@@ -238,7 +243,10 @@ int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, in
  * direct collectives (ddl_allreduce[_batch], ddl_broadcast, ddl_allgather[v], ddl_allreduce_host,
  * split_communicator) on every rank, so both RCCL communicators see their work in one order
  * everywhere. A direct collective issued while a round is being placed waits for the placement
- * (one negotiation). */
+ * (one negotiation). If the communicator's handler stops on an error (a control link lost, a
+ * token-protocol fault), its pending requests complete with that status, and from then on every
+ * direct collective on the communicator returns it too instead of waiting for a placement that
+ * can no longer happen: the communicator is unusable, finalize and re-initialise. */
 int ddl_allreduce_submit(ddl_communicator_id id, const char *key, const void *in, void *out,
                          size_t elements, int dtype, int op, void *hip_stream,
                          ddl_done_fn done, void *user);
@@ -290,6 +298,15 @@ int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes,
 
 #ifdef __cplusplus
 }
+#endif
+
+/* Transition aid (r03 moved the test / diagnostic entry points — ddl_init_test_transport,
+ * ddl_p2p_op, ddl_control_negotiate*, ddl_allreduce_variant, ddl_reduce_*, ddl_pack / ddl_unpack,
+ * ddl_local_*, the schedule introspection — into ddl_amd_testing.h; the symbols are still
+ * exported): define DDL_AMD_WITH_TESTING_API before including this header to get them as before.
+ * ddl_init_test_transport also needs DDL_ALLOW_TEST_TRANSPORT=1 in the environment. */
+#ifdef DDL_AMD_WITH_TESTING_API
+#include "ddl_amd_testing.h"
 #endif
 
 #endif /* DDL_AMD_H */

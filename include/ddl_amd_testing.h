@@ -158,6 +158,12 @@ int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *co
  * bytes[i] bytes (whole elements of dtype); *subplans (may be NULL) = the sub-plans per rank. */
 int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const *srcs, void *const *dsts,
                                        const size_t *bytes, int dtype, void *hip_stream, size_t *subplans);
+/* Fault injection for the keyed handler's error path: with on = 1, the next keyed round a member
+ * rank joins closes that rank's control link right after it froze its user collectives for the
+ * round (a link lost mid-round). Every rank's handler then stops, its pending requests complete
+ * with an error, and later user collectives on the communicator return that error instead of
+ * blocking behind the round that can no longer be placed. */
+int ddl_testing_control_fault(int on);
 /* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
  * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
 int ddl_testing_drop_wait(int tick);

@@ -523,6 +523,44 @@ def check_keyed_round_order(ctx):
     assert mine[1] and mine[1] == sorted(mine[1]), mine
 
 
+def check_control_link_lost(ctx):
+    """a member's control link is lost right after it froze its user
+    collectives for a keyed round (ddl_testing_control_fault on rank 1). Every rank's handler
+    stops: the pending keyed request completes with an error on every rank, ddl_wait_all returns,
+    and a later direct ddl_allreduce on the communicator returns the error instead of blocking
+    behind the round that can no longer be placed. Run on its own (it leaves the handler dead)."""
+    import threading
+
+    import _helpers as h
+    from ddl.torch.cpp_backend import DONE_FN
+    from ddl.torch.tensor_communicate import allreduce_async
+    torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
+    s = torch.cuda.current_stream().cuda_stream
+    w = torch.full((500,), float(r), device='cuda')  # a healthy round first: the ring is up
+    assert torch.equal(allreduce_async(w, 'warm', comm).wait(timeout=60), torch.full_like(w, float(P * (P - 1) // 2)))
+    if r == 1:
+        assert lib.ddl_testing_control_fault(1) == 0
+    ctx['dist'].barrier()
+    got, ev = [], threading.Event()
+
+    @DONE_FN
+    def done(status, user):
+        got.append(status)
+        ev.set()
+    y = torch.full((300,), float(r), device='cuda')
+    assert lib.ddl_allreduce_submit(comm.id, b'lost', y.data_ptr(), y.data_ptr(), 300, h.DT_FLOAT, 0, s,
+                                    done, None) == 0, lib.ddl_last_error()
+    assert ev.wait(60) and got and got[0] != 0, got
+    lib.ddl_wait_all(comm.id)  # returns: it must not block on the stopped handler
+    x = torch.full((4099,), float(r), device='cuda')
+    st = lib.ddl_allreduce(comm.id, x.data_ptr(), x.data_ptr(), x.numel(), h.DT_FLOAT, 0, s)
+    msg = lib.ddl_last_error().decode()
+    assert st != 0 and 'handler stopped' in msg, (st, msg)
+
+
+FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost}
+
+
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,
           check_keyed_fusion,
           check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
@@ -530,7 +568,7 @@ CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allred
           check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]
 
 
-def worker(rank, world, port, q):
+def worker(rank, world, port, q, only=None):
     results = []
     try:
         for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), HERE, os.path.join(ROOT, 'tools')):
@@ -565,7 +603,7 @@ def worker(rank, world, port, q):
         ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
                'oracle': h.Oracle()}
         import time
-        for fn in CHECKS:
+        for fn in ([FAULT_CHECKS[n] for n in only] if only else CHECKS):
             try:
                 t0 = time.perf_counter()
                 fn(ctx)

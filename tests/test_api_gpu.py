@@ -412,6 +412,56 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
             lib.ddl_set_config(k, v)
 
 
+def test_registration_cache_address_reuse(world, lib):
+    """the registration cache is keyed by virtual address. A cached pageable
+    tensor's pages are unmapped and fresh pages mapped at the same address (munmap, then mmap
+    MAP_FIXED); the next keyed host allreduce on that range is a cache hit (host_register_hits)
+    and must still read and write the NEW pages — the GPU driver's userptr registration follows
+    the process's page tables (invalidated on munmap, restored from the new mapping) — so the
+    result is the new tensor's, bit for bit, through the zero-copy unpack path."""
+    import mmap as _mmap
+    from ddl.torch.tensor_communicate import allreduce_async
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    n = 3 << 20  # 12 MiB of fp32: several host chunks below
+    size = n * 4
+    prot = _mmap.PROT_READ | _mmap.PROT_WRITE
+    flags = _mmap.MAP_PRIVATE | _mmap.MAP_ANONYMOUS
+    MAP_FIXED = 0x10
+    addr = libc.mmap(None, size, prot, flags, -1, 0)
+    assert addr not in (None, ctypes.c_void_p(-1).value)
+    keys = (b'one_rank_shortcut', b'host_chunk_bytes', b'host_register_cache_bytes', b'host_zero_copy')
+    old = {k: lib.ddl_get_config(k) for k in keys}
+    try:
+        for k, v in ((b'one_rank_shortcut', 0), (b'host_chunk_bytes', 4 << 20), (b'host_register_cache_bytes', 1 << 30),
+                     (b'host_zero_copy', 1)):
+            assert lib.ddl_set_config(k, v) == 0
+        g = torch.Generator().manual_seed(5)
+        for rnd in range(3):
+            x = torch.frombuffer((ctypes.c_char * size).from_address(addr), dtype=torch.float32)
+            want = torch.randn(n, generator=g)
+            x.copy_(want)
+            hits0, zc0 = lib.ddl_get_config(b'host_register_hits'), lib.ddl_get_config(b'host_zero_copy_plans')
+            got = allreduce_async(x, f'reuse_{rnd}', world, output=x).wait(timeout=60)  # in place
+            assert torch.equal(got, want), f'round {rnd}: the keyed result is not the tensor now at the address'
+            assert torch.equal(x, want)
+            if rnd:  # the range was registered by round 0: a hit, and the device unpack path ran
+                assert lib.ddl_get_config(b'host_register_hits') > hits0
+                assert lib.ddl_get_config(b'host_zero_copy_plans') > zc0
+            del x
+            # new pages at the same address: the cache entry now names a range whose pages changed
+            assert libc.munmap(ctypes.c_void_p(addr), size) == 0
+            again = libc.mmap(ctypes.c_void_p(addr), size, prot, flags | MAP_FIXED, -1, 0)
+            assert again == addr
+    finally:
+        assert lib.ddl_set_config(b'host_register_cache_bytes', 0) == 0  # unregisters the cached range
+        for k, v in old.items():
+            lib.ddl_set_config(k, v)
+        libc.munmap(ctypes.c_void_p(addr), size)
+
+
 def _cpulist(text):
     out = set()
     for part in text.strip().split(','):

@@ -56,3 +56,37 @@ def test_engine_multiprocess_on_one_gpu(gpu, world, pipelined, monkeypatch):
     for rank, results in sorted(res.items()):
         for name, ok, detail in results:
             assert ok, f'rank {rank} {name}:\n{detail}'
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_control_link_lost_mid_round(gpu, world):
+    """a control link lost after a member froze its user collectives for a keyed round
+    stops every rank's handler; keyed requests complete with an error and direct collectives
+    return one instead of hanging (tests/_mp_gpu_worker.py check_control_link_lost)."""
+    import torch.multiprocessing as mp
+
+    import _mp_gpu_worker
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_gpu_worker.worker, args=(r, world, port, q, ['check_control_link_lost']))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, results = q.get(timeout=120)
+            res[rank] = results
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    assert sorted(res) == list(range(world)), f'ranks reported: {sorted(res)}'
+    for rank, results in sorted(res.items()):
+        assert [n for n, _, _ in results][:1] == ['check_control_link_lost'], results
+        for name, ok, detail in results:
+            assert ok, f'rank {rank} {name}:\n{detail}'
