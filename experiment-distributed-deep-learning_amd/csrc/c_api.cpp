@@ -150,14 +150,27 @@ void negotiate_keys(ControlChannel &ch, const char *keys, char *out, size_t len)
 
 // One thread world per (ranks, device, compute_cu_mask): its executors' compute streams are
 // created with the mask in force when the world is.
+// ddl_testing_thread_transport: 0 = device copies, 1 = RCCL loopback (the thread worlds made while
+// it is 1 move their bytes through the RCCL loopback communicator)
+std::atomic<int> g_thread_rccl{0};
+std::mutex g_thread_mu;
+std::map<std::tuple<int, int, int, ncclComm_t>, std::unique_ptr<ThreadWorld>> *g_thread_worlds =
+    new std::map<std::tuple<int, int, int, ncclComm_t>, std::unique_ptr<ThreadWorld>>();
+
 ThreadWorld &thread_world(int nranks) {
-    static std::mutex mu;
-    static auto *worlds = new std::map<std::tuple<int, int, int>, std::unique_ptr<ThreadWorld>>();
     int dev = current_device();
-    std::lock_guard<std::mutex> g(mu);
-    auto key = std::make_tuple(nranks, dev, config_compute_cu_mask());
-    auto it = worlds->find(key);
-    if (it == worlds->end()) it = worlds->emplace(key, std::unique_ptr<ThreadWorld>(new ThreadWorld(nranks, dev))).first;
+    ncclComm_t loop = nullptr;
+    if (g_thread_rccl.load()) {
+        RcclLoopback &l = rccl_loopback();
+        std::lock_guard<std::mutex> lg(l.mu);
+        DDL_REQUIRE(l.comm, DDL_STATUS_NOT_INITIALIZED, "thread transport 1 needs ddl_rccl_loopback_init first");
+        loop = l.comm;
+    }
+    std::lock_guard<std::mutex> g(g_thread_mu);
+    auto key = std::make_tuple(nranks, dev, config_compute_cu_mask(), loop);
+    auto it = g_thread_worlds->find(key);
+    if (it == g_thread_worlds->end())
+        it = g_thread_worlds->emplace(key, std::unique_ptr<ThreadWorld>(new ThreadWorld(nranks, dev, loop))).first;
     return *it->second;
 }
 
@@ -918,6 +931,20 @@ int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const 
     });
 }
 
+int ddl_testing_thread_transport(int rccl, long long *loopback_pairs) {
+    return guarded([&] {
+        DDL_REQUIRE(rccl == 0 || rccl == 1, DDL_STATUS_INVALID_ARGUMENT, "thread transport " << rccl);
+        if (loopback_pairs) {
+            long long n = 0;
+            std::lock_guard<std::mutex> g(g_thread_mu);
+            for (auto &kv : *g_thread_worlds)
+                if (std::get<3>(kv.first)) n += kv.second->loopback_pairs();
+            *loopback_pairs = n;
+        }
+        g_thread_rccl = rccl;
+    });
+}
+
 int ddl_testing_control_fault(int on) {
     return guarded([&] { set_testing_control_fault(on); });
 }
@@ -1119,6 +1146,11 @@ int ddl_rccl_loopback_finalize(void) {
         std::lock_guard<std::mutex> g(l.mu);
         (void)hipDeviceSynchronize();
         l.worlds.clear();
+        {  // thread worlds moving their bytes through these communicators go first
+            std::lock_guard<std::mutex> tg(g_thread_mu);
+            for (auto it = g_thread_worlds->begin(); it != g_thread_worlds->end();)
+                it = std::get<3>(it->first) ? g_thread_worlds->erase(it) : std::next(it);
+        }
         for (auto it = l.owned.rbegin(); it != l.owned.rend(); ++it) (void)rccl().CommDestroy(*it);
         l.owned.clear();
         l.comm = nullptr;

@@ -483,6 +483,10 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     p.finish();
 }
 
+ThreadFabric::ThreadFabric(int P, ncclComm_t loopback) : P_(P), q_((size_t)P * P) {
+    if (loopback) loop_.reset(new RcclTransport(loopback));
+}
+
 ThreadFabric::~ThreadFabric() {
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
 }
@@ -552,7 +556,15 @@ void ThreadFabric::group(int rank, const std::vector<P2POp> &ops, hipStream_t st
                                   << sd->ptr << " -> " << op.ptr);
         DDL_HIP(hipStreamWaitEvent(stream, sd->ready, 0));
         dep::wait(stream, sd->ready);
-        if (op.bytes) DDL_HIP(hipMemcpyAsync(op.ptr, sd->ptr, op.bytes, hipMemcpyDeviceToDevice, stream));
+        if (op.bytes && loop_) {  // the bytes through RCCL: a self pair in one group on this stream
+            std::lock_guard<std::mutex> lg(loop_mu_);
+            loop_->group({P2POp{true, 0, op.tag, const_cast<void *>(sd->ptr), op.bytes},
+                          P2POp{false, 0, op.tag, op.ptr, op.bytes}},
+                         stream);
+            ++loopback_pairs;
+        } else if (op.bytes) {
+            DDL_HIP(hipMemcpyAsync(op.ptr, sd->ptr, op.bytes, hipMemcpyDeviceToDevice, stream));
+        }
         if (dep::on()) {
             std::ostringstream os;
             os << "recv rank " << rank << " <- " << op.peer << " tag " << op.tag;
@@ -600,8 +612,8 @@ void ThreadTransport::allgather(const GatherOp &g, hipStream_t stream) {
     group(ops, stream);
 }
 
-ThreadWorld::ThreadWorld(int nranks, int device) : P_(nranks), device_(device) {
-    fab_ = std::make_shared<ThreadFabric>(nranks);
+ThreadWorld::ThreadWorld(int nranks, int device, ncclComm_t loopback) : P_(nranks), device_(device) {
+    fab_ = std::make_shared<ThreadFabric>(nranks, loopback);
     for (int r = 0; r < nranks; ++r) {
         ex_.emplace_back(new RingExecutor(r, nranks, device, std::unique_ptr<Transport>(new ThreadTransport(fab_, r))));
         hipStream_t s;

@@ -149,7 +149,11 @@ private:
 // transport (CallbackTransport) would hide.
 class ThreadFabric {
 public:
-    explicit ThreadFabric(int P) : P_(P), q_((size_t)P * P) {}
+    // `loopback` (a one-rank RCCL communicator, optional): each matched send / receive pair moves
+    // its bytes through RcclTransport::group as a self send + self receive on the receiver's
+    // stream (after the wait on the sender's ready event) instead of a D2D copy — the production
+    // executor then runs asynchronously AND hands its data to RCCL (ddl_testing_thread_transport)
+    explicit ThreadFabric(int P, ncclComm_t loopback = nullptr);
     ~ThreadFabric();
     ThreadFabric(const ThreadFabric &) = delete;
     ThreadFabric &operator=(const ThreadFabric &) = delete;
@@ -176,6 +180,10 @@ private:
     std::vector<hipEvent_t> events_;
     size_t next_event_ = 0;
     bool aborted_ = false;
+    std::unique_ptr<RcclTransport> loop_;  // see the constructor
+    std::mutex loop_mu_;                   // one thread at a time inside an RCCL group
+public:
+    long long loopback_pairs = 0;          // pairs moved through RCCL (under loop_mu_)
 };
 
 class ThreadTransport : public Transport {
@@ -308,7 +316,8 @@ private:
 // on its own stream forked from / joined to the caller's (test / diagnostic path).
 class ThreadWorld {
 public:
-    ThreadWorld(int nranks, int device);
+    ThreadWorld(int nranks, int device, ncclComm_t loopback = nullptr);
+    long long loopback_pairs() const { return fab_->loopback_pairs; }
     ~ThreadWorld();
     void allreduce(const void *const *in, void *const *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);

@@ -146,6 +146,7 @@ class CPPBackend:
             ctypes.POINTER(sz), ci, vp)
         sig('ddl_testing_drop_wait', ci, ci)
         sig('ddl_testing_control_fault', ci, ci)
+        sig('ddl_testing_thread_transport', ci, ci, ctypes.POINTER(ctypes.c_longlong))
         sig('ddl_testing_dep_trace', ci, ci)
         sig('ddl_testing_thread_fused_allreduce', ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp),
             ctypes.POINTER(sz), ci, vp, ctypes.POINTER(sz))

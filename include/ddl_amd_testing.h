@@ -158,6 +158,12 @@ int ddl_testing_thread_allgatherv(int nranks, const void *const *sends, void *co
  * bytes[i] bytes (whole elements of dtype); *subplans (may be NULL) = the sub-plans per rank. */
 int ddl_testing_thread_fused_allreduce(int nranks, int count, const void *const *srcs, void *const *dsts,
                                        const size_t *bytes, int dtype, void *hip_stream, size_t *subplans);
+/* Data movement of the thread worlds made from now on: rccl = 0 device copies (default); 1 every
+ * matched send / receive pair goes through RcclTransport::group as a self send + self receive on
+ * the RCCL loopback communicator (ddl_rccl_loopback_init first), posted on the receiver's stream
+ * after its wait on the sender's event — the production executor, asynchronous, handing its bytes
+ * to RCCL. *loopback_pairs (may be NULL) = pairs moved through RCCL so far by such worlds. */
+int ddl_testing_thread_transport(int rccl, long long *loopback_pairs);
 /* Fault injection for the keyed handler's error path: with on = 1, the next keyed round a member
  * rank joins closes that rank's control link right after it froze its user collectives for the
  * round (a link lost mid-round). Every rank's handler then stops, its pending requests complete
