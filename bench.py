@@ -401,16 +401,19 @@ def fold_roofline(lib, dev, sh, S, nb=7, order=0, half=False, form=0):
             if order == 0 and ((S == 256 << 20 and not half) or (S == 16 << 20 and half)) else None}
 
 
-def fold_batch_roofline(lib, dev, sh, buckets=64, per_launch=8, bucket_bytes=16 << 20, P=8):
+def fold_batch_roofline(lib, dev, sh, buckets=64, per_launch=8, bucket_bytes=16 << 20, P=8, form=0):
     """C4's folds as the grouped allreduce launches them: `buckets` fp16 buckets of `bucket_bytes`
     at P ranks -> one chunk of bucket_bytes / P per bucket with P - 1 received inputs; the chunks of
     `per_launch` buckets share one launch (ddl_reduce_fold_batch, FoldBatch: blockIdx.y = bucket).
     All buckets' operands live at once (64 x 9 x 2 MiB = 1.2 GB: HBM, not the Infinity Cache). The
     launches of one pass over the buckets are captured into a hipGraph and replayed between HIP
-    events; `us` is the mean per launch over 3 rounds."""
+    events; `us` is the mean per launch over 3 rounds. `form` (config fold_form): 0 the engine's
+    choice, 1 the tile form, 2 the run form."""
     import torch
     from ddl.torch.cpp_backend import check
     nb, es = P - 1, 2
+    old_form = lib.ddl_get_config(b'fold_form')
+    check(lib.ddl_set_config(b'fold_form', form), 'ddl_set_config')
     n = bucket_bytes // P // es
     sets = [[torch.rand(n, device=dev).half() for _ in range(nb + 2)] for _ in range(buckets)]  # in, inputs, out
     V = ctypes.c_void_p
@@ -424,12 +427,15 @@ def fold_batch_roofline(lib, dev, sh, buckets=64, per_launch=8, bucket_bytes=16 
     def run(stream):
         for outs, as_, ins, ns, c in launches:
             check(lib.ddl_reduce_fold_batch(c, outs, as_, ins, nb, ns, 19, 0, stream), 'ddl_reduce_fold_batch')
-    run(sh)
-    torch.cuda.synchronize()
-    gs = torch.cuda.Stream()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=gs):
-        run(gs.cuda_stream)
+    try:
+        run(sh)
+        torch.cuda.synchronize()
+        gs = torch.cuda.Stream()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gs):  # the form is fixed at capture
+            run(gs.cuda_stream)
+    finally:
+        check(lib.ddl_set_config(b'fold_form', old_form), 'ddl_set_config')
     rounds = []
     for _ in range(3):
         with torch.cuda.stream(gs):
