@@ -405,6 +405,7 @@ long long ddl_get_config(const char *key) {
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable
     if (k == "host_register_failures") return c.host_register_failures;  // statistic, not settable
     if (k == "host_register_hits") return c.host_register_hits;          // statistic, not settable
+    if (k == "host_unregistered_ranges") return c.host_unregistered_ranges;  // statistic, not settable
     if (k == "host_zero_copy_plans") return c.host_zero_copy_plans;  // statistic, not settable
     if (k == "host_pack_us") return c.host_pack_ns / 1000;      // statistic, not settable
     if (k == "host_wait_us") return c.host_wait_ns / 1000;      // statistic, not settable
@@ -752,6 +753,13 @@ int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes,
         *launches = s.launches;
         *bytes = s.bytes;
         *ms = s.ms;
+    });
+}
+
+int ddl_host_unregister(const void *ptr, size_t bytes) {
+    return guarded([&] {
+        for (auto &comm : Registry::get().all())
+            if (RequestHandler *h = comm->handler_if_created()) h->unregister_range(ptr, bytes);
     });
 }
 

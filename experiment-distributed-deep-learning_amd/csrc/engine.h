@@ -59,6 +59,7 @@ struct Config {
     std::atomic<long long> host_registered_bytes{0};
     std::atomic<long long> host_register_failures{0};
     std::atomic<long long> host_register_hits{0};  // tensors found inside a cached registration
+    std::atomic<long long> host_unregistered_ranges{0};  // cached registrations dropped by ddl_host_unregister
     // read-only statistic (ddl_get_config "host_zero_copy_plans"): keyed host allreduce plans
     // that unpacked on the device in this process
     std::atomic<long long> host_zero_copy_plans{0};

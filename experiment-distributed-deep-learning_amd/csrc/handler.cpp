@@ -1090,7 +1090,51 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
 void RequestHandler::release_registrations() {
     std::lock_guard<std::mutex> g(reg_mu_);
     DeviceGuard dg(owner_->device());
+    {
+        std::lock_guard<std::mutex> q(unreg_mu_);
+        unreg_q_.clear();  // everything goes anyway
+    }
     if (!reg_.empty()) unregister_all_();
+}
+
+void RequestHandler::unregister_range(const void *ptr, size_t bytes) {
+    if (!ptr || !bytes) return;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
+    std::unique_lock<std::mutex> g(reg_mu_, std::try_to_lock);
+    if (!g.owns_lock()) {  // a host plan is being posted: the engine drains the queue before its next lookup
+        std::lock_guard<std::mutex> q(unreg_mu_);
+        unreg_q_.emplace_back(lo, hi);
+        return;
+    }
+    DeviceGuard dg(owner_->device());
+    drain_unregisters_();
+    drop_overlapping_(lo, hi);
+}
+
+void RequestHandler::drain_unregisters_() {
+    std::vector<std::pair<uintptr_t, uintptr_t>> q;
+    {
+        std::lock_guard<std::mutex> g(unreg_mu_);
+        q.swap(unreg_q_);
+    }
+    for (const auto &r : q) drop_overlapping_(r.first, r.second);
+}
+
+void RequestHandler::drop_overlapping_(uintptr_t lo, uintptr_t hi) {
+    std::vector<uintptr_t> drop;
+    for (auto &e : reg_)
+        if (e.first < hi && lo < e.first + e.second.first) drop.push_back(e.first);
+    if (drop.empty()) return;
+    for (hipStream_t st : {h2d_, d2h_, stream_})  // plans in flight may still DMA from / to them
+        if (st) DDL_HIP(hipStreamSynchronize(st));
+    for (uintptr_t a : drop) {
+        (void)hipHostUnregister(reinterpret_cast<void *>(a));
+        reg_bytes_ -= reg_[a].first;
+        config().host_registered_bytes.fetch_sub((long long)reg_[a].first);
+        config().host_unregistered_ranges.fetch_add(1);
+        reg_.erase(a);
+    }
+    (void)hipGetLastError();
 }
 
 void RequestHandler::unregister_all_() {
@@ -1107,6 +1151,7 @@ void RequestHandler::unregister_all_() {
 
 void RequestHandler::register_hosts_(const std::vector<std::pair<const void *, size_t>> &ranges) {
     constexpr uintptr_t kPage = 4096;
+    drain_unregisters_();  // ranges freed since the last lookup are not hits
     const size_t cap = (size_t)config().host_register_cache_bytes.load();
     // 1) the page ranges of the tensors not pinned already, merged where they share pages (small
     //    tensors of one heap page; hipHostRegister refuses a page registered twice)

@@ -202,6 +202,11 @@ public:
     // Unregisters every range of the host registration cache (ddl_set_config
     // "host_register_cache_bytes" 0): waits for the handler's streams first.
     void release_registrations();
+    // The host range [ptr, ptr + bytes) is about to be freed (ddl_host_unregister): every cached
+    // registration overlapping it goes — now if no host plan is being posted, otherwise before the
+    // next lookup of the cache (the engine thread drains the queue first), so a later tensor at the
+    // same address is never taken for the old, still-registered pages.
+    void unregister_range(const void *ptr, size_t bytes);
     // All-or-nothing registration of several requests under one lock (one wake-up).
     void submit_batch(std::vector<Request> &rs);
     void wait_all();
@@ -318,6 +323,11 @@ private:
     // are merged (a page cannot be registered twice), overlapping entries join the union
     void register_hosts_(const std::vector<std::pair<const void *, size_t>> &ranges);
     void unregister_all_();  // the cache was switched off (host_register_cache_bytes 0)
+    // drops the entries overlapping [lo, hi) (reg_mu_ held); syncs the handler's streams first
+    void drop_overlapping_(uintptr_t lo, uintptr_t hi);
+    void drain_unregisters_();  // reg_mu_ held: the queued unregister_range calls
+    std::mutex unreg_mu_;
+    std::vector<std::pair<uintptr_t, uintptr_t>> unreg_q_;
     std::mutex reg_mu_;  // reg_: the engine thread registers, ddl_set_config may release
     std::map<uintptr_t, std::pair<size_t, uint64_t>> reg_;  // page-aligned start -> (bytes, last use)
     size_t reg_bytes_ = 0;

@@ -109,6 +109,7 @@ class CPPBackend:
         sig('ddl_control_channel_negotiate', ci, ctypes.c_longlong, ctypes.c_char_p, ctypes.c_char_p, sz)
         sig('ddl_control_channel_close', ci, ctypes.c_longlong)
         sig('ddl_wait_all', ci, cid)
+        sig('ddl_host_unregister', ci, ctypes.c_void_p, ctypes.c_size_t)
         sig('ddl_broadcast_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
         sig('ddl_allgather_submit', ci, cid, ctypes.c_char_p, vp, sz, sz, ci, vp, ALLOC_FN, DONE_FN, vp)
         sig('ddl_broadcast', ci, cid, vp, sz, ci, ci, vp)

@@ -14,6 +14,7 @@ through pinned memory to the GPU, reduced there and copied back.
 import ctypes
 import itertools
 import threading
+import weakref
 
 import torch
 
@@ -190,6 +191,37 @@ def _on_done(status, user):
         h._event.set()
 
 
+_watched = {}  # id(host tensor) -> its finalizer (see _watch_host)
+_watched_lock = threading.Lock()
+
+
+def _unregister_host(key, ptr, nbytes):
+    with _watched_lock:
+        _watched.pop(key, None)
+    try:
+        CPPBackend.c_api().ddl_host_unregister(ptr, nbytes)
+    except Exception:  # noqa: BLE001 (interpreter shutdown: the library may be gone)
+        pass
+
+
+def _watch_host(tensors):
+    """With the engine's host registration cache on (config host_register_cache_bytes > 0), every
+    host tensor a keyed request uses may stay registered after the request. Before such a tensor's
+    memory is freed its storage range must leave the cache (ddl_host_unregister): a later tensor at
+    the same address would otherwise be taken for the old, unmapped pages. A finalizer per tensor
+    object does that when the tensor is collected."""
+    lib = CPPBackend.c_api()
+    if lib.ddl_get_config(b'host_register_cache_bytes') <= 0:
+        return
+    for t in tensors:
+        if t.is_cuda or id(t) in _watched:
+            continue
+        st = t.untyped_storage()
+        with _watched_lock:
+            if id(t) not in _watched:
+                _watched[id(t)] = weakref.finalize(t, _unregister_host, id(t), st.data_ptr(), st.nbytes())
+
+
 def _same_memory(a: torch.Tensor, b: torch.Tensor, what: str) -> int:
     ma, mb = memory_kind(a, f'{what} input'), memory_kind(b, f'{what} output')
     if ma != mb:
@@ -209,6 +241,8 @@ def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     communicator = _comm(communicator)
     out = torch.empty_like(tensor) if output is None else output
     mem = _same_memory(tensor, out, 'allreduce_async')
+    if mem == cb.MEMORY_HOST:
+        _watch_host((tensor, out))
     uid = next(_ids)
     h = Handle(name, out, (tensor, out))
     with _pending_lock:
@@ -238,6 +272,8 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     if k == 0:
         return []
     mems = [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
+    if cb.MEMORY_HOST in mems:
+        _watch_host([x for i, m in enumerate(mems) if m == cb.MEMORY_HOST for x in (tensors[i], outputs[i])])
     uids = [next(_ids) for _ in range(k)]
     handles = [Handle(n, o, (t, o)) for n, t, o in zip(names, tensors, outputs)]
     with _pending_lock:
@@ -269,6 +305,8 @@ def broadcast_async(tensor: torch.Tensor, name: str, root_rank: int, communicato
     communicator = _comm(communicator)
     out = torch.empty_like(tensor) if output is None else output
     mem = _same_memory(tensor, out, 'broadcast_async')
+    if mem == cb.MEMORY_HOST:
+        _watch_host((tensor, out))
     uid = next(_ids)
     h = Handle(name, out, (tensor, out))
     with _pending_lock:

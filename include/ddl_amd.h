@@ -129,9 +129,11 @@ int ddl_is_initialized(void);
  * the GPU's NUMA node, where pinned host memory lives; 0: placement left to the OS),
  * "host_register_cache_bytes" (0, default = off; > 0: pageable host tensors of keyed requests
  * are hipHostRegister'ed once and the registrations kept, least recently used out past this many
- * bytes, so repeated allreduce(cpu_tensor) calls take the pinned paths — the caller keeps those
- * tensors allocated while cached; setting it to 0 unregisters every cached range at once, after
- * ddl_wait_all), the read-only timeline of keyed host plans "host_pack_us" / "host_wait_us" /
+ * bytes, so repeated allreduce(cpu_tensor) calls take the pinned paths — a cached range must be
+ * released with ddl_host_unregister before its memory is freed (the torch mirror does this for
+ * the tensors it submits); setting it to 0 unregisters every cached range at once, after
+ * ddl_wait_all; read-only statistics "host_registered_bytes", "host_register_hits",
+ * "host_register_failures", "host_unregistered_ranges"), the read-only timeline of keyed host plans "host_pack_us" / "host_wait_us" /
  * "host_unpack_us" (microseconds the engine thread spent packing chunks, waiting for a pinned
  * slot's DMA / device work, waiting for the unpack lane — staged results are unpacked by their own
  * copy threads while the next chunks are packed), "capture_mode" (0, default: inside a
@@ -288,6 +290,16 @@ int ddl_allgather_submit_mem(ddl_communicator_id id, const char *key, const void
                              ddl_done_fn done, void *user);
 /* Blocks until every request submitted on `id` so far has completed. */
 int ddl_wait_all(ddl_communicator_id id);
+
+/* With "host_register_cache_bytes" > 0: the host range [ptr, ptr + bytes) is about to be freed —
+ * call this BEFORE freeing (munmap / free / the framework's deallocator) any host tensor that was
+ * part of a keyed request. Every cached registration overlapping the range is dropped (at once,
+ * or — while the engine is posting a host plan — before its next cache lookup), so a later
+ * tensor placed at the same address is registered afresh instead of being taken for the old,
+ * now unmapped pages (a device access through the stale registration faults). The torch mirror
+ * (ddl.torch.tensor_communicate) calls it from a finalizer of every host tensor it submits while
+ * the cache is on. A no-op for ranges that are not cached. */
+int ddl_host_unregister(const void *ptr, size_t bytes);
 
 /* Measurement: bracket every reduce-kernel launch of ddl_allreduce on `id` with timing
  * events on the engine's compute stream (the stream the kernel runs on). ddl_kernel_stats

@@ -25,7 +25,7 @@ DEPLOYMENT = {
     'ddl_comm_transport', 'ddl_allreduce', 'ddl_allreduce_batch', 'ddl_broadcast', 'ddl_allgatherv', 'ddl_allgather',
     'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit',
     'ddl_allgather_submit', 'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem',
-    'ddl_allreduce_submit_batch_mem', 'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all',
+    'ddl_allreduce_submit_batch_mem', 'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all', 'ddl_host_unregister',
     'ddl_kernel_timing', 'ddl_kernel_stats'}
 
 

@@ -413,12 +413,17 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
 
 
 def test_registration_cache_address_reuse(world, lib):
-    """the registration cache is keyed by virtual address. A cached pageable
-    tensor's pages are unmapped and fresh pages mapped at the same address (munmap, then mmap
-    MAP_FIXED); the next keyed host allreduce on that range is a cache hit (host_register_hits)
-    and must still read and write the NEW pages — the GPU driver's userptr registration follows
-    the process's page tables (invalidated on munmap, restored from the new mapping) — so the
-    result is the new tensor's, bit for bit, through the zero-copy unpack path."""
+    """the registration cache is keyed by virtual address. r04 measured what the
+    advisor feared: a cached pageable range unmapped and mapped afresh at the same address (munmap,
+    then mmap MAP_FIXED) and used again faults the GPU (illegal memory access) — the old
+    registration's device mapping points at pages that are gone. So a cached range must leave the
+    cache before its memory is freed: ddl_host_unregister, which the torch mirror calls from a
+    finalizer of every host tensor it submits while the cache is on. Here, three rounds of: a
+    tensor over the mapping, two keyed allreduces in place (the second a cache hit through the
+    zero-copy unpack), the tensor dropped (its finalizer unregisters the range: registered bytes
+    back to where they were), then new pages at the same address — the next round's result is the
+    new tensor's, bit for bit. The munmap only happens once the range is out of the cache."""
+    import gc
     import mmap as _mmap
     from ddl.torch.tensor_communicate import allreduce_async
     libc = ctypes.CDLL(None, use_errno=True)
@@ -439,22 +444,38 @@ def test_registration_cache_address_reuse(world, lib):
                      (b'host_zero_copy', 1)):
             assert lib.ddl_set_config(k, v) == 0
         g = torch.Generator().manual_seed(5)
+        reg0 = lib.ddl_get_config(b'host_registered_bytes')
         for rnd in range(3):
             x = torch.frombuffer((ctypes.c_char * size).from_address(addr), dtype=torch.float32)
             want = torch.randn(n, generator=g)
             x.copy_(want)
-            hits0, zc0 = lib.ddl_get_config(b'host_register_hits'), lib.ddl_get_config(b'host_zero_copy_plans')
-            got = allreduce_async(x, f'reuse_{rnd}', world, output=x).wait(timeout=60)  # in place
-            assert torch.equal(got, want), f'round {rnd}: the keyed result is not the tensor now at the address'
-            assert torch.equal(x, want)
-            if rnd:  # the range was registered by round 0: a hit, and the device unpack path ran
-                assert lib.ddl_get_config(b'host_register_hits') > hits0
-                assert lib.ddl_get_config(b'host_zero_copy_plans') > zc0
+            for call in range(2):
+                hits0, zc0 = lib.ddl_get_config(b'host_register_hits'), lib.ddl_get_config(b'host_zero_copy_plans')
+                got = allreduce_async(x, f'reuse_{rnd}_{call}', world, output=x).wait(timeout=60)  # in place
+                assert torch.equal(got, want), f'round {rnd} call {call}: not the tensor now at the address'
+                del got
+            # the second call found the range in the cache and unpacked on the device
+            assert lib.ddl_get_config(b'host_register_hits') > hits0
+            assert lib.ddl_get_config(b'host_zero_copy_plans') > zc0
+            assert lib.ddl_get_config(b'host_registered_bytes') >= reg0 + size
+            unreg0 = lib.ddl_get_config(b'host_unregistered_ranges')
             del x
-            # new pages at the same address: the cache entry now names a range whose pages changed
+            gc.collect()
+            # the tensor's finalizer took the range out of the cache: safe to free it now
+            assert lib.ddl_get_config(b'host_unregistered_ranges') > unreg0
+            assert lib.ddl_get_config(b'host_registered_bytes') == reg0
             assert libc.munmap(ctypes.c_void_p(addr), size) == 0
             again = libc.mmap(ctypes.c_void_p(addr), size, prot, flags | MAP_FIXED, -1, 0)
             assert again == addr
+        # the C-ABI contract directly: a cached range, ddl_host_unregister, the cache no longer holds it
+        y = torch.frombuffer((ctypes.c_char * size).from_address(addr), dtype=torch.float32)
+        y.fill_(2.0)
+        assert torch.equal(allreduce_async(y, 'reuse_c', world, output=y).wait(timeout=60), torch.full((n,), 2.0))
+        assert lib.ddl_get_config(b'host_registered_bytes') >= reg0 + size
+        assert lib.ddl_host_unregister(ctypes.c_void_p(addr), ctypes.c_size_t(size)) == 0
+        assert lib.ddl_get_config(b'host_registered_bytes') == reg0
+        del y
+        gc.collect()
     finally:
         assert lib.ddl_set_config(b'host_register_cache_bytes', 0) == 0  # unregisters the cached range
         for k, v in old.items():
