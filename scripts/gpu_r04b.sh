@@ -9,7 +9,7 @@ timeout -k 10 700 python -u -m pytest tests/test_multiproc_gpu.py::test_control_
     --durations=10 > $O/new_tests.log 2>&1
 rc=$?; tail -30 $O/new_tests.log
 case $rc in 0|1) ;; *) exit $rc;; esac
-true
-rc2=0
+timeout -k 10 200 python tools/host_numa_ab.py > $O/host_numa_ab.jsonl 2>&1
+rc2=$?; tail -8 $O/host_numa_ab.jsonl
 [ $rc -ne 0 ] && exit $rc
 exit $rc2
