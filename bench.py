@@ -683,7 +683,12 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
         def step():
             check(lib.ddl_allreduce_submit_batch_mem(comm.id, *args), 'ddl_allreduce_submit_batch_mem')
             check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
-        step()
+        warm = []  # warm-up by time as host_resident_rate (freshly pinned tensors), each step timed
+        t_alloc = time.perf_counter()
+        while not warm or (time.perf_counter() - t_alloc < 0.5 and len(warm) < 8):
+            t1 = time.perf_counter()
+            step()
+            warm.append(round((time.perf_counter() - t1) * 1e3, 2))
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
         tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us', b'host_check_us', b'host_plan_us')
         tl0 = [lib.ddl_get_config(kk) for kk in tl_keys]
@@ -716,6 +721,7 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
             'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path, 'engine_thread': timeline,
+            'warmup_steps_ms': warm,
             'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},
             **(registered if 'host_register_cache_bytes' in settings else {})}
 
@@ -728,12 +734,22 @@ def host_resident_rate(lib, comm, S, reps):
     n = S // 4
     src = torch.rand(n, pin_memory=True)
     dst = torch.empty(n, pin_memory=True)
-    check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
+    # warm-up by time, each call timed: DMA over freshly pinned buffers reads ~1.6x slower for the
+    # first ~0.1-0.2 s after a long run of device kernels on some boxes (r04 s2: 10.2 ms per call
+    # for a whole first round, 6.2 ms from the next one on) — the steady rate is the
+    # one a training loop sees, the first calls are reported beside it
+    warm = []
+    t_alloc = time.perf_counter()
+    while len(warm) < 2 or (time.perf_counter() - t_alloc < 0.5 and len(warm) < 60):
+        t1 = time.perf_counter()
+        check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
+        warm.append(round((time.perf_counter() - t1) * 1e3, 3))
     t0 = time.perf_counter()
     for _ in range(reps):
         check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
     dt = (time.perf_counter() - t0) / reps
     return {'bucket_GiBs': round(S / GiB / dt, 2), 'ms': round(dt * 1e3, 3), 'bucket_bytes': S,
+            'warmup_calls_ms': warm[:12], 'warmup_calls': len(warm),
             'path': 'pinned host -> H2D -> ring allreduce -> D2H -> pinned host, 32 MiB chunks on 3 streams',
             'pcie_bytes_per_bucket': 2 * S}
 

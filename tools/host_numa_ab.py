@@ -64,10 +64,10 @@ def main():
                 os.sched_setaffinity(0, local)
             src = torch.rand(n, pin_memory=True)
             dst = torch.empty(n, pin_memory=True)
-            check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, 0, 0), 'ddl_allreduce_host')
+            check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, 1, 0), "ddl_allreduce_host")
             t0 = time.perf_counter()
             for _ in range(6):
-                check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, 0, 0), 'ddl_allreduce_host')
+                check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, 1, 0), "ddl_allreduce_host")
             ms = (time.perf_counter() - t0) / 6 * 1e3
             print(json.dumps({'rep': rep, 'bind': bind, 'ms': round(ms, 3), 'src_pages': page_nodes(src),
                               'dst_pages': page_nodes(dst), 'cpu': os.sched_getaffinity(0) == local}), flush=True)
