@@ -690,12 +690,20 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             step()
             warm.append(round((time.perf_counter() - t1) * 1e3, 2))
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
-        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us', b'host_check_us', b'host_plan_us')
+        tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us', b'host_check_us', b'host_plan_us',
+                   b'host_coll_us', b'host_d2h_post_us', b'host_unpack_submit_us')
         tl0 = [lib.ddl_get_config(kk) for kk in tl_keys]
+        cg0 = cgroup_cpu()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         dt = (time.perf_counter() - t0) / steps
+        cg1 = cgroup_cpu()
+        cgroup = None if not cg0 or not cg1 else {
+            'quota_cores': cg0['quota_cores'],
+            'cpu_cores_busy': round((cg1['usage_usec'] - cg0['usage_usec']) / 1e6 / (dt * steps), 2),
+            'throttled_periods_per_step': (cg1['nr_throttled'] - cg0['nr_throttled']) / steps,
+            'throttled_ms_per_step': round((cg1['throttled_usec'] - cg0['throttled_usec']) / 1e3 / steps, 2)}
         zero_copy_plans = lib.ddl_get_config(b'host_zero_copy_plans') - plans0
         # the engine thread's timeline per step: packing chunks into the pinned slots, waiting
         # for a slot's DMA / device work, waiting for the unpack lane (staged results are unpacked
@@ -707,7 +715,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
         # negotiation, planning, the last chunks' device work after the loop, done() (rest_ms)
         timeline = {'pack_ms': round(tl[0], 3), 'slot_wait_ms': round(tl[1], 3), 'unpack_ms': round(tl[2], 3),
                     'other_ms': round(dt * 1e3 - sum(tl[:3]), 3), 'check_ms': round(tl[3], 3),
-                    'plan_ms': round(tl[4], 3), 'rest_ms': round(dt * 1e3 - tl[3] - tl[4], 3)}
+                    'plan_ms': round(tl[4], 3), 'rest_ms': round(dt * 1e3 - tl[3] - tl[4], 3),
+                    'coll_post_ms': round(tl[5], 3), 'd2h_post_ms': round(tl[6], 3), 'unpack_submit_ms': round(tl[7], 3)}
         registered = {'host_registered_bytes': int(lib.ddl_get_config(b'host_registered_bytes')),
                       'host_register_failures': int(lib.ddl_get_config(b'host_register_failures'))}
     finally:
@@ -721,9 +730,35 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
             'pcie_bytes': 2 * int(total), 'host_chunk_bytes': int(lib.ddl_get_config(b'host_chunk_bytes')),
             'host_copy_threads': int(lib.ddl_get_config(b'host_copy_threads')),
             'device_unpack_plans_per_step': zero_copy_plans / steps, 'path': path, 'engine_thread': timeline,
-            'warmup_steps_ms': warm,
+            'warmup_steps_ms': warm, 'cgroup_cpu': cgroup,
             'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},
             **(registered if 'host_register_cache_bytes' in settings else {})}
+
+
+def cgroup_cpu():
+    """This process's cgroup (v2) CPU quota in cores and its throttling counters, or None: the GPU
+    boxes give a process a CPU share by quota, and the keyed host legs run up to 16 copy threads."""
+    try:
+        rel = [l.split(':', 2)[2].strip() for l in open('/proc/self/cgroup') if l.startswith('0::')][0]
+        base = '/sys/fs/cgroup' + rel
+        if not os.path.exists(base + '/cpu.max') and os.path.exists('/sys/fs/cgroup/cpu.max'):
+            base = '/sys/fs/cgroup'  # a cgroup namespace: the process's own group is the root
+        if os.path.exists(base + '/cpu.max'):  # cgroup v2
+            stat = dict(l.split() for l in open(base + '/cpu.stat'))
+            quota, period = open(base + '/cpu.max').read().split()
+            return {'quota_cores': None if quota == 'max' else round(int(quota) / int(period), 2),
+                    'nr_throttled': int(stat.get('nr_throttled', 0)),
+                    'throttled_usec': int(stat.get('throttled_usec', 0)), 'usage_usec': int(stat.get('usage_usec', 0))}
+        v1 = '/sys/fs/cgroup/cpu'  # cgroup v1 (the process's own cpu controller mount)
+        stat = dict(l.split() for l in open(v1 + '/cpu.stat'))
+        quota = int(open(v1 + '/cpu.cfs_quota_us').read())
+        period = int(open(v1 + '/cpu.cfs_period_us').read())
+        return {'quota_cores': None if quota < 0 else round(quota / period, 2),
+                'nr_throttled': int(stat.get('nr_throttled', 0)),
+                'throttled_usec': int(stat.get('throttled_time', 0)) // 1000,
+                'usage_usec': int(open('/sys/fs/cgroup/cpuacct/cpuacct.usage').read()) // 1000}
+    except (OSError, IndexError, ValueError):
+        return None
 
 
 def host_resident_rate(lib, comm, S, reps):

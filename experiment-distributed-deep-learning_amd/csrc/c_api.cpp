@@ -412,6 +412,9 @@ long long ddl_get_config(const char *key) {
     if (k == "host_unpack_us") return c.host_unpack_ns / 1000;  // statistic, not settable
     if (k == "host_check_us") return c.host_check_ns / 1000;    // statistic, not settable
     if (k == "host_plan_us") return c.host_plan_ns / 1000;      // statistic, not settable
+    if (k == "host_coll_us") return c.host_coll_ns / 1000;      // statistic, not settable
+    if (k == "host_d2h_post_us") return c.host_d2h_post_ns / 1000;  // statistic, not settable
+    if (k == "host_unpack_submit_us") return c.host_unpack_submit_ns / 1000;  // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;

@@ -74,6 +74,12 @@ struct Config {
     // each plan's staging loop (pack, slot waits, posting, unpack; host_plan_us)
     std::atomic<long long> host_check_ns{0};
     std::atomic<long long> host_plan_ns{0};
+    // inside the staging loop, besides pack / slot waits / unpack waits: the chunk's allreduce
+    // posting (host_coll_us), the D2H enqueue of staged chunks (host_d2h_post_us) and the unpack
+    // job's submission (host_unpack_submit_us)
+    std::atomic<long long> host_coll_ns{0};
+    std::atomic<long long> host_d2h_post_ns{0};
+    std::atomic<long long> host_unpack_submit_ns{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};

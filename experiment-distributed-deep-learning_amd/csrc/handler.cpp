@@ -986,6 +986,26 @@ CopyPool &RequestHandler::pool_for_config_() {
     return *pool_;
 }
 
+namespace {
+// Waits for a plan's event without holding a core for a whole long round: queries with yields
+// for the first 200 us (a plan about to land — small rounds keep their latency), then sleeps
+// between queries (each sleep ~20-70 us with the kernel's timer slack), so the completion thread
+// does not spin beside the engine thread, the host copies and the framework's own threads. Also
+// the unpack lane's wait for a D2H: hipEventSynchronize from a helper thread held up the engine
+// thread's own HIP calls on the same streams (r04 s2: ~27 ms per pageable C5 batch outside every
+// timed section of the staging loop; 3.9 ms once polled).
+hipError_t wait_plan(hipEvent_t e) {
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q != hipErrorNotReady) return q;
+        if (clk::now() - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+}  // namespace
+
 void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, bool upload,
                                   const std::function<void(void *, size_t)> &coll, bool padded, bool device_unpack) {
     std::vector<size_t> starts;
@@ -1019,7 +1039,9 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         CopyPool *op = out_pool_.get();
         unpacked[j] = lane_->submit([dev, landed, op, pc = std::move(pc)] {
             DeviceGuard g(dev);
-            DDL_HIP(hipEventSynchronize(landed));  // D2H of chunk j landed
+            // D2H of chunk j landed (polled: see wait_plan)
+            const hipError_t q = wait_plan(landed);
+            DDL_REQUIRE(q == hipSuccess, DDL_STATUS_HIP_ERROR, "D2H of a staged chunk: " << hipGetErrorString(q));
             op->run(pc);
         });
     };
@@ -1050,7 +1072,9 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         }
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
+        const clk::time_point t_coll = clk::now();
         coll(dslot_[k], n / es);
+        config().host_coll_ns.fetch_add(ns_since(t_coll));
         DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
         DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
         if (device_unpack) {
@@ -1073,11 +1097,17 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
             fp_.copier.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
         } else {
             if (i >= (size_t)kHostSlots) wait_unpack(i - kHostSlots);  // download slot k free again
+            const clk::time_point t_post = clk::now();
             DDL_HIP(hipMemcpyAsync(pout_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
+            config().host_d2h_post_ns.fetch_add(ns_since(t_post));
         }
         DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
         slot_used_[k] = true;
-        if (!device_unpack) unpack_async(i);
+        if (!device_unpack) {
+            const clk::time_point t_sub = clk::now();
+            unpack_async(i);
+            config().host_unpack_submit_ns.fetch_add(ns_since(t_sub));
+        }
     }
     if (device_unpack) {
         // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
@@ -1636,22 +1666,6 @@ void RequestHandler::execute_(const std::vector<ReqId> &ids, int forced) {
     if (status != DDL_STATUS_OK && status != forced) fail(status, "keyed collective failed");
 }
 
-namespace {
-// Waits for a plan's event without holding a core for a whole long round: queries with yields
-// for the first 200 us (a plan about to land — small rounds keep their latency), then sleeps
-// between queries (each sleep ~20-70 us with the kernel's timer slack), so the completion thread
-// does not spin beside the engine thread, the host copies and the framework's own threads.
-hipError_t wait_plan(hipEvent_t e) {
-    using clk = std::chrono::steady_clock;
-    const clk::time_point t0 = clk::now();
-    for (;;) {
-        const hipError_t q = hipEventQuery(e);
-        if (q != hipErrorNotReady) return q;
-        if (clk::now() - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-}
-}  // namespace
 
 // done() in plan order as each request's last element lands (MPIRTC.cc:593-597, 690-725).
 void RequestHandler::complete_(Round &rd) {
