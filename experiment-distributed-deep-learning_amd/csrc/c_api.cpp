@@ -350,8 +350,7 @@ int ddl_set_config(const char *key, long long value) {
         } else if (k == "host_copy_threads") {
             DDL_REQUIRE(value >= 0 && value <= 64, DDL_STATUS_INVALID_ARGUMENT, "host_copy_threads must be in [0, 64]");
             c.host_copy_threads = value;
-        } else if (k == "host_copy_nt") c.host_copy_nt = value ? 1 : 0;
-        else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
+        } else if (k == "host_zero_copy") c.host_zero_copy = value ? 1 : 0;
         else if (k == "host_numa_bind") c.host_numa_bind = value ? 1 : 0;
         else if (k == "host_register_cache_bytes") {
             DDL_REQUIRE(value >= 0, DDL_STATUS_INVALID_ARGUMENT, "host_register_cache_bytes must be >= 0");
@@ -401,7 +400,6 @@ long long ddl_get_config(const char *key) {
     if (k == "tune") return c.tune;
     if (k == "host_copy_threads") return c.host_copy_threads;
     if (k == "host_zero_copy") return c.host_zero_copy;
-    if (k == "host_copy_nt") return c.host_copy_nt;
     if (k == "host_register_cache_bytes") return c.host_register_cache_bytes;
     if (k == "host_numa_bind") return c.host_numa_bind;
     if (k == "host_registered_bytes") return c.host_registered_bytes;    // statistic, not settable

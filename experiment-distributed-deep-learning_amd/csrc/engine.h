@@ -39,9 +39,6 @@ struct Config {
     // memcpy workers of the keyed host-staging pipeline (pageable <-> pinned), besides the
     // engine thread itself
     std::atomic<long long> host_copy_threads{7};
-    // the copy threads' host memcpys (pack into the pinned slots, unpack out of them): 1 with
-    // non-temporal stores for pieces of at least 4 KiB (AVX2), 0 plain memcpy (local tunable)
-    std::atomic<long long> host_copy_nt{0};
     // keyed host allreduce plans whose outputs are all pinned and mapped into the device's
     // address space (torch pin_memory, hipHostMalloc, hipHostRegister): the unpack kernel writes
     // them over PCIe in place of the D2H copy and the host unpack memcpy (1 on, 0 always stage)

@@ -297,53 +297,12 @@ void CopyPool::parallel(size_t n, const std::function<void(size_t, size_t)> &fn)
     submit_and_wait_(tasks);
 }
 
-namespace {
-// dst <- src with non-temporal 32-byte stores (no read-for-ownership of the destination lines, which
-// go straight to memory: the pinned slot is read next by the GPU's DMA, a tensor by the framework
-// much later). memcpy switches to such stores only above a threshold near the L3 size, and the
-// pieces here are single tensors of 4 KiB .. 4 MiB. Ends with an sfence: the stores are weakly
-// ordered, and the caller signals completion to the thread that enqueues the DMA.
-__attribute__((target("avx2"))) void copy_nt_avx2(void *dst, const void *src, size_t n) {
-    char *d = static_cast<char *>(dst);
-    const char *s = static_cast<const char *>(src);
-    const size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
-    if (head) {
-        const size_t h = head < n ? head : n;
-        std::memcpy(d, s, h);
-        d += h;
-        s += h;
-        n -= h;
-    }
-    typedef long long v4i __attribute__((vector_size(32)));
-    for (; n >= 128; n -= 128, d += 128, s += 128) {
-        v4i v[4];
-        __builtin_memcpy(v, s, 128);  // unaligned loads
-#pragma unroll
-        for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], reinterpret_cast<v4i *>(d) + k);
-    }
-    if (n) std::memcpy(d, s, n);
-    __builtin_ia32_sfence();
-}
-
-bool cpu_has_avx2() {
-    static const bool v = __builtin_cpu_supports("avx2");
-    return v;
-}
-
-// config "host_copy_nt": 1 = pieces of at least 4 KiB with non-temporal stores (where AVX2 runs)
-void copy_piece(void *dst, const void *src, size_t n, bool nt) {
-    if (nt && n >= 4096) copy_nt_avx2(dst, src, n);
-    else std::memcpy(dst, src, n);
-}
-}  // namespace
-
 void CopyPool::run(const std::vector<Piece> &pieces) {
     size_t total = 0;
     for (const Piece &p : pieces) total += p.bytes;
     const size_t T = threads_.size() + 1;
-    const bool nt = config().host_copy_nt.load() != 0 && cpu_has_avx2();
     if (threads_.empty() || total < (2u << 20)) {
-        for (const Piece &p : pieces) copy_piece(p.dst, p.src, p.bytes, nt);
+        for (const Piece &p : pieces) std::memcpy(p.dst, p.src, p.bytes);
         return;
     }
     // T shares of about total / T bytes each, pieces cut where a share ends
@@ -366,8 +325,8 @@ void CopyPool::run(const std::vector<Piece> &pieces) {
     }
     std::vector<std::function<void()>> tasks;
     for (auto &sh : shares)
-        tasks.push_back([work = std::move(sh), nt] {
-            for (const Piece &p : work) copy_piece(p.dst, p.src, p.bytes, nt);
+        tasks.push_back([work = std::move(sh)] {
+            for (const Piece &p : work) std::memcpy(p.dst, p.src, p.bytes);
         });
     submit_and_wait_(tasks);
 }
