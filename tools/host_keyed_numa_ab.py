@@ -32,4 +32,5 @@ for rep in range(3):
         r = bench.keyed_host_c5(lib, comm, steps=3)
         os.sched_setaffinity(0, allowed)
         print(json.dumps({'rep': rep, 'bind': bind, 'ms': r['ms'], 'pack_ms': r['engine_thread']['pack_ms'],
-                          'unpack_ms': r['engine_thread']['unpack_ms'], 'warm': r['warmup_steps_ms']}), flush=True)
+                          'unpack_ms': r['engine_thread']['unpack_ms'], 'warm': r['warmup_steps_ms'],
+                          'cgroup': r['cgroup_cpu']}), flush=True)
