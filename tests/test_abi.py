@@ -190,3 +190,47 @@ def test_host_chunk_cuts(lib, chunk):
     assert _host_cuts(lib, 256 << 20, 32 << 20) == [k * (32 << 20) for k in range(9)]
     assert lib.ddl_testing_host_chunk_cuts(ctypes.c_size_t(1024), ctypes.c_size_t(100), None, ctypes.c_size_t(0),
                                            ctypes.byref(ctypes.c_size_t())) != 0
+
+
+def test_host_tensor_finalizer_unregisters_its_range(lib, monkeypatch):
+    """The torch mirror's side of the registration cache contract (ddl_host_unregister):
+    with host_register_cache_bytes > 0 every host tensor a keyed request uses gets a finalizer that
+    hands its storage range to ddl_host_unregister when the tensor is collected — before its memory
+    can be reused at the same address; with the cache off nothing is watched. CPU only: the calls
+    are recorded through a wrapper of the library (no communicator is needed for a no-op)."""
+    import gc
+
+    import torch
+
+    from ddl.torch import tensor_communicate as tc
+    from ddl.torch.cpp_backend import CPPBackend
+    assert lib.ddl_host_unregister(None, 0) == 0  # no handler, nothing cached: a no-op
+    calls = []
+
+    class Recording:
+        def __getattr__(self, name):
+            return getattr(lib, name)
+
+        def ddl_host_unregister(self, ptr, nbytes):
+            calls.append((ptr, nbytes))
+            return lib.ddl_host_unregister(ptr, nbytes)
+    monkeypatch.setattr(CPPBackend, 'c_api', staticmethod(lambda: Recording()))
+    old = lib.ddl_get_config(b'host_register_cache_bytes')
+    try:
+        assert lib.ddl_set_config(b'host_register_cache_bytes', 0) == 0
+        t = torch.zeros(1 << 16)
+        tc._watch_host([t])
+        assert id(t) not in tc._watched  # cache off: not watched
+        assert lib.ddl_set_config(b'host_register_cache_bytes', 1 << 30) == 0
+        a, b = torch.zeros(1 << 16), torch.ones(3, 5)
+        view = b[1:]  # a view: its whole storage is the range
+        tc._watch_host([a, view, a])  # twice the same tensor: one finalizer
+        assert id(a) in tc._watched and id(view) in tc._watched
+        want = {(a.untyped_storage().data_ptr(), a.untyped_storage().nbytes()),
+                (b.untyped_storage().data_ptr(), b.untyped_storage().nbytes())}
+        del a, view
+        gc.collect()
+        assert set(calls) == want and len(calls) == 2, calls
+        assert not tc._watched  # the finalizers removed their entries
+    finally:
+        lib.ddl_set_config(b'host_register_cache_bytes', old)
