@@ -367,11 +367,13 @@ int ddl_set_config(const char *key, long long value) {
         else if (k == "pipeline_rounds") c.pipeline_rounds = value ? 1 : 0;
         else if (k == "reference_order") c.reference_order = value ? 1 : 0;
         else if (k == "capture_mode") {
-            DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT,
-                        "capture_mode must be 0 (serial), 1 (forked streams) or 2 (single-stream DAG)");
+            DDL_REQUIRE(value != 1, DDL_STATUS_INVALID_ARGUMENT,
+                        "capture_mode 1 (forked streams) was removed in r04: HIP 7.0's hipStreamEndCapture crashes "
+                        "on three or more cross-waiting forked streams (DESIGN §9); 2 keeps the overlap");
+            DDL_REQUIRE(value == 0 || value == 2, DDL_STATUS_INVALID_ARGUMENT,
+                        "capture_mode must be 0 (serial) or 2 (single-stream DAG)");
             c.capture_mode = value;
-        } else if (k == "capture_forked") c.capture_mode = value ? 1 : 0;
-        else if (k == "compute_cu_mask") {
+        } else if (k == "compute_cu_mask") {
             DDL_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, DDL_STATUS_INVALID_ARGUMENT,
                         "compute_cu_mask must be 0 (all CUs), 2, 4 or 8 (every n-th CU left to RCCL)");
             c.compute_cu_mask = value;
@@ -422,7 +424,6 @@ long long ddl_get_config(const char *key) {
     if (k == "capture_mode") return c.capture_mode;
     if (k == "fold_form") return get_fold_form();
     if (k == "compute_cu_mask") return c.compute_cu_mask;
-    if (k == "capture_forked") return c.capture_mode.load() == 1 ? 1 : 0;
     return -1;
 }
 

@@ -164,12 +164,6 @@ int get_fold_form();
 // variant < 0 selects default_variant().
 void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant = -1);
 int device_cu_count();
-// One empty kernel node on `stream`. Inside a hipGraph capture every stream the engine forks gets
-// one before it records any event: the HIP runtime (7.0 / 7.2) segfaults in hipStreamEndCapture
-// when a stream waits on an event that was recorded on a forked stream while that stream had no
-// captured node yet, once that stream has captured nodes since (tools/capture_replay.hip bisected
-// the engine's own program to that wait; profiles/r03/graph/).
-void launch_capture_anchor(hipStream_t stream);
 
 // Chunk boundaries [cut[i], cut[i + 1]) of a host-staged transfer of `total` bytes through
 // `chunk`-byte slots (chunk a multiple of 256): whole chunks, the last one short. They depend

@@ -99,14 +99,13 @@ struct Config {
     // one-shot folds in MPICH's order, the ring replaced by the direct schedule at P > 2
     // (RingConfig::ref_order); 0: ring order / left folds (error-bounded against the reference)
     std::atomic<long long> reference_order{1};
-    // how a program is posted inside a hipGraph capture: 0 (default) — serially on
-    // the captured stream: one dependency chain, which HIP 7.0's graph executor replays fastest
+    // how a program is posted inside a hipGraph capture: 0 (default) — serially on the
+    // captured stream: one dependency chain, which HIP 7.0's graph executor replays fastest
     // (1.7-3x faster than the DAG below in profiles/r03/graph/capture_overlap_*); 2 — as a
     // single-stream DAG: every op on the captured stream with its dependencies set explicitly
     // from its logical stream (comm / compute of each rank), so the graph keeps the recv / reduce /
-    // send overlap without forked streams; 1 — forked onto the comm / compute streams as eagerly
-    // (crashes hipStreamEndCapture in this HIP runtime once 3+ forked streams cross-wait). Config
-    // key "capture_forked" (1 / 0) is the r02/r03 spelling of modes 1 / 0.
+    // send overlap without forked streams. (r03's mode 1, the forked streams as eagerly, crashed
+    // hipStreamEndCapture in this HIP runtime and was removed in r04.)
     std::atomic<long long> capture_mode{0};
     // multi-rank executors' compute streams (the reduce / fold kernels that overlap RCCL's send /
     // recv kernels) run on all CUs but every n-th (n = 2, 4, 8; 0 = all CUs, the default): those

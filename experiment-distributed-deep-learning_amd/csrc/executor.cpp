@@ -337,7 +337,7 @@ void RingExecutor::allgatherv(const void *send, void *recv, const size_t *counts
 Poster::Mode Poster::mode_for(hipStream_t user) {
     if (!stream_capturing(user)) return kStreams;
     const int m = config_capture_mode();
-    return m == 0 ? kSerial : m == 1 ? kStreams : kDag;
+    return m == 0 ? kSerial : kDag;
 }
 
 Poster::Poster(Mode m, hipStream_t user) : m_(m), user_(user) {
@@ -406,8 +406,8 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     DDL_TRACE("executor rank " << rank_ << "/" << size_ << " run: " << prog_.ticks.size() << " ticks, user " << (void *)user);
     // Eagerly the program forks from the caller's stream onto the comm / compute streams and joins
     // back. Inside a graph capture the Poster turns the same posting into a serial order on the
-    // captured stream (default), a single-stream DAG or forked streams (config capture_mode;
-    // executor.h).
+    // captured stream (default) or a single-stream DAG (config capture_mode; executor.h,
+    // DESIGN §9).
     const bool capturing = stream_capturing(user);
     DDL_REQUIRE(!capturing || !transport_ || transport_->capturable(), DDL_STATUS_INVALID_ARGUMENT,
                 "this communicator's transport synchronises the host and cannot be captured into a graph");
@@ -418,10 +418,6 @@ void RingExecutor::run_(int dtype, hipStream_t user) {
     p.record(res_.fork_ev, user);
     p.wait(comm, res_.fork_ev);
     p.wait(compute, res_.fork_ev);
-    if (capturing && p.mode() == Poster::kStreams) {  // no event recorded on a forked stream before its first node (common.h)
-        launch_capture_anchor(comm);
-        launch_capture_anchor(compute);
-    }
     const int drop = g_drop_wait_tick.load();
     for (size_t t = 0; t < prog_.ticks.size(); ++t) {
         const Tick &tk = prog_.ticks[t];
@@ -799,8 +795,7 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         loop_ev_.push_back(e);
     }
     // posted through a Poster as RingExecutor::run_ is: real streams eagerly; inside a capture a
-    // single-stream DAG (default), forked streams or the serial order (config capture_mode)
-    const bool capturing = stream_capturing(user);
+    // serial order (default) or a single-stream DAG (config capture_mode)
     Poster p(Poster::mode_for(user), user);
     auto comm = [&](int r) { return res_[r]->comm; };
     auto compute = [&](int r) { return res_[r]->compute; };
@@ -821,13 +816,6 @@ void LocalWorld::run_(int dtype, hipStream_t user) {
         wait(compute(r), fork);
     }
     if (loop_) wait(loop_stream_, fork);
-    if (capturing && p.mode() == Poster::kStreams) {  // no event recorded on a forked stream before its first node
-        for (int r = 0; r < P_; ++r) {
-            launch_capture_anchor(comm(r));
-            launch_capture_anchor(compute(r));
-        }
-        if (loop_) launch_capture_anchor(loop_stream_);
-    }
     for (size_t t = 0; t < T; ++t) {
         // 1) each rank's comm stream reaches the tick (after its reduce dependency)
         for (int r = 0; r < P_; ++r) {

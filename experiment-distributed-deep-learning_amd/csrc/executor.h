@@ -42,7 +42,7 @@ public:
 // warm-up rule as for any captured workload).
 bool stream_capturing(hipStream_t s);
 // Config "capture_mode": how a program is posted inside a capture — 0 serially on the captured
-// stream, 1 on the forked comm / compute streams as eagerly, 2 as a single-stream DAG (Poster).
+// stream, 2 as a single-stream DAG (Poster).
 int config_capture_mode();
 // Config "compute_cu_mask" (0 off, 2 / 4 / 8): the compute streams of multi-rank executors leave
 // every n-th CU to RCCL (read when an executor is created).
@@ -54,7 +54,8 @@ hipStream_t create_compute_stream(int every);
 // Posts a program's ops on its logical streams (each rank's comm / compute stream, a transport
 // stream) with event records and waits between them, in one of three ways:
 //  * kStreams — on the real streams: record / wait are hipEventRecord / hipStreamWaitEvent (eager
-//    calls, and capture_mode 1);
+//    calls; r03's capture_mode 1 posted captures this way too, and HIP 7.0's hipStreamEndCapture
+//    crashed on it — removed in r04);
 //  * kSerial — every op on the caller's stream in posting order, records and waits dropped
 //    (stream order implies every dependency: they all point backwards; capture_mode 0, the
 //    default: the chain replays fastest in HIP 7.0's graph executor);

@@ -116,22 +116,24 @@ __global__ void __launch_bounds__(THREADS) k_seg_tiles(char *flat, const SegDesc
     }
 }
 
+// one 1 KiB tile per 64-lane workgroup (kSegTile): the r01 tile-shape measurement (C5 bucket
+// set, pack / unpack) had 6.10 / 6.37 TB/s for it against 6.09 / 6.29 for 2 KiB tiles of 128 lanes
+// and 5.74 / 6.30 for 4 KiB tiles of 128 lanes x 2 chunks; the span kernel with an in-kernel
+// segment search (2-64 KiB spans) 4.5-6.0
+constexpr uint64_t kSegTile = 1024;
 template <int DIR, bool NARROW>
-void launch_dir(int variant, dim3 g, hipStream_t stream, char *fl, const SegDesc *dd, const uint32_t *db,
-                const void *map) {
-    if (variant == 2) hipLaunchKernelGGL((k_seg_tiles<DIR, 1, 128, NARROW>), g, dim3(128), 0, stream, fl, dd, db, map);
-    else if (variant == 3) hipLaunchKernelGGL((k_seg_tiles<DIR, 2, 128, NARROW>), g, dim3(128), 0, stream, fl, dd, db, map);
-    else hipLaunchKernelGGL((k_seg_tiles<DIR, 1, 64, NARROW>), g, dim3(64), 0, stream, fl, dd, db, map);
+void launch_dir(dim3 g, hipStream_t stream, char *fl, const SegDesc *dd, const uint32_t *db, const void *map) {
+    hipLaunchKernelGGL((k_seg_tiles<DIR, 1, 64, NARROW>), g, dim3(64), 0, stream, fl, dd, db, map);
 }
 
-void launch_tiles(int dir, int variant, bool narrow, dim3 g, hipStream_t stream, char *fl, const SegDesc *dd,
-                  const uint32_t *db, const void *map) {
+void launch_tiles(int dir, bool narrow, dim3 g, hipStream_t stream, char *fl, const SegDesc *dd, const uint32_t *db,
+                  const void *map) {
     if (dir == 0) {
-        if (narrow) launch_dir<0, true>(variant, g, stream, fl, dd, db, map);
-        else launch_dir<0, false>(variant, g, stream, fl, dd, db, map);
+        if (narrow) launch_dir<0, true>(g, stream, fl, dd, db, map);
+        else launch_dir<0, false>(g, stream, fl, dd, db, map);
     } else {
-        if (narrow) launch_dir<1, true>(variant, g, stream, fl, dd, db, map);
-        else launch_dir<1, false>(variant, g, stream, fl, dd, db, map);
+        if (narrow) launch_dir<1, true>(g, stream, fl, dd, db, map);
+        else launch_dir<1, false>(g, stream, fl, dd, db, map);
     }
 }
 
@@ -184,19 +186,8 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     if (count <= 0) return;
     DDL_REQUIRE(flat && segs && bytes, DDL_STATUS_INVALID_ARGUMENT, "null pack arguments");
     Slot &sl = free_slot_();
-    // DDL_PACK_VARIANT (measurement only; tools/pack_tune.py, C5 bucket set, pack / unpack, r01):
-    //   1: segment tiles of 1 KiB, 64 lanes (default)                                     6.10 / 6.37 TB/s
-    //   2: segment tiles of 2 KiB, 128 lanes                                              6.09 / 6.29
-    //   3: segment tiles of 4 KiB, 128 lanes x 2 chunks                                   5.74 / 6.30
-    // (the r01 span kernel — 64 KiB spans with an in-kernel segment search — measured 5.56 / 5.61
-    // and is gone; spans of 2-8 KiB with the search measured 4.5-6.0.)
-    static const int variant = [] {
-        const char *e = std::getenv("DDL_PACK_VARIANT");
-        const int v = e ? std::atoi(e) : 1;
-        return v >= 1 && v <= 3 ? v : 1;
-    }();
-    // segment-aligned tiles (variants 1..3): tile bytes per workgroup; tile0 = running tile count
-    const uint64_t seg_tile = variant == 2 ? 2048 : variant == 3 ? 4096 : 1024;
+    // segment-aligned tiles of kSegTile bytes per workgroup; tile0 = running tile count
+    const uint64_t seg_tile = kSegTile;
     uint64_t tiles = 0;
     for (int i = 0; i < count; ++i) tiles += (bytes[i] + seg_tile - 1) / seg_tile;
     DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "fusion buffer too large");
@@ -227,12 +218,7 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     if (off == 0) return;
     // block b's base: the segment of tile b * 128 (the last one with tile0 <= it, as
     // k_tile_index resolves); narrow when no block spans more than 255 segments
-    // (DDL_PACK_INDEX=32 forces the int32 index, for measurement)
-    static const bool wide_only = [] {
-        const char *e = std::getenv("DDL_PACK_INDEX");
-        return e && std::atoi(e) == 32;
-    }();
-    bool narrow = !wide_only;
+    bool narrow = true;
     for (uint64_t b = 0, s0 = 0, s1 = 0; b < nblk; ++b) {
         const uint64_t first = b * kIdxBlock, last = std::min(tiles, first + kIdxBlock) - 1;
         while (s0 + 1 < (uint64_t)count && t[s0 + 1].tile0 <= first) ++s0;
@@ -256,7 +242,7 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
         const dim3 ig((unsigned)((tiles + 255) / 256)), g((unsigned)tiles);
         if (narrow) hipLaunchKernelGGL(k_tile_index<true>, ig, dim3(256), 0, stream, dd, count, (uint64_t)tiles, db, sl.idx);
         else hipLaunchKernelGGL(k_tile_index<false>, ig, dim3(256), 0, stream, dd, count, (uint64_t)tiles, db, sl.idx);
-        launch_tiles(dir, variant, narrow, g, stream, fl, dd, db, sl.idx);
+        launch_tiles(dir, narrow, g, stream, fl, dd, db, sl.idx);
     }
     DDL_HIP(hipGetLastError());
     DDL_HIP(hipEventRecord(sl.ready, stream));

@@ -239,17 +239,10 @@ __device__ __forceinline__ typename Acc<DT>::T fold_values(typename Acc<DT>::T *
     }
 }
 
-// Lanes per workgroup (one tile of THREADS x 16 B) of the two-input reduce (DDL_REDUCE_THREADS:
-// 64, 128 or 256; measurement). Default 128 (2 KiB tiles): 6.72-6.77 TB/s vs 6.37-6.55 with
-// 256 lanes on the N=1 bench (256 MiB fp32, 3 rotating sets, interleaved rounds).
-int reduce_threads() {
-    static const int v = [] {
-        const char *e = std::getenv("DDL_REDUCE_THREADS");
-        const int t = e ? std::atoi(e) : 128;
-        return t == 64 || t == 256 ? t : 128;
-    }();
-    return v;
-}
+// Lanes per workgroup (one tile of kReduceThreads x 16 B) of the two-input reduce: 128 (2 KiB
+// tiles) measured 6.72-6.77 TB/s vs 6.37-6.55 with 256 lanes on the N=1 bench (256 MiB fp32, 3
+// rotating sets, interleaved rounds); 64 lanes were slower too.
+constexpr int kReduceThreads = 128;
 
 // Fold cache policy (FV bits): 1 non-temporal loads, 2 non-temporal store, 4 write-through
 // (sc0 sc1) store. Chunks above 8 MiB stream every input once: non-temporal loads, and the output
@@ -257,15 +250,7 @@ int reduce_threads() {
 // 6.48-6.51 TB/s vs 6.35-6.36 all-nt, the r02 policy). Chunks up to 8 MiB (their operands fit the
 // 256 MiB Infinity Cache, where RCCL has just written the received slices) read through the
 // caches: 5.53 vs 5.05 TB/s at 4 MiB (plain loads + write-through store vs all-nt).
-// DDL_FOLD_VARIANT (0..7) forces one policy for measurement (4 or 5; anything else maps to 5).
-int fold_variant(size_t chunk_bytes) {
-    static const int forced = [] {
-        const char *e = std::getenv("DDL_FOLD_VARIANT");
-        return e ? std::atoi(e) & 7 : -1;
-    }();
-    if (forced >= 0) return forced == 4 ? 4 : 5;
-    return chunk_bytes <= (8u << 20) ? 4 : 5;
-}
+int fold_variant(size_t chunk_bytes) { return chunk_bytes <= (8u << 20) ? 4 : 5; }
 
 // One 2 KiB tile of the output per 128-lane workgroup: each lane folds its 16 bytes across a
 // and the nb received inputs, one buffer_load_dwordx4 per input through one descriptor per input
@@ -578,11 +563,7 @@ void launch_variant(const SegTable &t, hipStream_t stream, int variant, dim3 gri
         fail(DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant");
     } else {
         if (variant == V) {
-            switch (reduce_threads()) {
-                case 64: hipLaunchKernelGGL((k_sum2_tile<DT, V, 64>), grid, dim3(64), 0, stream, t); break;
-                case 256: hipLaunchKernelGGL((k_sum2_tile<DT, V, 256>), grid, dim3(256), 0, stream, t); break;
-                default: hipLaunchKernelGGL((k_sum2_tile<DT, V, 128>), grid, dim3(128), 0, stream, t);
-            }
+            hipLaunchKernelGGL((k_sum2_tile<DT, V, kReduceThreads>), grid, dim3(kReduceThreads), 0, stream, t);
         } else {
             launch_variant<DT, V + 1>(t, stream, variant, grid);
         }
@@ -599,7 +580,7 @@ void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned,
         return;
     }
     constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
-    const uint64_t tv = (uint64_t)reduce_threads();
+    constexpr uint64_t tv = kReduceThreads;
     const uint64_t tiles = (max_n / V + tv) / tv;  // +1 vector of room for the tail
     DDL_REQUIRE(tiles < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << max_n << " elements");
     launch_variant<DT, 0>(t, stream, variant, dim3((unsigned)tiles, t.count));
@@ -613,14 +594,6 @@ int g_cu_count = 0;
 
 void set_fold_form(int form) { g_fold_form.store(form, std::memory_order_relaxed); }
 int get_fold_form() { return g_fold_form.load(std::memory_order_relaxed); }
-
-// An empty node (one wavefront, no memory access) for graph captures: see launch_capture_anchor.
-__global__ void k_capture_anchor() {}
-
-void launch_capture_anchor(hipStream_t stream) {
-    hipLaunchKernelGGL(k_capture_anchor, dim3(1), dim3(64), 0, stream);
-    DDL_HIP(hipGetLastError());
-}
 
 int device_cu_count() {
     if (g_cu_count == 0) {
@@ -706,12 +679,6 @@ void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) { launch_sum
 //     TB/s plain stores).
 constexpr size_t kNtMinBytes = 32u << 20, kNtStoreMinBytes = 256u << 20;
 int default_variant(size_t bytes) {
-    static int v = [] {
-        const char *e = std::getenv("DDL_REDUCE_VARIANT");
-        const int x = e ? std::atoi(e) : -1;
-        return (x >= 0 && x <= kVariantMask) ? x : -1;
-    }();
-    if (v >= 0) return v;
     if (bytes >= kNtStoreMinBytes) return kNtLoadA | kNtLoadB | kNtStore;
     if (bytes >= kNtMinBytes) return kNtLoadA | kNtLoadB | kWtStore;
     return kWtStore;
@@ -720,15 +687,7 @@ int default_variant(size_t bytes) {
 // Ring reduce-scatter step: a = the rank's own gradient (read once: non-temporal), b = the slice
 // RCCL just received (likely still in the Infinity Cache: plain), out = forwarded by the next
 // step's send (keep it cache-resident: plain store).
-int ring_variant() {
-    static int v = [] {
-        const char *e = std::getenv("DDL_RING_REDUCE_VARIANT");
-        const int dflt = kNtLoadA;
-        int x = e ? std::atoi(e) : dflt;
-        return (x >= 0 && x <= kVariantMask) ? x : dflt;
-    }();
-    return v;
-}
+int ring_variant() { return kNtLoadA; }
 
 void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) {
     DDL_REQUIRE(t.count >= 1 && t.count <= kMaxSegments, DDL_STATUS_INVALID_ARGUMENT,

@@ -139,8 +139,9 @@ int ddl_is_initialized(void);
  * copy threads while the next chunks are packed), "capture_mode" (0, default: inside a
  * hipGraph capture the program is posted serially on the captured stream — one chain; 2: as a
  * single-stream DAG, every op on the captured stream with its dependencies set explicitly, which
- * keeps the recv / reduce / send overlap in the graph; 1: on the forked comm / compute streams —
- * DESIGN §9; "capture_forked" 1 / 0 is the older spelling of modes 1 / 0), "compute_cu_mask" (0,
+ * keeps the recv / reduce / send overlap in the graph; r03's 1, the forked comm / compute
+ * streams, crashed HIP 7.0's hipStreamEndCapture and is refused since r04 — DESIGN §9; so is its
+ * older key "capture_forked"), "compute_cu_mask" (0,
  * default: all CUs; 8 / 4 / 2: the compute streams of multi-rank executors and handlers — the
  * reduce / fold / pack kernels that overlap RCCL's send / recv kernels — avoid every 8th / 4th /
  * 2nd CU, which stay free for RCCL; each masked stream takes a hardware queue of its own; read

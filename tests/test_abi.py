@@ -106,14 +106,15 @@ def test_config_roundtrip(lib):
     assert lib.ddl_get_config(b'reference_order') == 1
     # keyed rounds pipelined by default (done() fired by the completion thread)
     assert lib.ddl_get_config(b'pipeline_rounds') == 1
-    # captures post serially by default (2: single-stream DAG); capture_forked spells modes 1 / 0
+    # captures post serially by default (2: single-stream DAG); r03's forked mode 1 and its
+    # capture_forked key are refused since r04 (the HIP runtime crashed on them)
     assert lib.ddl_get_config(b'capture_mode') == 0
-    assert lib.ddl_get_config(b'capture_forked') == 0
     assert lib.ddl_set_config(b'capture_mode', 3) == 3
-    assert lib.ddl_set_config(b'capture_forked', 1) == 0
-    assert lib.ddl_get_config(b'capture_mode') == 1 and lib.ddl_get_config(b'capture_forked') == 1
-    assert lib.ddl_set_config(b'capture_forked', 0) == 0
-    assert lib.ddl_get_config(b'capture_mode') == 0
+    assert lib.ddl_set_config(b'capture_mode', 1) == 3 and b'removed' in lib.ddl_last_error()
+    assert lib.ddl_set_config(b'capture_forked', 1) == 3
+    assert lib.ddl_get_config(b'capture_forked') == -1
+    assert lib.ddl_set_config(b'capture_mode', 2) == 0 and lib.ddl_get_config(b'capture_mode') == 2
+    assert lib.ddl_set_config(b'capture_mode', 0) == 0
     # multi-rank compute streams on every CU by default (8 / 4 / 2: leave every n-th to RCCL)
     assert lib.ddl_get_config(b'compute_cu_mask') == 0
     assert lib.ddl_set_config(b'compute_cu_mask', 3) == 3

@@ -6,8 +6,8 @@
   fold    — one N-input fold kernel launch (single stream)
   ring2   — local world P = 2, ring schedule (two-input reduce kernels, no fold)
   rawlocal— `local` captured with hipStreamBeginCapture through ctypes (no torch graph)
-    python graph_probe.py <mode> [algo] [forked: 1 = config capture_forked, the program on its
-    forked comm / compute streams inside the capture; 0 = posted serially]
+    python graph_probe.py <mode> [algo] [capture_mode: 0 = posted serially (default), 2 = as a
+    single-stream DAG; r03's forked mode 1 was removed in r04]
 Prints one line per stage; a crash names the last stage reached."""
 import ctypes
 import os
@@ -24,11 +24,11 @@ def say(*a):
     print(*a, flush=True)
 
 
-def main(mode, P=3, n=300, algo=1, forked=0):
+def main(mode, P=3, n=300, algo=1, capture_mode=0):
     lib = CPPBackend.c_api()
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
-    lib.ddl_set_config(b'capture_forked', forked)
+    lib.ddl_set_config(b'capture_mode', capture_mode)
     lib.ddl_set_config(b'tune', 0)
     lib.ddl_set_config(b'algo', algo)
     lib.ddl_set_config(b'slice_bytes', 64 << 10)
@@ -128,7 +128,7 @@ def raw_capture(lib, s, P, send, recv, n, outs):
 if __name__ == '__main__':
     m = sys.argv[1]
     algo = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    forked = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    capture_mode = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     if m == 'group':  # the one-shot schedule: one group of self pairs, one fold
         algo = 2
-    main(m, algo=algo, forked=forked)
+    main(m, algo=algo, capture_mode=capture_mode)
