@@ -14,8 +14,9 @@ import ctypes
 
 import pytest
 
+import test_batch_gpu as tb
 import test_thread_world_gpu as tw
-from _helpers import DT_DOUBLE, DT_FLOAT, DT_INT32, NAME
+from _helpers import DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME
 
 pytestmark = pytest.mark.gpu
 
@@ -86,3 +87,11 @@ def test_rccl_threads_repeated_calls(lib, oracle, gpu, through_rccl):
 @pytest.mark.parametrize('algo,ref', [(0, 0), (1, 1), (4, 1)])
 def test_rccl_threads_posted_dependencies_have_no_race(lib, gpu, through_rccl, P, algo, ref):
     tw.test_posted_dependencies_have_no_race(lib, gpu, P, algo, ref)
+
+
+@pytest.mark.parametrize('P', [3, 8])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_HALF], ids=lambda d: NAME[d])
+def test_rccl_threads_grouped_allreduce(lib, oracle, gpu, through_rccl, P, dt):
+    """The grouped allreduce (RingExecutor::allreduce_batch: one group per tick for every bucket,
+    batched folds) with its pairs through RCCL: every bucket bit for bit its own MPICH order."""
+    tb.test_thread_batch_bit_exact_per_bucket(lib, oracle, gpu, P, 1, dt)
