@@ -558,7 +558,17 @@ def check_control_link_lost(ctx):
     assert st != 0 and 'handler stopped' in msg, (st, msg)
 
 
-FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost}
+def check_resources(ctx):
+    """Diagnostic for soak runs (tools/soak_mp.py): this rank's threads and open fds on stderr, so
+    a leak across repeated checks shows as growth."""
+    r = ctx['rank']
+    threads = len(os.listdir('/proc/self/task'))
+    fds = len(os.listdir('/proc/self/fd'))
+    sys.stderr.write(f'[rank {r}] threads {threads} fds {fds}\n')
+    sys.stderr.flush()
+
+
+FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resources': check_resources}
 
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,
@@ -603,7 +613,11 @@ def worker(rank, world, port, q, only=None):
         ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
                'oracle': h.Oracle()}
         import time
-        for fn in ([FAULT_CHECKS[n] for n in only] if only else CHECKS):
+        if os.environ.get('DDL_MP_STACKS_S'):  # soak diagnostics: Python stacks of a hung rank
+            import faulthandler
+            faulthandler.dump_traceback_later(float(os.environ['DDL_MP_STACKS_S']), repeat=True)
+        by_name = {**{f.__name__: f for f in CHECKS}, **FAULT_CHECKS}  # `only`: any checks by name, in order
+        for fn in ([by_name[n] for n in only] if only else CHECKS):
             try:
                 t0 = time.perf_counter()
                 fn(ctx)
