@@ -184,7 +184,7 @@ private:
     std::unique_ptr<RcclTransport> loop_;  // see the constructor
     std::mutex loop_mu_;                   // one thread at a time inside an RCCL group
 public:
-    long long loopback_pairs = 0;          // pairs moved through RCCL (under loop_mu_)
+    std::atomic<long long> loopback_pairs{0};  // pairs moved through RCCL
 };
 
 class ThreadTransport : public Transport {
