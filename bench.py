@@ -646,7 +646,7 @@ def keyed_c1_latency(lib, comm, dev, reps=200):
             'path': 'keyed submit -> star negotiation -> allreduce in place on the tensor -> done'}
 
 
-def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
+def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None, warm_steps=6):
     """C5's bucket set as HOST tensors (the reference's deployment: CPU tensors behind the MPI
     buffers) through the keyed path: negotiation, dtype groups, plans, then per plan in chunks
     through pinned slots: host pack -> H2D -> allreduce -> D2H -> host unpack; with pinned tensors
@@ -683,9 +683,11 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None):
         def step():
             check(lib.ddl_allreduce_submit_batch_mem(comm.id, *args), 'ddl_allreduce_submit_batch_mem')
             check(lib.ddl_wait_all(comm.id), 'ddl_wait_all')
-        warm = []  # warm-up by time as host_resident_rate (freshly pinned tensors), each step timed
-        t_alloc = time.perf_counter()
-        while not warm or (time.perf_counter() - t_alloc < 0.5 and len(warm) < 8):
+        # warm-up steps, each timed (freshly pinned tensors read slowly for a while on some boxes,
+        # DESIGN §7). A FIXED count: every step is a collective, so every rank must run the same
+        # number — a time-based loop could leave one rank a step ahead and hang the others
+        warm = []
+        for _ in range(max(1, warm_steps)):
             t1 = time.perf_counter()
             step()
             warm.append(round((time.perf_counter() - t1) * 1e3, 2))
@@ -761,7 +763,7 @@ def cgroup_cpu():
         return None
 
 
-def host_resident_rate(lib, comm, S, reps):
+def host_resident_rate(lib, comm, S, reps, warm_calls=60):
     """Deployment case: the bucket starts and ends in (pinned) host memory; ddl_allreduce_host
     pipelines H2D -> device ring -> D2H in 32 MiB chunks. PCIe-inclusive rate, never `value`."""
     import torch
@@ -769,13 +771,12 @@ def host_resident_rate(lib, comm, S, reps):
     n = S // 4
     src = torch.rand(n, pin_memory=True)
     dst = torch.empty(n, pin_memory=True)
-    # warm-up by time, each call timed: DMA over freshly pinned buffers reads ~1.6x slower for the
-    # first ~0.1-0.2 s after a long run of device kernels on some boxes (r04 s2: 10.2 ms per call
-    # for a whole first round, 6.2 ms from the next one on) — the steady rate is the
-    # one a training loop sees, the first calls are reported beside it
+    # warm-up calls, each timed: the pipeline's H2D and D2H ran serialized for its first tens of
+    # calls late in the bench (r04 s2: 10.2 ms per call, then 6.2 ms) — the steady rate
+    # is the one a training loop sees, the first calls are reported beside it. A FIXED count:
+    # ddl_allreduce_host is a collective, so every rank must make the same number of calls
     warm = []
-    t_alloc = time.perf_counter()
-    while len(warm) < 2 or (time.perf_counter() - t_alloc < 0.5 and len(warm) < 60):
+    for _ in range(max(1, warm_calls)):
         t1 = time.perf_counter()
         check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
         warm.append(round((time.perf_counter() - t1) * 1e3, 3))
@@ -784,7 +785,7 @@ def host_resident_rate(lib, comm, S, reps):
         check(lib.ddl_allreduce_host(comm.id, src.data_ptr(), dst.data_ptr(), n, DT_FLOAT, 0), 'ddl_allreduce_host')
     dt = (time.perf_counter() - t0) / reps
     return {'bucket_GiBs': round(S / GiB / dt, 2), 'ms': round(dt * 1e3, 3), 'bucket_bytes': S,
-            'warmup_calls_ms': warm[:12], 'warmup_calls': len(warm),
+            'warmup_calls_ms': warm[:12], 'warmup_last_ms': warm[-3:], 'warmup_calls': len(warm),
             'path': 'pinned host -> H2D -> ring allreduce -> D2H -> pinned host, 32 MiB chunks on 3 streams',
             'pcie_bytes_per_bucket': 2 * S}
 
@@ -1085,7 +1086,7 @@ def multi_gpu(args):
     state['leg'] = 'host_resident'
     try:
         if not args.no_host:
-            out['host_resident'] = host_resident_rate(lib, comm, S, reps=4)
+            out['host_resident'] = host_resident_rate(lib, comm, S, reps=4, warm_calls=1 if args.rehearse else 20)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['host_resident'] = repr(e)[:400]
     state['leg'] = 'fusion_c5'
@@ -1110,7 +1111,8 @@ def multi_gpu(args):
     state['leg'] = 'keyed_host_c5_pinned'
     try:
         if not args.no_fusion and not args.no_host:
-            out['keyed_host_c5_pinned'] = keyed_host_c5(lib, comm, steps=2, pinned=True)
+            out['keyed_host_c5_pinned'] = keyed_host_c5(lib, comm, steps=2, pinned=True,
+                                                        warm_steps=1 if args.rehearse else 3)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['keyed_host_c5_pinned'] = repr(e)[:400]
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per
