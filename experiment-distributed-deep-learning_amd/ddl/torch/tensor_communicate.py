@@ -11,6 +11,7 @@ Device tensors stay in HBM; the call is ordered on torch's current stream and do
 synchronise the host. A host (CPU) tensor — the reference's deployment case — is staged
 through pinned memory to the GPU, reduced there and copied back.
 """
+import bisect
 import ctypes
 import itertools
 import threading
@@ -191,35 +192,87 @@ def _on_done(status, user):
         h._event.set()
 
 
-_watched = {}  # id(host tensor) -> its finalizer (see _watch_host)
+# Host ranges the engine's registration cache may hold, as the torch mirror submitted them (see
+# _watch_host): start address -> (end, id of the storage object, its finalizer); _watched_starts
+# keeps the starts sorted for the overlap lookup.
+_watched = {}
+_watched_starts = []
+_watched_by_storage = {}  # id of the storage object -> the start it was recorded at
 _watched_lock = threading.Lock()
 
 
-def _unregister_host(key, ptr, nbytes):
-    with _watched_lock:
-        _watched.pop(key, None)
+def _release_range(lo, hi):
     try:
-        CPPBackend.c_api().ddl_host_unregister(ptr, nbytes)
+        CPPBackend.c_api().ddl_host_unregister(lo, hi - lo)
     except Exception:  # noqa: BLE001 (interpreter shutdown: the library may be gone)
         pass
 
 
+def _forget_locked(lo):
+    entry = _watched.pop(lo, None)
+    if entry is not None:
+        _watched_starts.pop(bisect.bisect_left(_watched_starts, lo))
+        if _watched_by_storage.get(entry[1]) == lo:
+            del _watched_by_storage[entry[1]]
+    return entry
+
+
+def _on_storage_freed(lo, key):
+    """Finalizer of a watched storage: its memory is about to be released."""
+    with _watched_lock:
+        entry = _watched.get(lo)
+        if entry is None or entry[1] != key:
+            return
+        _forget_locked(lo)
+    _release_range(lo, entry[0])
+
+
 def _watch_host(tensors):
-    """With the engine's host registration cache on (config host_register_cache_bytes > 0), every
-    host tensor a keyed request uses may stay registered after the request. Before such a tensor's
-    memory is freed its storage range must leave the cache (ddl_host_unregister): a later tensor at
-    the same address would otherwise be taken for the old, unmapped pages. A finalizer per tensor
-    object does that when the tensor is collected."""
+    """With the engine's host registration cache on (config host_register_cache_bytes > 0), the
+    host memory of a keyed request may stay registered after the request. A registered range
+    must leave the cache before its memory is freed, or a later tensor placed at the same address
+    is taken for the old, unmapped pages (a device access through it faults; ADVICE r3, DESIGN
+    §7). For every host tensor submitted while the cache is on:
+      * a finalizer on its STORAGE object (torch keeps one Python object per live storage) hands
+        the range to ddl_host_unregister when the storage dies — after its last view;
+      * a recorded range that the tensor's storage now overlaps but does not match — the memory
+        of a storage that was resized / re-set in place, or a range reused by a new storage — is
+        unregistered before this submission can hit it in the cache."""
     lib = CPPBackend.c_api()
     if lib.ddl_get_config(b'host_register_cache_bytes') <= 0:
         return
     for t in tensors:
-        if t.is_cuda or id(t) in _watched:
+        if t.is_cuda:
             continue
         st = t.untyped_storage()
+        lo, nbytes = st.data_ptr(), st.nbytes()
+        if not lo or not nbytes:
+            continue
+        hi, key = lo + nbytes, id(st)
+        stale = []
         with _watched_lock:
-            if id(t) not in _watched:
-                _watched[id(t)] = weakref.finalize(t, _unregister_host, id(t), st.data_ptr(), st.nbytes())
+            prev = _watched_by_storage.get(key)
+            if prev is not None and prev != lo:  # this storage's memory moved (resize_ / set_)
+                end, _, fin = _forget_locked(prev)
+                fin.detach()
+                stale.append((prev, end))
+            i = max(0, bisect.bisect_right(_watched_starts, lo) - 1)
+            while i < len(_watched_starts) and _watched_starts[i] < hi:
+                start = _watched_starts[i]
+                end, k, fin = _watched[start]
+                if end > lo and (start, end, k) != (lo, hi, key):
+                    _forget_locked(start)
+                    fin.detach()
+                    stale.append((start, end))
+                    continue
+                i += 1
+            if lo not in _watched:
+                fin = weakref.finalize(st, _on_storage_freed, lo, key)
+                _watched[lo] = (hi, key, fin)
+                _watched_by_storage[key] = lo
+                bisect.insort(_watched_starts, lo)
+        for a, b in stale:
+            _release_range(a, b)
 
 
 def _same_memory(a: torch.Tensor, b: torch.Tensor, what: str) -> int:

@@ -195,10 +195,12 @@ def test_host_chunk_cuts(lib, chunk):
 
 def test_host_tensor_finalizer_unregisters_its_range(lib, monkeypatch):
     """The torch mirror's side of the registration cache contract (ddl_host_unregister):
-    with host_register_cache_bytes > 0 every host tensor a keyed request uses gets a finalizer that
-    hands its storage range to ddl_host_unregister when the tensor is collected — before its memory
-    can be reused at the same address; with the cache off nothing is watched. CPU only: the calls
-    are recorded through a wrapper of the library (no communicator is needed for a no-op)."""
+    with host_register_cache_bytes > 0 every host tensor a keyed request uses gets a finalizer on
+    its STORAGE that hands the storage's range to ddl_host_unregister when the storage dies (after
+    its last view, not before); a storage resized in place (its memory moved) has its old range
+    released at its next submission, and so has a recorded range that a new storage now overlaps.
+    With the cache off nothing is watched. CPU only: the calls are recorded through a wrapper of
+    the library (no communicator is needed for a no-op)."""
     import gc
 
     import torch
@@ -217,21 +219,40 @@ def test_host_tensor_finalizer_unregisters_its_range(lib, monkeypatch):
             return lib.ddl_host_unregister(ptr, nbytes)
     monkeypatch.setattr(CPPBackend, 'c_api', staticmethod(lambda: Recording()))
     old = lib.ddl_get_config(b'host_register_cache_bytes')
+
+    def rng(t):
+        st = t.untyped_storage()
+        return st.data_ptr(), st.nbytes()
     try:
         assert lib.ddl_set_config(b'host_register_cache_bytes', 0) == 0
         t = torch.zeros(1 << 16)
         tc._watch_host([t])
-        assert id(t) not in tc._watched  # cache off: not watched
+        assert not tc._watched  # cache off: not watched
         assert lib.ddl_set_config(b'host_register_cache_bytes', 1 << 30) == 0
         a, b = torch.zeros(1 << 16), torch.ones(3, 5)
-        view = b[1:]  # a view: its whole storage is the range
-        tc._watch_host([a, view, a])  # twice the same tensor: one finalizer
-        assert id(a) in tc._watched and id(view) in tc._watched
-        want = {(a.untyped_storage().data_ptr(), a.untyped_storage().nbytes()),
-                (b.untyped_storage().data_ptr(), b.untyped_storage().nbytes())}
+        ra, rb = rng(a), rng(b)
+        view = b[1:]  # a view: its storage is b's
+        tc._watch_host([a, view, a])  # the same storage twice: one entry
+        assert set(tc._watched) == {ra[0], rb[0]}
         del a, view
         gc.collect()
-        assert set(calls) == want and len(calls) == 2, calls
-        assert not tc._watched  # the finalizers removed their entries
+        assert calls == [ra], calls  # a's storage died; b's lives on
+        del b
+        gc.collect()
+        assert calls == [ra, rb], calls
+        assert not tc._watched
+        # a storage resized in place: its old memory is released at its next submission
+        c = torch.zeros(1 << 10)
+        tc._watch_host([c])
+        rc_old = rng(c)
+        c.resize_(1 << 20)
+        assert rng(c)[0] != rc_old[0]
+        calls.clear()
+        tc._watch_host([c])
+        assert calls == [rc_old], calls
+        assert set(tc._watched) == {rng(c)[0]}
+        del c
+        gc.collect()
+        assert not tc._watched
     finally:
         lib.ddl_set_config(b'host_register_cache_bytes', old)
