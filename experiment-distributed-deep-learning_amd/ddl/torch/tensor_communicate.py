@@ -241,16 +241,19 @@ def _watch_host(tensors):
     lib = CPPBackend.c_api()
     if lib.ddl_get_config(b'host_register_cache_bytes') <= 0:
         return
-    for t in tensors:
-        if t.is_cuda:
-            continue
-        st = t.untyped_storage()
-        lo, nbytes = st.data_ptr(), st.nbytes()
-        if not lo or not nbytes:
-            continue
-        hi, key = lo + nbytes, id(st)
-        stale = []
-        with _watched_lock:
+    stale = []
+    with _watched_lock:
+        for t in tensors:
+            if t.is_cuda:
+                continue
+            st = t.untyped_storage()
+            lo, nbytes = st.data_ptr(), st.nbytes()
+            if not lo or not nbytes:
+                continue
+            hi, key = lo + nbytes, id(st)
+            e = _watched.get(lo)
+            if e is not None and e[0] == hi and e[1] == key:
+                continue  # recorded as it is: live storages never overlap, nothing else to check
             prev = _watched_by_storage.get(key)
             if prev is not None and prev != lo:  # this storage's memory moved (resize_ / set_)
                 end, _, fin = _forget_locked(prev)
@@ -271,8 +274,8 @@ def _watch_host(tensors):
                 _watched[lo] = (hi, key, fin)
                 _watched_by_storage[key] = lo
                 bisect.insort(_watched_starts, lo)
-        for a, b in stale:
-            _release_range(a, b)
+    for a, b in stale:  # outside the lock: the engine may wait for its streams
+        _release_range(a, b)
 
 
 def _same_memory(a: torch.Tensor, b: torch.Tensor, what: str) -> int:
