@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
 #include <string>
 #include <sstream>
 #include <vector>
@@ -84,6 +85,18 @@ void log_line(int level, const std::string &msg);
             _os << msg;                                         \
             ::ddl::log_line((level), _os.str());                \
         }                                                       \
+    } while (0)
+
+// Step-by-step trace of the program posting (log_level >= 4): every HIP call of run_, flushed
+// before the call, so a crash inside the runtime names the call it was in.
+#define DDL_TRACE(msg)                                                                          \
+    do {                                                                                        \
+        if (::ddl::log_level() >= 4) {                                                          \
+            std::ostringstream _os;                                                             \
+            _os << msg;                                                                         \
+            std::fprintf(stderr, "[ddl trace] %s\n", _os.str().c_str());                         \
+            std::fflush(stderr);                                                                \
+        }                                                                                       \
     } while (0)
 
 // ---- kernels (reduce_kernels.hip) ----------------------------------------------------

@@ -1,4 +1,4 @@
-// deptrace.cpp — see deptrace.h.
+// deptrace.cpp — the happens-before recorder and checker (see deptrace.h). Testing library only.
 #include "deptrace.h"
 
 #include <algorithm>
@@ -8,8 +8,6 @@
 
 namespace ddl {
 namespace dep {
-
-std::atomic<bool> g_on{false};
 
 namespace {
 
@@ -21,7 +19,10 @@ struct OpRec {
     std::vector<Access> acc;
 };
 
-struct State {
+struct State : Sink {
+    void op(hipStream_t s, const std::string &what, std::vector<Access> acc) override;
+    void record(hipEvent_t e, hipStream_t s) override;
+    void wait(hipStream_t s, hipEvent_t e) override;
     std::mutex mu;
     std::unordered_map<hipStream_t, int> sid;
     std::vector<std::vector<uint32_t>> vc;                       // per stream
@@ -68,14 +69,13 @@ void start() {
     s.vc.clear();
     s.ev.clear();
     s.ops.clear();
-    g_on = true;
+    g_sink = &s;
 }
 
-void stop() { g_on = false; }
+void stop() { g_sink = nullptr; }
 
-void op(hipStream_t h, const std::string &what, std::vector<Access> acc) {
-    if (!on()) return;
-    State &s = st();
+void State::op(hipStream_t h, const std::string &what, std::vector<Access> acc) {
+    State &s = *this;
     std::lock_guard<std::mutex> g(s.mu);
     const int i = stream_id_(s, h);
     std::vector<uint32_t> &v = s.vc[(size_t)i];
@@ -84,16 +84,14 @@ void op(hipStream_t h, const std::string &what, std::vector<Access> acc) {
     s.ops.push_back(OpRec{i, v[(size_t)i], v, what, std::move(acc)});
 }
 
-void record(hipEvent_t e, hipStream_t h) {
-    if (!on()) return;
-    State &s = st();
+void State::record(hipEvent_t e, hipStream_t h) {
+    State &s = *this;
     std::lock_guard<std::mutex> g(s.mu);
     s.ev[e] = s.vc[(size_t)stream_id_(s, h)];
 }
 
-void wait(hipStream_t h, hipEvent_t e) {
-    if (!on()) return;
-    State &s = st();
+void State::wait(hipStream_t h, hipEvent_t e) {
+    State &s = *this;
     std::lock_guard<std::mutex> g(s.mu);
     const int i = stream_id_(s, h);
     auto it = s.ev.find(e);

@@ -1,5 +1,8 @@
 // deptrace.h — happens-before tracing of the work the engine posts on HIP streams (test /
-// diagnostic: off unless ddl_testing_dep_trace(1); one relaxed atomic load per posted op when off).
+// diagnostic). The engine itself only carries the hooks: op() / record() / wait() forward to a
+// Sink when one is installed and cost one relaxed atomic load otherwise. The recorder and its
+// checker (start / stop / check, deptrace.cpp) are linked into the testing library only
+// (libddl_amd_testing.so, ddl_testing_dep_trace); the deployment library never installs a sink.
 //
 // Every op the executors post — copies, transport receives / RCCL groups, reduce and fold
 // launches — is logged with the byte ranges it reads and writes, and every event record and
@@ -33,15 +36,31 @@ struct Access {
 inline Access rd(const void *p, size_t bytes) { return Access{(uintptr_t)p, (uintptr_t)p + bytes, false}; }
 inline Access wr(const void *p, size_t bytes) { return Access{(uintptr_t)p, (uintptr_t)p + bytes, true}; }
 
-extern std::atomic<bool> g_on;
-inline bool on() { return g_on.load(std::memory_order_relaxed); }
-void start();  // clears the log and starts tracing
-void stop();
+// Receiver of the posting log (the testing library's recorder).
+class Sink {
+public:
+    virtual ~Sink() = default;
+    virtual void op(hipStream_t s, const std::string &what, std::vector<Access> acc) = 0;
+    virtual void record(hipEvent_t e, hipStream_t s) = 0;
+    virtual void wait(hipStream_t s, hipEvent_t e) = 0;
+};
+extern std::atomic<Sink *> g_sink;  // null unless tracing (defined by the engine, executor.cpp)
+inline bool on() { return g_sink.load(std::memory_order_relaxed) != nullptr; }
 
 // Call right after the HIP call that posted the op / record / wait on `s`.
-void op(hipStream_t s, const std::string &what, std::vector<Access> acc);
-void record(hipEvent_t e, hipStream_t s);
-void wait(hipStream_t s, hipEvent_t e);
+inline void op(hipStream_t s, const std::string &what, std::vector<Access> acc) {
+    if (Sink *k = g_sink.load(std::memory_order_relaxed)) k->op(s, what, std::move(acc));
+}
+inline void record(hipEvent_t e, hipStream_t s) {
+    if (Sink *k = g_sink.load(std::memory_order_relaxed)) k->record(e, s);
+}
+inline void wait(hipStream_t s, hipEvent_t e) {
+    if (Sink *k = g_sink.load(std::memory_order_relaxed)) k->wait(s, e);
+}
+
+// ---- the recorder (deptrace.cpp: testing library only) ----
+void start();  // clears the log and installs the recorder
+void stop();   // uninstalls it (the log stays for check())
 
 struct Report {
     long long ops = 0;

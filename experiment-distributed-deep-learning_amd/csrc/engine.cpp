@@ -81,8 +81,9 @@ Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std:
     std::unique_ptr<Transport> t;
     if (size_ > 1) {
         if (hooks_) {
-            cb_ = new CallbackTransport(hooks_, tag_, world_ranks_, rank_, size_);
-            t.reset(cb_);
+            DDL_REQUIRE(hooks_->make_transport, DDL_STATUS_INVALID_ARGUMENT, "test hooks without a transport");
+            t = hooks_->make_transport(hooks_, tag_, world_ranks_, rank_, size_);
+            cb_ = t.get();
         } else {
             t.reset(new RcclTransport(nccl_));
         }
@@ -750,21 +751,6 @@ void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, h
     DDL_HIP(hipFree(d));
 }
 
-RcclLoopback &rccl_loopback() {
-    static RcclLoopback *l = new RcclLoopback();  // leaked: no static-destruction order issues
-    return *l;
-}
-
-LocalWorld &RcclLoopback::world(int nranks) {
-    DDL_REQUIRE(comm != nullptr, DDL_STATUS_NOT_INITIALIZED, "ddl_rccl_loopback_init has not been called");
-    int dev = 0;
-    DDL_HIP(hipGetDevice(&dev));
-    auto key = std::make_pair(nranks, comm);
-    auto it = worlds.find(key);
-    if (it == worlds.end()) it = worlds.emplace(key, std::unique_ptr<LocalWorld>(new LocalWorld(nranks, dev, comm))).first;
-    return *it->second;
-}
-
 RequestHandler *Communicator::handler_if_created() {
     std::lock_guard<std::mutex> g(handler_mu_);
     return handler_.get();
@@ -843,16 +829,29 @@ bool Registry::initialized() {
     return world_ != nullptr;
 }
 
-LocalWorld &local_world(int nranks) {
-    static std::mutex mu;
-    static std::map<std::pair<int, int>, std::unique_ptr<LocalWorld>> worlds;
-    int dev = 0;
-    DDL_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(mu);
-    auto key = std::make_pair(nranks, dev);
-    auto it = worlds.find(key);
-    if (it == worlds.end()) it = worlds.emplace(key, std::unique_ptr<LocalWorld>(new LocalWorld(nranks, dev))).first;
-    return *it->second;
+namespace {
+std::mutex &finalize_mu() {
+    static std::mutex *mu = new std::mutex;
+    return *mu;
+}
+std::vector<void (*)()> &finalize_hooks() {
+    static auto *v = new std::vector<void (*)()>;
+    return *v;
+}
+}  // namespace
+
+void add_finalize_hook(void (*fn)()) {
+    std::lock_guard<std::mutex> g(finalize_mu());
+    finalize_hooks().push_back(fn);
+}
+
+void run_finalize_hooks() {
+    std::vector<void (*)()> v;
+    {
+        std::lock_guard<std::mutex> g(finalize_mu());
+        v = finalize_hooks();
+    }
+    for (auto fn : v) fn();
 }
 
 }  // namespace ddl

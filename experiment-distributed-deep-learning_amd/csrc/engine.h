@@ -273,7 +273,7 @@ private:
     std::shared_ptr<TestHooks> hooks_;
     long long tag_ = 0;
     std::vector<int> world_ranks_;
-    CallbackTransport *cb_ = nullptr;  // the executor's transport when hooks_ (owned by exec_)
+    Transport *cb_ = nullptr;  // the executor's transport when hooks_ (owned by exec_): host groups
     std::mutex mu_;  // one collective at a time per communicator (RCCL ordering)
     std::unique_ptr<RingExecutor> exec_;
     std::shared_ptr<ControlChannel> control_;
@@ -307,6 +307,11 @@ private:
     std::shared_ptr<Communicator> world_;
 };
 
+// Cleanups ddl_finalize runs once the registry is cleared (the testing library adds its own: its
+// control channels and worlds).
+void add_finalize_hook(void (*fn)());
+void run_finalize_hooks();
+
 // Current-device guard: sets `device` for the scope, restores the previous one.
 class DeviceGuard {
 public:
@@ -316,8 +321,6 @@ public:
 private:
     int prev_ = -1;
 };
-
-LocalWorld &local_world(int nranks);
 
 // ---- RCCL pieces shared by the product path and the one-GPU loopback tests ---------------------
 // ncclCommInitRank of `rank` in a `size`-rank communicator from a 128-byte ncclUniqueId.
@@ -332,16 +335,5 @@ void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stre
 void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, hipStream_t stream);
 // Fails with DDL_STATUS_CONFIG_MISMATCH (naming every rank's hash) unless all hashes are equal.
 void check_config_agreement(int rank, const std::vector<uint64_t> &hashes);
-
-// One-rank RCCL communicator driving P virtual ranks' programs through RcclTransport (self
-// send/recv pairs) — test / diagnostic path (ddl_rccl_loopback_*), never used by ddl_init.
-struct RcclLoopback {
-    std::mutex mu;
-    ncclComm_t comm = nullptr;                  // current (the last split, or the initial comm)
-    std::vector<ncclComm_t> owned;              // every communicator created, destroyed at finalize
-    std::map<std::pair<int, ncclComm_t>, std::unique_ptr<LocalWorld>> worlds;  // (P, comm)
-    LocalWorld &world(int nranks);
-};
-RcclLoopback &rccl_loopback();
 
 }  // namespace ddl

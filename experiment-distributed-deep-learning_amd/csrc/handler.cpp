@@ -481,6 +481,8 @@ void RequestHandler::wait_all() {
 
 std::atomic<int> g_control_fault{0};
 void set_testing_control_fault(int on) { g_control_fault = on ? 1 : 0; }
+std::atomic<long long> g_host_coll_fault{-1};
+void set_testing_host_coll_fault(long long chunk) { g_host_coll_fault = chunk; }
 
 void RequestHandler::fail_all_(int status) {
     std::map<ReqId, Request> left;
@@ -1052,6 +1054,12 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     };
     std::vector<void *> dst;
     std::vector<size_t> len;
+    // no unpack job may outlive the plan: if posting throws midway (a collective, a
+    // HIP call, a failed unpack), the lane finishes the jobs already submitted — they write into
+    // the requests' outputs — before the error reaches complete_() and done(), after which the
+    // caller may free those outputs; drain() also clears the lane's error, so it cannot surface in
+    // a later plan's wait
+    try {
     for (size_t i = 0; i < nchunks; ++i) {
         const int k = (int)(i % kHostSlots);
         const size_t off = cut[i], n = cut[i + 1] - off;
@@ -1073,6 +1081,11 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
         DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
         const clk::time_point t_coll = clk::now();
+        const long long fault = g_host_coll_fault.load();
+        if (fault >= 0 && (long long)i >= fault) {  // test hook (ddl_testing_host_coll_fault)
+            g_host_coll_fault = -1;
+            fail(DDL_STATUS_COMM_ERROR, "test fault: host plan collective of chunk " + std::to_string(i));
+        }
         coll(dslot_[k], n / es);
         config().host_coll_ns.fetch_add(ns_since(t_coll));
         DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
@@ -1115,6 +1128,10 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         return;
     }
     for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) wait_unpack(j);
+    } catch (...) {
+        lane_->drain();
+        throw;
+    }
 }
 
 void RequestHandler::release_registrations() {

@@ -362,5 +362,9 @@ private:
 // Test hook (ddl_testing_control_fault): the next keyed round a member joins closes that member's
 // control link right after its snapshot froze the user collectives (a link lost mid-round).
 void set_testing_control_fault(int on);
+// Test hook (ddl_testing_host_coll_fault): the next host plan's staging loop fails at chunk
+// `chunk` (-1: off) — its device collective is not posted — to check that no unpack job of the
+// chunks before outlives the plan.
+void set_testing_host_coll_fault(long long chunk);
 
 }  // namespace ddl

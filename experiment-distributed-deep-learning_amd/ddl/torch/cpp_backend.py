@@ -4,6 +4,11 @@ The reference loads one library twice — as a TF op library and through ctypes.
 no op library: every call goes through the C-ABI of lib/libddl_amd.so (include/ddl_amd.h).
 `import torch` happens first so the engine binds to the HIP runtime (and RCCL) PyTorch has
 already loaded. If the library is missing the import fails loudly: there is no fallback path.
+
+`ddl_lib` (the reference's override, cpp_backend.py:34) selects another build: the tests, the
+bench and smoke() load lib/libddl_amd_testing.so — the same engine objects plus the test /
+measurement surface (include/ddl_amd_testing.h) — and the signatures of that surface are bound
+only when the loaded library exports it.
 """
 import ctypes
 import os
@@ -12,6 +17,19 @@ import torch  # noqa: F401  (must precede the CDLL: one HIP runtime per process)
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 DEFAULT_LIB = os.path.join(_PKG_ROOT, 'lib', 'libddl_amd.so')
+TESTING_LIB = os.path.join(_PKG_ROOT, 'lib', 'libddl_amd_testing.so')
+
+# include/ddl_amd.h: what the deployment library exports (and nothing else)
+DEPLOYMENT_API = (
+    'ddl_version', 'ddl_build_info', 'ddl_last_error', 'ddl_dtype_name', 'ddl_dtype_size', 'ddl_get_unique_id',
+    'ddl_init', 'ddl_init_single', 'ddl_control_listen', 'ddl_control_connect', 'ddl_control_stats', 'ddl_finalize',
+    'ddl_is_initialized', 'ddl_set_config', 'ddl_get_config', 'ddl_comm_transport', 'communicator_rank',
+    'communicator_size', 'world_communicator', 'split_communicator', 'detach_communicator', 'py_info', 'py_debug',
+    'py_error', 'ddl_allreduce', 'ddl_allreduce_batch', 'ddl_broadcast', 'ddl_allgatherv', 'ddl_allgather',
+    'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit', 'ddl_allgather_submit',
+    'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem', 'ddl_allreduce_submit_batch_mem',
+    'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all', 'ddl_host_unregister',
+    'ddl_kernel_timing', 'ddl_kernel_stats')
 
 # enum ddl_dtype (tensorflow::DataType numbers, reference src/cpp/def.h:10-53)
 DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_BFLOAT16, DT_HALF, DT_UINT64 = 1, 2, 3, 9, 14, 19, 23
@@ -53,10 +71,15 @@ class CPPBackend:
                 f'ddl engine library not found at {cls.__path_to_lib}; build it with '
                 f'`python -c "import __graft_entry__ as g; g.build()"` (no fallback exists)')
         lib = ctypes.CDLL(cls.__path_to_lib, mode=ctypes.RTLD_GLOBAL)
+        missing = [n for n in DEPLOYMENT_API if not hasattr(lib, n)]
+        if missing:
+            raise ImportError(f'{cls.__path_to_lib} lacks the deployment C-ABI: {missing}')
         cid, sz, vp, ci = ctypes.c_longlong, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
 
         def sig(name, restype, *argtypes):
-            f = getattr(lib, name)
+            f = getattr(lib, name, None)
+            if f is None:  # a test / measurement entry point: not in the deployment library
+                return
             f.restype = restype
             f.argtypes = list(argtypes)
 
@@ -147,6 +170,7 @@ class CPPBackend:
             ctypes.POINTER(sz), ci, vp)
         sig('ddl_testing_drop_wait', ci, ci)
         sig('ddl_testing_control_fault', ci, ci)
+        sig('ddl_testing_host_coll_fault', ci, ctypes.c_longlong)
         sig('ddl_testing_thread_transport', ci, ci, ctypes.POINTER(ctypes.c_longlong))
         sig('ddl_testing_dep_trace', ci, ci)
         sig('ddl_testing_thread_fused_allreduce', ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -178,6 +202,11 @@ class CPPBackend:
         if not cls.__initialized:
             cls.__initialize()
         return cls.__c_api
+
+    @classmethod
+    def has_testing_api(cls) -> bool:
+        """Whether the loaded library is the testing build (include/ddl_amd_testing.h)."""
+        return hasattr(cls.c_api(), 'ddl_init_test_transport')
 
     @classmethod
     def path(cls) -> str:

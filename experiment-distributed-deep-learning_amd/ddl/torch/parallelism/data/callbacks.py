@@ -6,8 +6,12 @@
 * MetricAverage — metric_average_callback.py:9-59: at epoch end every metric is averaged over
   the ranks (allreduce / size), metrics in sorted name order so every rank issues the same
   sequence of collectives; skipped at size 1 (:56-59).
+* LearningRateSchedule / LearningRateWarmup — lr_warm_up_callback.py:6-124: the learning rate
+  of a torch optimizer scaled per batch (or per epoch: staircase) by a multiplier of the epoch,
+  with momentum correction; the warm-up ramps from lr / size to lr over `warmup_epochs`. No
+  communication: only the communicator's size and rank are read.
 
-Both go through the engine's keyed requests (one negotiated, fused round per call).
+The first two go through the engine's keyed requests (one negotiated, fused round per call).
 """
 import torch
 
@@ -63,4 +67,124 @@ class MetricAverage:
     def on_epoch_end(self, epoch=None, logs=None):
         if self._comm.size > 1:
             self.average(logs)
+        return logs
+
+
+class LearningRateSchedule:
+    """Mirror of LearningRateScheduleCallback (lr_warm_up_callback.py:6-93) for a torch optimizer.
+
+    Call the hooks from the training loop as Keras calls them: `on_train_begin()` once,
+    `on_epoch_begin(epoch)`, `on_batch_begin(batch)` / `on_batch_end(batch)` around every step,
+    `on_epoch_end(epoch, logs)`. Between `start_epoch` and `end_epoch` every parameter group's lr
+    is `initial_lr * multiplier(epoch)` — at the first batch of an epoch with `staircase`, else
+    at every batch with the fractional epoch `epoch + batch / steps_per_epoch`. With
+    `momentum_correction` a group's momentum (SGD's `momentum`, what Keras' `optimizer.momentum`
+    is) is scaled by new_lr / old_lr for that one batch and restored after it.
+
+    `initial_lr`: None takes each group's lr at `on_train_begin` (the reference reads the
+    optimizer's single lr); a number sets every group from it. `steps_per_epoch`: needed unless
+    staircase; `on_train_begin(params=...)` may detect it from Keras-style params ('steps', or
+    'samples' and 'batch_size', :29-43)."""
+
+    def __init__(self, optimizer, multiplier, start_epoch=0, end_epoch=None, staircase=True,
+                 momentum_correction=True, steps_per_epoch=None, initial_lr=None):
+        self.optimizer = optimizer
+        self.start_epoch = start_epoch
+        self.end_epoch = end_epoch
+        self.staircase = staircase
+        self.momentum_correction = momentum_correction
+        self.initial_lr = initial_lr
+        self.restore_momentum = None
+        self.steps_per_epoch = steps_per_epoch
+        self.current_epoch = None
+        if not callable(multiplier):  # a constant multiplier changes only at epoch boundaries (:24-26)
+            self.staircase = True
+            self.multiplier = lambda epoch: multiplier
+        else:
+            self.multiplier = multiplier
+
+    def _autodetect_steps_per_epoch(self, params):
+        params = params or {}
+        if params.get('steps'):
+            return params['steps']
+        if params.get('samples') and params.get('batch_size'):
+            return params['samples'] // params['batch_size']
+        raise ValueError('Could not autodetect the number of steps per epoch. Please specify the steps_per_epoch '
+                         f'parameter to the {self.__class__.__name__}().')
+
+    def _adjust_learning_rate(self, epoch):
+        factor = self.multiplier(epoch)
+        self.restore_momentum = None
+        for i, group in enumerate(self.optimizer.param_groups):
+            old_lr = group['lr']
+            new_lr = self.initial_lr[i] * factor
+            group['lr'] = new_lr
+            if self.momentum_correction and 'momentum' in group and old_lr:
+                if self.restore_momentum is None:
+                    self.restore_momentum = {}
+                self.restore_momentum[i] = group['momentum']
+                group['momentum'] = group['momentum'] * new_lr / old_lr
+
+    def _restore_momentum_if_needed(self):
+        if self.restore_momentum:
+            for i, m in self.restore_momentum.items():
+                self.optimizer.param_groups[i]['momentum'] = m
+            self.restore_momentum = None
+
+    def on_train_begin(self, logs=None, params=None):
+        groups = self.optimizer.param_groups
+        if self.initial_lr is None:
+            self.initial_lr = [g['lr'] for g in groups]
+        elif not isinstance(self.initial_lr, (list, tuple)):
+            self.initial_lr = [self.initial_lr] * len(groups)
+        if not self.staircase and not self.steps_per_epoch:
+            self.steps_per_epoch = self._autodetect_steps_per_epoch(params)
+
+    def on_epoch_begin(self, epoch, logs=None):
+        self.current_epoch = epoch
+
+    def on_batch_begin(self, batch, logs=None):
+        if self.current_epoch < self.start_epoch or (self.end_epoch is not None and
+                                                     self.current_epoch >= self.end_epoch):
+            return
+        if self.staircase and batch == 0:
+            self._adjust_learning_rate(self.current_epoch)
+        elif not self.staircase:
+            self._adjust_learning_rate(self.current_epoch + float(batch) / self.steps_per_epoch)
+
+    def on_batch_end(self, batch, logs=None):
+        self._restore_momentum_if_needed()
+
+    def on_epoch_end(self, epoch, logs=None):
+        if logs is not None:
+            logs['lr'] = self.optimizer.param_groups[0]['lr']
+        return logs
+
+
+class LearningRateWarmup(LearningRateSchedule):
+    """Mirror of LearningRateWarmupCallback (lr_warm_up_callback.py:96-124): over the first
+    `warmup_epochs` the lr rises linearly from initial_lr / size to initial_lr, per batch:
+    multiplier(e) = 1 / size * ((e + 1 / steps_per_epoch) * (size - 1) / warmup_epochs + 1), with
+    e the fractional epoch. The scripts scale the base lr by the size first (the reference's
+    examples/data_parallelism.py:73-101). `verbose` prints only on rank 0."""
+
+    def __init__(self, optimizer, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0,
+                 initial_lr=None, communicator: Communicator = None):
+        comm = Communicator.world() if communicator is None else communicator
+
+        def multiplier(epoch):
+            # shifted by one batch so each epoch ends on a round number (:106-109)
+            epoch += 1. / self.steps_per_epoch
+            return 1. / comm.size * (epoch * (comm.size - 1) / warmup_epochs + 1)
+
+        super().__init__(optimizer, multiplier, start_epoch=0, end_epoch=warmup_epochs, staircase=False,
+                         momentum_correction=momentum_correction, steps_per_epoch=steps_per_epoch,
+                         initial_lr=initial_lr)
+        self.verbose = verbose if comm.rank == 0 else 0
+
+    def on_epoch_end(self, epoch, logs=None):
+        logs = super().on_epoch_end(epoch, logs)
+        if epoch == self.end_epoch - 1 and self.verbose > 0:
+            print('\nEpoch %d: finished gradual learning rate warmup to %g.' %
+                  (epoch + 1, self.optimizer.param_groups[0]['lr']))
         return logs

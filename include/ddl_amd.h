@@ -12,8 +12,12 @@
  *   cpp/c_api.h:37-41   py_info/py_debug/py_error         py_info/py_debug/py_error
  *   cpp/global/initialize.cc:57-65 + MPIBackend.cc:77-97  ddl_get_unique_id + ddl_init
  *     (MPI_Init_thread at dlopen)                          (explicit RCCL bootstrap)
- *   cpp/communicate/backend/Communicator.h:45-48 /        ddl_allreduce (device buffers,
- *     mpi/MPICommunicator.cc:14-28  (MPI_Allreduce SUM)     ring RS/AG over RCCL + HIP reduce)
+ *   cpp/communicate/backend/Communicator.h:45-48 /        ddl_allreduce (device buffers; at
+ *     mpi/MPICommunicator.cc:14-28  (MPI_Allreduce SUM)     P > 2 by default the direct schedule:
+ *                                                          reduce-scatter of slices to every peer
+ *                                                          over RCCL send/recv, a HIP fold of the P
+ *                                                          inputs in MPICH's order, allgather; a
+ *                                                          ring at P = 2; autotuned per size class)
  *   cpp/op/tensorflow/AllreduceOp.cc:32-66 →              ddl_allreduce_submit
  *     TensorsCollectiveCommunicateController::handleRequest (keyed async request, done callback)
  *     (.../controller/TensorsCollectiveCommunicateController.h:14-34)
@@ -304,8 +308,10 @@ int ddl_host_unregister(const void *ptr, size_t bytes);
 
 /* Measurement: bracket every reduce-kernel launch of ddl_allreduce on `id` with timing
  * events on the engine's compute stream (the stream the kernel runs on). ddl_kernel_stats
- * waits for the recorded events and returns launches, algorithmic HBM bytes
- * (3 * elements * sizeof(T) per launch) and summed kernel milliseconds, then resets. */
+ * waits for the recorded events and returns launches, algorithmic HBM bytes (per launch: a
+ * two-input ring step 3 * elements * sizeof(T); a fold of nb received inputs
+ * (nb + 2) * elements * sizeof(T) — the own input, the nb inputs, one write) and summed kernel
+ * milliseconds, then resets. */
 int ddl_kernel_timing(ddl_communicator_id id, int on);
 int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes, double *ms);
 

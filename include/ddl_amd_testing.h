@@ -170,6 +170,10 @@ int ddl_testing_thread_transport(int rccl, long long *loopback_pairs);
  * with an error, and later user collectives on the communicator return that error instead of
  * blocking behind the round that can no longer be placed. */
 int ddl_testing_control_fault(int on);
+/* Fault for the host staging loop: the next keyed host plan fails at chunk `chunk`
+ * (its collective is not posted; -1 turns it off). The staged unpacks of the chunks before it
+ * have all landed when the requests' done() reports the error. */
+int ddl_testing_host_coll_fault(long long chunk);
 /* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
  * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
 int ddl_testing_drop_wait(int tick);

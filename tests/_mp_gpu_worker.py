@@ -434,6 +434,34 @@ def check_dp_training(ctx):
     assert torch.allclose(emb.weight.detach(), want)
     logs = MetricAverage(comm).on_epoch_end(0, {'loss': float(r), 'acc': 2.0 * r})
     assert logs == {'loss': (P - 1) / 2, 'acc': float(P - 1)}
+    # the reference's DP script (examples/data_parallelism.py:73-101): lr scaled by the size, the
+    # warm-up callback beside MetricAverage, the wrapped optimizer stepping under it
+    from ddl.torch.parallelism.data import LearningRateWarmup
+    base_lr, steps, warm = 0.05, 2, 2
+    wopt = data_parallelism_distributed_optimizer_wrapper(
+        torch.optim.SGD(model.parameters(), lr=base_lr * P, momentum=0.5), comm)
+    cbs = [LearningRateWarmup(wopt, warmup_epochs=warm, steps_per_epoch=steps, communicator=comm),
+           MetricAverage(comm)]
+    cbs[0].on_train_begin()
+    for e in range(warm + 1):
+        cbs[0].on_epoch_begin(e)
+        for b in range(steps):
+            cbs[0].on_batch_begin(b)
+            if e < warm:
+                want = base_lr * P / P * ((e + (b + 1) / steps) * (P - 1) / warm + 1)
+                assert abs(wopt.param_groups[0]['lr'] - want) < 1e-12, (e, b, wopt.param_groups[0]['lr'], want)
+            wopt.zero_grad()
+            torch.nn.functional.mse_loss(model(xb[r].cuda()), yb[r].cuda()).backward()
+            wopt.step()
+            cbs[0].on_batch_end(b)
+            assert wopt.param_groups[0]['momentum'] == 0.5
+        logs = cbs[1].on_epoch_end(e, cbs[0].on_epoch_end(e, {'loss': float(r)}))
+        assert logs['loss'] == (P - 1) / 2 and abs(logs['lr'] - base_lr * P) < 1e-12 or e < warm - 1
+    everyone = [None] * P
+    dist.all_gather_object(everyone, [p.detach().cpu() for p in model.parameters()])
+    for other in everyone[1:]:  # replicas stay identical under the schedule
+        for a, b in zip(everyone[0], other):
+            assert torch.equal(a, b)
 
 
 def check_config_mismatch(ctx):

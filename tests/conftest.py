@@ -42,18 +42,26 @@ def _library_build_id(path):
     return m.group(1).decode() if m else None
 
 
+DEPLOYMENT_LIB = os.path.join(PKG, 'lib', 'libddl_amd.so')
+TESTING_LIB = os.path.join(PKG, 'lib', 'libddl_amd_testing.so')
+
+
 def _build_if_stale():
-    """The library under test must be built from these sources: built when missing, rebuilt when
-    its baked-in source hash differs (a stale prebuilt .so is never tested)."""
-    lib = os.path.join(PKG, 'lib', 'libddl_amd.so')
+    """The libraries under test must be built from these sources: built when missing, rebuilt
+    when a baked-in source hash differs (a stale prebuilt .so is never tested)."""
     ora = os.path.join(ROOT, 'oracle', 'build', 'libddl_oracle.so')
-    if not os.path.exists(lib) or _library_build_id(lib) != source_hash():
+    want = source_hash()
+    if any(not os.path.exists(p) or _library_build_id(p) != want for p in (DEPLOYMENT_LIB, TESTING_LIB)):
         subprocess.run(['make', '-C', os.path.join(PKG, 'csrc'), '-j8', '-B'], check=True)
     if not os.path.exists(ora):
         subprocess.run(['make', '-C', os.path.join(ROOT, 'oracle')], check=True)
 
 
 _build_if_stale()
+# the suite drives the engine through the testing build (the same engine objects plus the test /
+# measurement surface, include/ddl_amd_testing.h) via the reference's `ddl_lib` override; worker
+# processes inherit it. tests/test_deployment_lib_gpu.py runs the deployment library on its own.
+os.environ.setdefault('ddl_lib', TESTING_LIB)
 
 
 @pytest.fixture(scope='session')

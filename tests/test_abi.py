@@ -11,7 +11,8 @@ from conftest import PKG, ROOT
 
 HEADER = os.path.join(ROOT, 'include', 'ddl_amd.h')
 TESTING_HEADER = os.path.join(ROOT, 'include', 'ddl_amd_testing.h')
-LIB = os.path.join(PKG, 'lib', 'libddl_amd.so')
+LIB = os.path.join(PKG, 'lib', 'libddl_amd.so')  # the deployment library
+TESTING_LIB = os.path.join(PKG, 'lib', 'libddl_amd_testing.so')
 
 # reference src/cpp/c_api.h:15-41 (the ctypes surface, cpp_backend.py:47-78)
 REFERENCE_C_API = {'communicator_rank', 'communicator_size', 'world_communicator', 'split_communicator',
@@ -57,12 +58,58 @@ def test_deployment_header_is_only_the_deployment_surface():
         assert n in testing, n
 
 
-def test_every_declared_symbol_is_exported():
-    out = subprocess.run(['nm', '-D', '--defined-only', LIB], capture_output=True, text=True, check=True).stdout
-    exported = set(line.split()[-1] for line in out.splitlines() if ' T ' in line)
+def _exported(path):
+    out = subprocess.run(['nm', '-D', '--defined-only', path], capture_output=True, text=True, check=True).stdout
+    return set(line.split()[-1] for line in out.splitlines() if ' T ' in line)
+
+
+def test_deployment_library_exports_exactly_the_header():
+    """libddl_amd.so exports the functions include/ddl_amd.h declares and
+    nothing else (version script ddl_amd.map): the reference's c_api.h names plus the deployment
+    surface."""
+    exported = _exported(LIB)
+    declared = set(declared_functions())
+    assert exported == declared, (sorted(exported - declared), sorted(declared - exported))
+    dyn = subprocess.run(['nm', '-D', '--defined-only', LIB], capture_output=True, text=True, check=True).stdout
+    assert all(line.split()[1] in 'T' for line in dyn.splitlines() if len(line.split()) == 3 and
+               line.split()[1] not in 'Aw'), 'the deployment library exports data or weak symbols'
+
+
+def test_testing_library_exports_both_headers():
+    exported = _exported(TESTING_LIB)
     declared = declared_functions() + declared_functions(TESTING_HEADER)
     missing = [n for n in declared if n not in exported]
     assert not missing, f'declared but not exported: {missing}'
+
+
+def test_deployment_library_links_no_test_harness():
+    """The test worlds, the test transport, the RCCL loopback and the happens-before recorder are
+    linked into the testing library only: not even a local symbol of theirs is in the deployment
+    library (both are built from the same engine objects; the harness objects are extra)."""
+    syms = subprocess.run(['nm', '-C', LIB], capture_output=True, text=True, check=True).stdout
+    for name in ('ThreadFabric', 'ThreadWorld', 'LocalWorld', 'CallbackTransport', 'RcclLoopback',
+                 'ddl_testing_', 'ddl_rccl_loopback', 'ddl_local_', 'dep::start', 'dep::check'):
+        assert name not in syms, name
+    tsyms = subprocess.run(['nm', '-C', TESTING_LIB], capture_output=True, text=True, check=True).stdout
+    assert 'ThreadWorld' in tsyms and 'dep::check' in tsyms
+
+
+def test_both_libraries_carry_identical_gpu_code():
+    """The kernels the tests and the bench measure (testing library) are byte-for-byte the
+    deployment library's: the same .hip_fatbin section (the gfx950 code objects)."""
+    import tempfile
+    blobs = []
+    with tempfile.TemporaryDirectory() as d:
+        for i, path in enumerate((LIB, TESTING_LIB)):
+            out = os.path.join(d, f'{i}.bin')
+            subprocess.run(['objcopy', '-O', 'binary', '--only-section=.hip_fatbin', path, out], check=True)
+            blobs.append(open(out, 'rb').read())
+    assert len(blobs[0]) > 100_000 and blobs[0] == blobs[1]
+
+
+def test_same_build_id_in_both_libraries():
+    from conftest import _library_build_id, source_hash
+    assert _library_build_id(LIB) == _library_build_id(TESTING_LIB) == source_hash()
 
 
 def test_test_transport_refused_without_opt_in(lib):
@@ -135,8 +182,9 @@ def test_product_does_not_reference_oracle():
             if f.endswith(('.cpp', '.h', '.hip', '.py')):
                 text = open(os.path.join(d, f), errors='replace').read()
                 assert 'ddl_oracle' not in text and 'ddlo_' not in text, f
-    out = subprocess.run(['readelf', '-d', LIB], capture_output=True, text=True, check=True).stdout
-    assert 'oracle' not in out
+    for path in (LIB, TESTING_LIB):
+        out = subprocess.run(['readelf', '-d', path], capture_output=True, text=True, check=True).stdout
+        assert 'oracle' not in out
 
 
 def test_python_config_module(lib):

@@ -412,6 +412,39 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
             lib.ddl_set_config(k, v)
 
 
+def test_host_plan_failure_drains_unpacks(world, lib):
+    """a host plan whose staging loop fails midway — here its collective at
+    chunk 8, past the 4 download slots, so unpack jobs of earlier chunks are queued on the unpack
+    lane — reports the error only once every unpack already submitted has written its chunk:
+    after done(error) the output never changes again (the caller may free it then). Chunks 0-7
+    hold the input, the rest is untouched; the next round on the same handler works (the lane's
+    error does not leak into it)."""
+    import time
+
+    import _helpers as h
+    from ddl.torch.cpp_backend import DDLError
+    from ddl.torch.tensor_communicate import allreduce_async
+    chunk = 256 << 10
+    x = torch.arange(3_000_017, dtype=torch.float32)
+    out = torch.full_like(x, -7.0)
+    with h.config(lib, one_rank_shortcut=0, host_chunk_bytes=chunk, host_zero_copy=0):
+        assert lib.ddl_testing_host_coll_fault(8) == 0
+        try:
+            hd = allreduce_async(x, 'fault_plan', world, output=out)
+            with pytest.raises(DDLError):
+                hd.wait(timeout=60)
+            snap = out.clone()
+            time.sleep(0.3)
+            assert torch.equal(out, snap), 'the output changed after done(error)'
+        finally:
+            assert lib.ddl_testing_host_coll_fault(-1) == 0
+        k = 8 * chunk // 4
+        assert torch.equal(out[:k], x[:k])
+        assert bool((out[k:] == -7.0).all())
+        y = torch.arange(1_000_003, dtype=torch.float32)
+        assert torch.equal(allreduce_async(y, 'after_fault', world, output=torch.empty_like(y)).wait(timeout=60), y)
+
+
 def test_registration_cache_address_reuse(world, lib):
     """the registration cache is keyed by virtual address. r04 measured what the
     advisor feared: a cached pageable range unmapped and mapped afresh at the same address (munmap,
