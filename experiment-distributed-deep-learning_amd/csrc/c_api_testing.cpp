@@ -124,12 +124,17 @@ std::mutex g_thread_mu;
 std::map<std::tuple<int, int, int, ncclComm_t>, std::unique_ptr<ThreadWorld>> *g_thread_worlds =
     new std::map<std::tuple<int, int, int, ncclComm_t>, std::unique_ptr<ThreadWorld>>();
 
+// Lock order: the loopback's mutex, then g_thread_mu — as ddl_rccl_loopback_finalize takes them — so
+// the loopback communicator cannot be destroyed between reading it and building the world on it
+// (ADVICE r4). A world returned here is used after the locks are released: finalize must not run
+// concurrently with thread-transport calls (the tests call it between them).
 ThreadWorld &thread_world(int nranks) {
     int dev = current_device();
     ncclComm_t loop = nullptr;
+    std::unique_lock<std::mutex> lg;
     if (g_thread_rccl.load()) {
         RcclLoopback &l = rccl_loopback();
-        std::lock_guard<std::mutex> lg(l.mu);
+        lg = std::unique_lock<std::mutex>(l.mu);
         DDL_REQUIRE(l.comm, DDL_STATUS_NOT_INITIALIZED, "thread transport 1 needs ddl_rccl_loopback_init first");
         loop = l.comm;
     }
@@ -507,6 +512,14 @@ int ddl_testing_control_fault(int on) {
 
 int ddl_testing_host_coll_fault(long long chunk) {
     return guarded([&] { set_testing_host_coll_fault(chunk); });
+}
+
+int ddl_testing_fold_variant(int variant) {
+    return guarded([&] {
+        DDL_REQUIRE(variant == -1 || variant == 4 || variant == 5, DDL_STATUS_INVALID_ARGUMENT,
+                    "fold variant " << variant << " (4, 5 or -1)");
+        set_testing_fold_variant(variant);
+    });
 }
 
 int ddl_testing_drop_wait(int tick) {

@@ -171,6 +171,7 @@ int ring_variant();     // reduce-scatter step of the ring
 // always tiled). Local: it changes no collective's program, only the kernel (the same sums either
 // way).
 void set_fold_form(int form);
+void set_testing_fold_variant(int v);  // ddl_testing_fold_variant: 4 / 5 forced, -1 the size rule
 int get_fold_form();
 
 // out = a + b for each segment; dtype-generic. Returns via fail() on bad arguments.

@@ -251,6 +251,8 @@ constexpr int kReduceThreads = 128;
 // 256 MiB Infinity Cache, where RCCL has just written the received slices) read through the
 // caches: 5.53 vs 5.05 TB/s at 4 MiB (plain loads + write-through store vs all-nt).
 int fold_variant(size_t chunk_bytes) { return chunk_bytes <= (8u << 20) ? 4 : 5; }
+// ddl_testing_fold_variant: forces the policy (4 or 5; -1 = fold_variant's rule) for A/Bs
+std::atomic<int> g_fold_variant{-1};
 
 // One 2 KiB tile of the output per 128-lane workgroup: each lane folds its 16 bytes across a
 // and the nb received inputs, one buffer_load_dwordx4 per input through one descriptor per input
@@ -495,7 +497,9 @@ void launch_sumN_nb(const FoldBatch &b, hipStream_t stream) {
             // 8 MiB, in cache)
             uint64_t elems = 0;
             for (int i = 0; i < b.count; ++i) elems += b.t[i].n;
-            if (fold_variant((size_t)elems * sizeof(typename Add<DT>::S)) == 4) launch_sumN_order<DT, NB, 4>(b, stream);
+            const int forced = g_fold_variant.load(std::memory_order_relaxed);
+            const int fv = forced >= 0 ? forced : fold_variant((size_t)elems * sizeof(typename Add<DT>::S));
+            if (fv == 4) launch_sumN_order<DT, NB, 4>(b, stream);
             else launch_sumN_order<DT, NB, 5>(b, stream);
         } else {
             launch_sumN_nb<DT, NB + 1>(b, stream);
@@ -593,6 +597,7 @@ int g_cu_count = 0;
 }  // namespace
 
 void set_fold_form(int form) { g_fold_form.store(form, std::memory_order_relaxed); }
+void set_testing_fold_variant(int v) { g_fold_variant.store(v, std::memory_order_relaxed); }
 int get_fold_form() { return g_fold_form.load(std::memory_order_relaxed); }
 
 int device_cu_count() {

@@ -29,7 +29,8 @@ DEPLOYMENT_API = (
     'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit', 'ddl_allgather_submit',
     'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem', 'ddl_allreduce_submit_batch_mem',
     'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all', 'ddl_host_unregister',
-    'ddl_kernel_timing', 'ddl_kernel_stats')
+    'ddl_kernel_timing', 'ddl_kernel_stats', 'ddl_completion_create', 'ddl_completion_slots', 'ddl_completion_done',
+    'ddl_completion_wait', 'ddl_completion_poll', 'ddl_completion_destroy')
 
 # enum ddl_dtype (tensorflow::DataType numbers, reference src/cpp/def.h:10-53)
 DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_BFLOAT16, DT_HALF, DT_UINT64 = 1, 2, 3, 9, 14, 19, 23
@@ -132,6 +133,12 @@ class CPPBackend:
         sig('ddl_control_channel_negotiate', ci, ctypes.c_longlong, ctypes.c_char_p, ctypes.c_char_p, sz)
         sig('ddl_control_channel_close', ci, ctypes.c_longlong)
         sig('ddl_wait_all', ci, cid)
+        sig('ddl_completion_create', vp, ci)
+        sig('ddl_completion_slots', ci, vp, ci, ci, ctypes.POINTER(vp))
+        sig('ddl_completion_done', None, ci, vp)
+        sig('ddl_completion_wait', ci, vp, ci, ctypes.c_double, ctypes.POINTER(ci))
+        sig('ddl_completion_poll', ci, vp, ctypes.POINTER(ci), ci)
+        sig('ddl_completion_destroy', None, vp)
         sig('ddl_host_unregister', ci, ctypes.c_void_p, ctypes.c_size_t)
         sig('ddl_broadcast_submit', ci, cid, ctypes.c_char_p, vp, vp, sz, ci, ci, vp, DONE_FN, vp)
         sig('ddl_allgather_submit', ci, cid, ctypes.c_char_p, vp, sz, sz, ci, vp, ALLOC_FN, DONE_FN, vp)
@@ -171,6 +178,7 @@ class CPPBackend:
         sig('ddl_testing_drop_wait', ci, ci)
         sig('ddl_testing_control_fault', ci, ci)
         sig('ddl_testing_host_coll_fault', ci, ctypes.c_longlong)
+        sig('ddl_testing_fold_variant', ci, ci)
         sig('ddl_testing_thread_transport', ci, ci, ctypes.POINTER(ctypes.c_longlong))
         sig('ddl_testing_dep_trace', ci, ci)
         sig('ddl_testing_thread_fused_allreduce', ci, ci, ci, ctypes.POINTER(vp), ctypes.POINTER(vp),

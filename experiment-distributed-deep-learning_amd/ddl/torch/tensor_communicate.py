@@ -65,8 +65,10 @@ def allreduce_(tensor: torch.Tensor, communicator: Communicator = None) -> torch
 def allreduce_batch_(tensors, communicator: Communicator = None):
     """In-place SUM of every device tensor in `tensors` (one dtype) over the ranks, as ONE grouped
     collective (ddl_allreduce_batch): a DDP-style bucket list reduced with one RCCL group per tick
-    and the folds of up to 8 buckets per kernel launch. Each result is bit for bit what
-    `allreduce_` gives that tensor alone. Every rank passes the same shapes in the same order."""
+    and the folds of up to 8 buckets per kernel launch. With reference_order 1 (the default) each
+    result is bit for bit what `allreduce_` gives that tensor alone (MPICH's order for its own
+    size); with reference_order 0 the batch schedule's order may differ from a solo call's in the
+    last bits (include/ddl_amd.h). Every rank passes the same shapes in the same order."""
     communicator = _comm(communicator)
     tensors = list(tensors)
     if not tensors:
@@ -178,18 +180,105 @@ class Handle:
         return self.output
 
 
-_pending = {}
-_pending_lock = threading.Lock()
+_pending_lock = threading.Lock()  # keyed allgathers in flight (_gathers)
 _ids = itertools.count(1)
 
 
-@cb.DONE_FN
-def _on_done(status, user):
-    with _pending_lock:
-        h = _pending.pop(user, None)
-    if h is not None:
-        h.status = status
-        h._event.set()
+class _Completion:
+    """A completion group of the engine (ddl_completion_*, csrc/completion.cpp): the engine's
+    done() is native and stores each request's status in its slot, so completing a request costs
+    no Python callback (~10 us of interpreter time each: 40-60 ms per 4096-tensor batch, DESIGN
+    §7); a handle blocks in C++ with the GIL released, and once every slot has completed one poll
+    caches all statuses, so the rest of a batch's waits are list reads. The group holds the
+    requests' tensors until every slot has completed (swept at later submissions), so a handle
+    dropped without wait() cannot free memory the engine still reads or writes; the engine frees
+    the group once its owner let go AND every slot completed."""
+    __slots__ = ('ptr', 'count', 'keep', 'final', '__weakref__')
+    _inflight = []  # groups with slots still pending: keep their tensors alive
+    _inflight_lock = threading.Lock()
+
+    def __init__(self, count: int, keep):
+        lib = CPPBackend.c_api()
+        self.ptr = lib.ddl_completion_create(count)
+        if not self.ptr:
+            raise MemoryError('ddl_completion_create')
+        self.count, self.keep, self.final = count, keep, None
+        weakref.finalize(self, lib.ddl_completion_destroy, self.ptr)
+        with _Completion._inflight_lock:
+            live = []
+            for g in _Completion._inflight:
+                if lib.ddl_completion_poll(g.ptr, None, 0) > 0:
+                    live.append(g)
+                else:
+                    g.keep = None
+            live.append(self)
+            _Completion._inflight = live
+
+    def slots(self, first: int = 0, count: int = None):
+        """The `user` pointers of slots [first, first + count) (a ctypes array)."""
+        count = self.count - first if count is None else count
+        arr = (ctypes.c_void_p * count)()
+        check(CPPBackend.c_api().ddl_completion_slots(self.ptr, first, count, arr), 'ddl_completion_slots')
+        return arr
+
+    def status(self, index: int, timeout: float = None) -> int:
+        """Slot `index`'s status once it completed (TimeoutError after `timeout` seconds)."""
+        if self.final is not None:
+            return self.final[index]
+        lib = CPPBackend.c_api()
+        st = ctypes.c_int()
+        if lib.ddl_completion_wait(self.ptr, index, -1.0 if timeout is None else float(timeout),
+                                   ctypes.byref(st)) != cb.STATUS_OK:
+            raise TimeoutError('request did not complete')
+        if self.count > 1 and lib.ddl_completion_poll(self.ptr, None, 0) == 0:
+            arr = (ctypes.c_int * self.count)()
+            lib.ddl_completion_poll(self.ptr, arr, self.count)
+            self.final = list(arr)
+        return st.value
+
+    def fail(self, indices, status):
+        """The submission was refused: nothing will complete these slots but us."""
+        lib = CPPBackend.c_api()
+        slots = self.slots()
+        for i in indices:
+            lib.ddl_completion_done(status, slots[i])
+
+
+_NATIVE_DONE = []
+
+
+def _native_done():
+    """ddl_completion_done as a ddl_done_fn argument (the C function itself: no Python callback)."""
+    if not _NATIVE_DONE:
+        lib = CPPBackend.c_api()
+        _NATIVE_DONE.append(cb.DONE_FN(ctypes.cast(lib.ddl_completion_done, ctypes.c_void_p).value))
+    return _NATIVE_DONE[0]
+
+
+class _NativeHandle(Handle):
+    """Handle of a request completed through a completion group (no Python done callback)."""
+
+    def __init__(self, key: str, output: torch.Tensor, keep_alive, group: _Completion, index: int):
+        # (no threading.Event: the slot is the completion)
+        self.key, self.output, self._keep, self.status = key, output, keep_alive, None
+        self._group, self._index = group, index
+
+    def done(self) -> bool:
+        try:
+            self.status = self._group.status(self._index, 0.0)
+        except TimeoutError:
+            return False
+        return True
+
+    def wait(self, timeout: float = None) -> torch.Tensor:
+        try:
+            self.status = self._group.status(self._index, timeout)
+        except TimeoutError:
+            raise TimeoutError(f'request {self.key!r} did not complete') from None
+        self._keep = None
+        if self.status != cb.STATUS_OK:
+            raise cb.DDLError(self.status, f'request {self.key!r}', '')
+        return self.output
 
 
 # Host ranges the engine's registration cache may hold, as the torch mirror submitted them (see
@@ -299,16 +388,13 @@ def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     mem = _same_memory(tensor, out, 'allreduce_async')
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
-    uid = next(_ids)
-    h = Handle(name, out, (tensor, out))
-    with _pending_lock:
-        _pending[uid] = h
+    group = _Completion(1, (tensor, out))
+    h = _NativeHandle(name, out, (tensor, out), group, 0)
     st = CPPBackend.c_api().ddl_allreduce_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(),
-        ddl_dtype(tensor), cb.OP_SUM, mem, stream_handle_for(tensor), _on_done, uid)
+        ddl_dtype(tensor), cb.OP_SUM, mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
     if st != cb.STATUS_OK:
-        with _pending_lock:
-            _pending.pop(uid, None)
+        group.fail([0], st)
         check(st, 'ddl_allreduce_submit_mem')
     return h
 
@@ -330,10 +416,11 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     mems = [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
     if cb.MEMORY_HOST in mems:
         _watch_host([x for i, m in enumerate(mems) if m == cb.MEMORY_HOST for x in (tensors[i], outputs[i])])
-    uids = [next(_ids) for _ in range(k)]
-    handles = [Handle(n, o, (t, o)) for n, t, o in zip(names, tensors, outputs)]
-    with _pending_lock:
-        _pending.update(zip(uids, handles))
+    # one completion group for the batch: the engine completes every request natively (no
+    # Python done() per tensor)
+    group = _Completion(k, (tensors, outputs))
+    handles = [_NativeHandle(n, o, (t, o), group, i) for i, (n, t, o) in enumerate(zip(names, tensors, outputs))]
+    done, slots = _native_done(), group.slots()
     for mem in sorted(set(mems)):
         idx = [i for i in range(k) if mems[i] == mem]
         m = len(idx)
@@ -342,14 +429,13 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
         outs = (ctypes.c_void_p * m)(*[outputs[i].data_ptr() for i in idx])
         ns = (ctypes.c_size_t * m)(*[tensors[i].numel() for i in idx])
         dts = (ctypes.c_int * m)(*[ddl_dtype(tensors[i]) for i in idx])
-        users = (ctypes.c_void_p * m)(*[uids[i] for i in idx])
+        users = (ctypes.c_void_p * m)(*[slots[i] for i in idx])
         st = CPPBackend.c_api().ddl_allreduce_submit_batch_mem(
             communicator.id, m, keys, ins, outs, ns, dts, cb.OP_SUM, mem, stream_handle_for(tensors[idx[0]]),
-            _on_done, users)
+            done, users)
         if st != cb.STATUS_OK:
-            with _pending_lock:
-                for i in idx:
-                    _pending.pop(uids[i], None)
+            rest = [i for i in range(k) if mems[i] >= mem]  # this submission and the ones not made
+            group.fail(rest, st)
             check(st, 'ddl_allreduce_submit_batch_mem')
     return handles
 
@@ -363,16 +449,13 @@ def broadcast_async(tensor: torch.Tensor, name: str, root_rank: int, communicato
     mem = _same_memory(tensor, out, 'broadcast_async')
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
-    uid = next(_ids)
-    h = Handle(name, out, (tensor, out))
-    with _pending_lock:
-        _pending[uid] = h
+    group = _Completion(1, (tensor, out))
+    h = _NativeHandle(name, out, (tensor, out), group, 0)
     st = CPPBackend.c_api().ddl_broadcast_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(), ddl_dtype(tensor),
-        int(root_rank), mem, stream_handle_for(tensor), _on_done, uid)
+        int(root_rank), mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
     if st != cb.STATUS_OK:
-        with _pending_lock:
-            _pending.pop(uid, None)
+        group.fail([0], st)
         check(st, 'ddl_broadcast_submit_mem')
     return h
 

@@ -205,7 +205,11 @@ int ddl_allreduce(ddl_communicator_id id, const void *send, void *recv, size_t e
 
 /* Grouped form of ddl_allreduce for `count` buckets of one dtype (MI355X extension: a DDP-style
  * bucket list in one call): recvs[b] = SUM over ranks of sends[b] (elements[b] each; in place when
- * recvs[b] == sends[b]), bit for bit what ddl_allreduce gives each bucket on its own. One program
+ * recvs[b] == sends[b]); with reference_order 1 (the default) bit for bit what ddl_allreduce
+ * gives each bucket on its own (both are MPICH's order for the bucket's own size); with
+ * reference_order 0 each bucket is summed in the batch schedule's order (direct: rank-order fold;
+ * one-shot: left fold), which may differ in the last bits from the ring or other schedule a solo
+ * ddl_allreduce of that bucket's size class was tuned to. One program
  * for all buckets — tick by tick one RCCL group carries every bucket's slices and the folds of up
  * to 8 buckets share a kernel launch — instead of a program, two or more groups and a fold launch
  * per bucket. The schedule is the one tuned for the largest bucket (direct, or one-shot for small
@@ -295,6 +299,24 @@ int ddl_allgather_submit_mem(ddl_communicator_id id, const char *key, const void
                              ddl_done_fn done, void *user);
 /* Blocks until every request submitted on `id` so far has completed. */
 int ddl_wait_all(ddl_communicator_id id);
+
+/* Completion groups (MI355X extension, csrc/completion.cpp): a native done callback for bindings
+ * whose own callbacks are costly — a Python done() per request costs ~10 us of interpreter time,
+ * 40-60 ms per 4096-tensor batch. Create a group of `count` slots, pass ddl_completion_done as the
+ * ddl_done_fn and slot i's pointer (ddl_completion_slots: `count` of them from `first` into out)
+ * as request i's `user`; done() stores the status in slot i and wakes its waiters.
+ * ddl_completion_wait blocks (no callback into the binding) until slot `index` completed or
+ * `timeout_s` (< 0: no limit; 0: a test) passed: DDL_STATUS_OK with *status = the request's
+ * status, or DDL_STATUS_ERROR_UNKNOWN while it is still pending. ddl_completion_poll copies the
+ * first `count` slots' statuses (-1: pending; statuses may be NULL when count is 0) and returns
+ * how many slots are pending. ddl_completion_destroy is the owner's release: the group is freed
+ * once every slot has completed too, so done() calls after it stay safe. */
+void *ddl_completion_create(int count);
+int ddl_completion_slots(void *group, int first, int count, void **out);
+void ddl_completion_done(int status, void *user);
+int ddl_completion_wait(void *group, int index, double timeout_s, int *status);
+int ddl_completion_poll(void *group, int *statuses, int count);
+void ddl_completion_destroy(void *group);
 
 /* With "host_register_cache_bytes" > 0: the host range [ptr, ptr + bytes) is about to be freed —
  * call this BEFORE freeing (munmap / free / the framework's deallocator) any host tensor that was

@@ -174,6 +174,9 @@ int ddl_testing_control_fault(int on);
  * (its collective is not posted; -1 turns it off). The staged unpacks of the chunks before it
  * have all landed when the requests' done() reports the error. */
 int ddl_testing_host_coll_fault(long long chunk);
+/* A/B knob of the N-input fold's cache policy (reduce_kernels.hip fold_variant): 4 = plain loads +
+ * write-through store, 5 = non-temporal loads + write-through store, -1 = the size rule. */
+int ddl_testing_fold_variant(int variant);
 /* Mutation for the ordering tests: RingExecutor skips the reduce wait (wait_reduce) of program
  * tick `tick` (-1 restores the product behaviour). A test that cannot see this is blind. */
 int ddl_testing_drop_wait(int tick);

@@ -27,7 +27,8 @@ DEPLOYMENT = {
     'ddl_allreduce_host', 'ddl_tune_result', 'ddl_allreduce_submit', 'ddl_broadcast_submit',
     'ddl_allgather_submit', 'ddl_allreduce_submit_batch', 'ddl_allreduce_submit_mem',
     'ddl_allreduce_submit_batch_mem', 'ddl_broadcast_submit_mem', 'ddl_allgather_submit_mem', 'ddl_wait_all', 'ddl_host_unregister',
-    'ddl_kernel_timing', 'ddl_kernel_stats'}
+    'ddl_kernel_timing', 'ddl_kernel_stats', 'ddl_completion_create', 'ddl_completion_slots', 'ddl_completion_done',
+    'ddl_completion_wait', 'ddl_completion_poll', 'ddl_completion_destroy'}
 
 
 def declared_functions(header=HEADER):

@@ -417,8 +417,9 @@ def test_host_plan_failure_drains_unpacks(world, lib):
     chunk 8, past the 4 download slots, so unpack jobs of earlier chunks are queued on the unpack
     lane — reports the error only once every unpack already submitted has written its chunk:
     after done(error) the output never changes again (the caller may free it then). Chunks 0-7
-    hold the input, the rest is untouched; the next round on the same handler works (the lane's
-    error does not leak into it)."""
+    hold the input, the rest is untouched. A failed keyed collective stops its communicator's
+    handler by design (later submissions there are refused), so the fault runs on a split
+    communicator of its own; the world's handler keeps working."""
     import time
 
     import _helpers as h
@@ -427,22 +428,29 @@ def test_host_plan_failure_drains_unpacks(world, lib):
     chunk = 256 << 10
     x = torch.arange(3_000_017, dtype=torch.float32)
     out = torch.full_like(x, -7.0)
-    with h.config(lib, one_rank_shortcut=0, host_chunk_bytes=chunk, host_zero_copy=0):
-        assert lib.ddl_testing_host_coll_fault(8) == 0
-        try:
-            hd = allreduce_async(x, 'fault_plan', world, output=out)
-            with pytest.raises(DDLError):
-                hd.wait(timeout=60)
-            snap = out.clone()
-            time.sleep(0.3)
-            assert torch.equal(out, snap), 'the output changed after done(error)'
-        finally:
-            assert lib.ddl_testing_host_coll_fault(-1) == 0
-        k = 8 * chunk // 4
-        assert torch.equal(out[:k], x[:k])
-        assert bool((out[k:] == -7.0).all())
-        y = torch.arange(1_000_003, dtype=torch.float32)
-        assert torch.equal(allreduce_async(y, 'after_fault', world, output=torch.empty_like(y)).wait(timeout=60), y)
+    sub = world.split_communicator(0)
+    try:
+        with h.config(lib, one_rank_shortcut=0, host_chunk_bytes=chunk, host_zero_copy=0):
+            assert lib.ddl_testing_host_coll_fault(8) == 0
+            try:
+                hd = allreduce_async(x, 'fault_plan', sub, output=out)
+                with pytest.raises(DDLError):
+                    hd.wait(timeout=60)
+                snap = out.clone()
+                time.sleep(0.3)
+                assert torch.equal(out, snap), 'the output changed after done(error)'
+            finally:
+                assert lib.ddl_testing_host_coll_fault(-1) == 0
+            k = 8 * chunk // 4
+            assert torch.equal(out[:k], x[:k])
+            assert bool((out[k:] == -7.0).all())
+            with pytest.raises(DDLError):  # the failed handler refuses further requests
+                allreduce_async(x, 'after_fault', sub, output=out).wait(timeout=60)
+            y = torch.arange(1_000_003, dtype=torch.float32)
+            assert torch.equal(allreduce_async(y, 'world_after_fault', world, output=torch.empty_like(y)).wait(
+                timeout=60), y)
+    finally:
+        sub.detach()
 
 
 def test_registration_cache_address_reuse(world, lib):

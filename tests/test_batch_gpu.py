@@ -69,6 +69,30 @@ def test_thread_batch_bit_exact_per_bucket(lib, oracle, gpu, P, algo, dt):
             assert _host(outs[r][b], xs[r][b]).tobytes() == want, (b, n, r)
 
 
+@pytest.mark.parametrize('algo', [0, 1, 2])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_DOUBLE], ids=lambda d: NAME[d])
+def test_thread_batch_reference_order_0(lib, oracle, gpu, algo, dt):
+    """with reference_order 0 the grouped allreduce sums every bucket in the
+    batch schedule's order — the direct rank-order fold, or the one-shot left fold where one-shot
+    is asked for (a ring request runs as direct inside a batch) — as include/ddl_amd.h now states;
+    a solo call of a ring-tuned size class may differ in the last bits, so the claim of equality
+    with ddl_allreduce is made for reference_order 1 only (test above)."""
+    P = 5
+    ns = [300, 65_537, 1_000_003, 5]
+    xs = [[random_input(dt, n, 900 * r + 7 * b + algo) for b, n in enumerate(ns)] for r in range(P)]
+    ins = [[_dev(x, gpu) for x in row] for row in xs]
+    outs = [[torch.full_like(t, 0) for t in row] for row in ins]
+    with config(lib, algo=algo, reference_order=0, tune=0, slice_bytes=64 << 10):
+        st = _batch(lib.ddl_testing_thread_allreduce_batch, P, ins, outs, ns, dt)
+        assert st == 0, lib.ddl_last_error()
+        torch.cuda.synchronize()
+    for b, n in enumerate(ns):
+        col = [xs[r][b] for r in range(P)]
+        want = (oracle.fold(dt, col) if algo == 2 else oracle.allreduce_direct(dt, col)).tobytes()
+        for r in range(P):
+            assert _host(outs[r][b], xs[r][b]).tobytes() == want, (algo, b, n, r)
+
+
 @pytest.mark.parametrize('P', [3, 8])
 def test_rccl_loopback_batch(lib, oracle, gpu, P):
     """The same grouped program with every matched pair through RCCL (one-rank loopback): a tick's
