@@ -230,10 +230,14 @@ class _Completion:
         if lib.ddl_completion_wait(self.ptr, index, -1.0 if timeout is None else float(timeout),
                                    ctypes.byref(st)) != cb.STATUS_OK:
             raise TimeoutError('request did not complete')
-        if self.count > 1 and lib.ddl_completion_poll(self.ptr, None, 0) == 0:
+        if lib.ddl_completion_poll(self.ptr, None, 0) == 0:
+            # every slot completed: cache the statuses and let the tensors go (a host tensor's
+            # storage finalizer may release its registration now, as with the reference's op,
+            # whose inputs are released when its done() has run)
             arr = (ctypes.c_int * self.count)()
             lib.ddl_completion_poll(self.ptr, arr, self.count)
             self.final = list(arr)
+            self.keep = None
         return st.value
 
     def fail(self, indices, status):
@@ -242,6 +246,8 @@ class _Completion:
         slots = self.slots()
         for i in indices:
             lib.ddl_completion_done(status, slots[i])
+        if lib.ddl_completion_poll(self.ptr, None, 0) == 0:
+            self.keep = None
 
 
 _NATIVE_DONE = []

@@ -341,11 +341,13 @@ int ddl_kernel_stats(ddl_communicator_id id, long long *launches, double *bytes,
 }
 #endif
 
-/* Transition aid (r03 moved the test / diagnostic entry points — ddl_init_test_transport,
- * ddl_p2p_op, ddl_control_negotiate*, ddl_allreduce_variant, ddl_reduce_*, ddl_pack / ddl_unpack,
- * ddl_local_*, the schedule introspection — into ddl_amd_testing.h; the symbols are still
- * exported): define DDL_AMD_WITH_TESTING_API before including this header to get them as before.
- * ddl_init_test_transport also needs DDL_ALLOW_TEST_TRANSPORT=1 in the environment. */
+/* The test / diagnostic entry points (ddl_init_test_transport, ddl_p2p_op, ddl_control_negotiate*,
+ * ddl_allreduce_variant, ddl_reduce_*, ddl_pack / ddl_unpack, ddl_local_*, ddl_testing_*,
+ * ddl_rccl_loopback_*, the schedule introspection) are declared in ddl_amd_testing.h and exported
+ * only by lib/libddl_amd_testing.so (the same engine objects plus the harness); lib/libddl_amd.so
+ * exports exactly this header. Define DDL_AMD_WITH_TESTING_API before including this header to
+ * get both (and link the testing library). ddl_init_test_transport also needs
+ * DDL_ALLOW_TEST_TRANSPORT=1 in the environment. */
 #ifdef DDL_AMD_WITH_TESTING_API
 #include "ddl_amd_testing.h"
 #endif

@@ -93,13 +93,18 @@ def test_torch_mirror_handles_over_a_group(lib):
         hs[0].wait(timeout=0.01)
     assert grp in tc._Completion._inflight
     lib.ddl_completion_done(0, grp.slots()[0])
-    assert hs[0].done() and hs[0].wait() is a and grp.final is None
-    grp.fail([1], 7)  # a refused submission
+    assert hs[0].done() and hs[0].wait() is a and grp.final is None and grp.keep is not None
+    grp.fail([1], 7)  # a refused submission: every slot complete, the tensors are let go
+    assert grp.keep is None
     with pytest.raises(DDLError) as e:
         hs[1].wait(timeout=1)
     assert e.value.status == 7 and grp.final == [0, 7]
-    tc._Completion(0, ())  # the next group sweeps the completed one: its tensors are released
-    assert grp not in tc._Completion._inflight and grp.keep is None
+    tc._Completion(0, ())  # the next group sweeps the completed one
+    assert grp not in tc._Completion._inflight
+    one = tc._Completion(1, (a,))  # a single request: its wait() releases the tensors
+    h = tc._NativeHandle('c', a, (a,), one, 0)
+    lib.ddl_completion_done(0, one.slots()[0])
+    assert h.wait() is a and one.keep is None and one.final == [0]
 
 
 def test_native_completion_is_cheaper_than_python_callbacks(lib):
