@@ -1135,6 +1135,22 @@ def multi_gpu(args):
     except Exception as e:
         out['parity_vs_mpich_order'] = {'bit_exact': False, 'error': repr(e)[:400]}
 
+    # the reference's own CPU+MPI path at this N, on the host cores: rank 0
+    # runs oracle/ref_path_port.c under MPICH at P = N on the C3 shape (cpu_baseline) and the C1 /
+    # C3 / C5-like legs (cpu_reference_path) while the other ranks wait at the barrier — no GPU
+    # work runs meanwhile. Right after the parity leg, so a later optional leg that hangs (the
+    # watchdog then prints the line as it stands) cannot cost the line its baseline. Path restated:
+    # RingTokenCommunicateHandler.cc:327-410 -> MPIRingTokenCommunication.cc:548-733 ->
+    # MPICommunicator.cc:14-28.
+    state['leg'] = 'cpu_baseline'
+    dist.barrier()
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            out['cpu_baseline'] = cpu_baseline(P=world, reps=4)
+            out['cpu_reference_path'] = cpu_reference_path()
+        except Exception as e:  # a failed optional leg must not cost the headline line
+            out.setdefault('leg_errors', {})['cpu_baseline'] = repr(e)[:400]
+    dist.barrier()
     state['leg'] = 'rccl_comparator'
     try:
         if not args.rehearse:
@@ -1349,20 +1365,6 @@ def multi_gpu(args):
                 del graph, a, b
     except Exception as e:  # e.g. the rehearsal's host-synchronising transport cannot be captured
         out.setdefault('leg_errors', {})['size_sweep_graph'] = repr(e)[:400]
-    # the reference's own CPU+MPI path at this N, on the host cores, after every GPU leg (VERDICT
-    # r4 next #1): rank 0 runs oracle/ref_path_port.c under MPICH at P = N on the C3 shape
-    # (cpu_baseline) and the C1 / C3 / C5-like legs (cpu_reference_path) while the other ranks
-    # wait at the barrier. Path restated: RingTokenCommunicateHandler.cc:327-410 ->
-    # MPIRingTokenCommunication.cc:548-733 -> MPICommunicator.cc:14-28.
-    state['leg'] = 'cpu_baseline'
-    dist.barrier()
-    if rank == 0 and not args.no_cpu_baseline:
-        try:
-            out['cpu_baseline'] = cpu_baseline(P=world, reps=4)
-            out['cpu_reference_path'] = cpu_reference_path()
-        except Exception as e:  # a failed optional leg must not cost the headline line
-            out.setdefault('leg_errors', {})['cpu_baseline'] = repr(e)[:400]
-    dist.barrier()
     state['leg'] = 'finalize'
     if rank == 0:
         emit(out)

@@ -1,13 +1,13 @@
 #!/bin/bash
 # CPU tests against the host-sanitized engine (AddressSanitizer + UBSan on the C++ host runtime:
 # schedules, program dumps, config, plans, control plane; GPU code is not sanitized — not
-# available on this pool). Builds lib/asan/libddl_amd.so, runs the CPU suite with it through
+# available on this pool). Builds lib/asan/libddl_amd_testing.so, runs the CPU suite with it through
 # the reference's `ddl_lib` override, then removes the sanitized build (it never ships).
 set -u
 cd "$(dirname "$0")/.."
 make -C experiment-distributed-deep-learning_amd/csrc asan -j8 > /dev/null || exit 2
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
-export ddl_lib=$PWD/experiment-distributed-deep-learning_amd/lib/asan/libddl_amd.so
+export ddl_lib=$PWD/experiment-distributed-deep-learning_amd/lib/asan/libddl_amd_testing.so
 export ASAN_OPTIONS=detect_leaks=0:alloc_dealloc_mismatch=0:detect_odr_violation=0:halt_on_error=1:abort_on_error=1
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
 LD_PRELOAD=$RT timeout -k 10 ${RT_S:-1500} python -m pytest tests -q -x -m "not gpu" -p no:cacheprovider "$@"
