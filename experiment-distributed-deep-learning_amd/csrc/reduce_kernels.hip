@@ -245,12 +245,18 @@ __device__ __forceinline__ typename Acc<DT>::T fold_values(typename Acc<DT>::T *
 constexpr int kReduceThreads = 128;
 
 // Fold cache policy (FV bits): 1 non-temporal loads, 2 non-temporal store, 4 write-through
-// (sc0 sc1) store. Chunks above 8 MiB stream every input once: non-temporal loads, and the output
-// written through (it leaves the XCD's L2 at once; r03 tools/fold_tune.hip at 32 MiB, 8 inputs:
-// 6.48-6.51 TB/s vs 6.35-6.36 all-nt, the r02 policy). Chunks up to 8 MiB (their operands fit the
-// 256 MiB Infinity Cache, where RCCL has just written the received slices) read through the
-// caches: 5.53 vs 5.05 TB/s at 4 MiB (plain loads + write-through store vs all-nt).
-int fold_variant(size_t chunk_bytes) { return chunk_bytes <= (8u << 20) ? 4 : 5; }
+// (sc0 sc1) store. Launches of more than 4 MiB per input stream every input once: non-temporal
+// loads, and the output written through (it leaves the XCD's L2 at once; r03 tools/fold_tune.hip
+// at 32 MiB, 8 inputs: 6.48-6.51 TB/s vs 6.35-6.36 all-nt, the r02 policy). Up to 4 MiB per input
+// (the operands of a 2 MiB slice, where RCCL has just written the received data) read through the
+// caches. r05 interleaved A/B of plain (4) vs non-temporal (5) loads, P = 8, one fold per launch,
+// operands cache-resident / HBM-resident (tools/fold_batch_policy_ab.py, profiles/r05/s5/):
+// 2 MiB fp16 3.7 / 5.7 us (4) vs 4.8 / 5.4 (5); 3 MiB fp32 4.0 / 7.3 vs 5.6 / 7.0; 4 MiB 4.8 / 8.8
+// vs 5.7 / 8.1 — and from 5 MiB on the non-temporal loads win both ways (5 MiB 9.5 / 12.0 vs
+// 8.6 / 10.9; 8 MiB 12.8 / 15.5 vs 12.0 / 14.0; 12 MiB 18.3 / 23.2 vs 16.8 / 20.8). r02-r04 split at
+// 8 MiB. A batched launch (FoldBatch) goes by its summed bytes per input: 8 chunks of 2 MiB read
+// non-temporally (26.2 vs 28.9 us from HBM, 23.3 vs 23.9 cache-resident).
+int fold_variant(size_t chunk_bytes) { return chunk_bytes <= (4u << 20) ? 4 : 5; }
 // ddl_testing_fold_variant: forces the policy (4 or 5; -1 = fold_variant's rule) for A/Bs
 std::atomic<int> g_fold_variant{-1};
 

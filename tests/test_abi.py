@@ -76,6 +76,13 @@ def test_deployment_library_exports_exactly_the_header():
                line.split()[1] not in 'Aw'), 'the deployment library exports data or weak symbols'
 
 
+def test_torch_mirror_requires_exactly_the_deployment_surface():
+    """The torch mirror refuses a library that lacks any deployment entry point, and its list is
+    the header's (cpp_backend.DEPLOYMENT_API)."""
+    from ddl.torch import cpp_backend
+    assert set(cpp_backend.DEPLOYMENT_API) == set(declared_functions())
+
+
 def test_testing_library_exports_both_headers():
     exported = _exported(TESTING_LIB)
     declared = declared_functions() + declared_functions(TESTING_HEADER)
