@@ -206,7 +206,10 @@ def cpu_reference_path():
 NSETS = 3  # rotating buffer sets: >= 2 x 768 MiB of traffic between reuses of one set, so the
            # 256 MiB Infinity Cache cannot serve a re-read (MI355X_MICROARCH.md §Infinity Cache)
 VARIANTS = {'default': -1, 'plain': 0, 'nt_load_a': 1, 'nt_load_ab': 3, 'nt_all': 7, 'lds_stage_b': 8,
-            'lds_stage_b_nt_a': 9, 'wt_store': 16, 'nt_load_ab_wt_store': 19}
+            'lds_stage_b_nt_a': 9, 'wt_store': 16, 'nt_load_ab_wt_store': 19,
+            # run form (bit 32: 8-tile runs per workgroup, a then b; bit 64: 4-tile runs), r05 A/B
+            'run8_nt_all': 32 | 7, 'run8_nt_load_ab_wt_store': 32 | 19, 'run4_nt_all': 96 | 7,
+            'run4_nt_load_ab_wt_store': 96 | 19}
 
 
 GRAPH_SWEEP_MAX = 8 << 20  # sweep points also timed as hipGraph replays (launch-bound sizes)

@@ -324,7 +324,7 @@ int ddl_local_tune(int nranks, size_t elements, int dtype, void *hip_stream, int
 int ddl_reduce_sum2_variant(int variant, void *out, const void *a, const void *b, size_t elements,
                             int dtype, void *hip_stream) {
     return guarded([&] {
-        DDL_REQUIRE(variant >= -1 && variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
+        DDL_REQUIRE(variant >= -1 && variant <= (kVariantMask | kRunForm | kRun4), DDL_STATUS_INVALID_ARGUMENT, "variant " << variant);
         SegTable t;
         t.count = 1;
         t.a[0] = a;

@@ -184,6 +184,50 @@ __global__ void __launch_bounds__(THREADS) k_sum2_tile(SegTable t) {
     }
 }
 
+// Run form of the two-input reduce (measurement variant kRunForm, r05): a 128-lane workgroup owns
+// U consecutive 2 KiB tiles; each lane loads its U vectors of a, then its U vectors of b, then
+// stores the U sums — so a workgroup streams one operand at a time in U * 2 KiB runs (the fold's
+// run form, §5.2). Tail elements as k_sum2_tile's (the lanes of the run holding nv).
+template <int DT, int VARIANT, int U>
+__global__ void __launch_bounds__(128) k_sum2_run(SegTable t) {
+    using A = Add<DT>;
+    using S = typename A::S;
+    constexpr uint64_t V = 16 / sizeof(S);
+    constexpr uint64_t kRun = 128ull * U;  // 16-byte vectors per run
+    const int seg = blockIdx.y;
+    const uint64_t n = t.n[seg];
+    const uint64_t nv = n / V;
+    const uint64_t base = (uint64_t)blockIdx.x * kRun;
+    const u32x4 *a = static_cast<const u32x4 *>(t.a[seg]);
+    const u32x4 *b = static_cast<const u32x4 *>(t.b[seg]);
+    u32x4 *o = static_cast<u32x4 *>(t.out[seg]);
+    if (base < nv) {
+        const int bytes = (int)((nv - base < kRun ? nv - base : kRun) * 16);
+        const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(a + base), 0, bytes, kRsrcWord3);
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4 *>(b + base), 0, bytes, kRsrcWord3);
+        const auto ro = __builtin_amdgcn_make_buffer_rsrc(o + base, 0, bytes, kRsrcWord3);
+        const int off = (int)threadIdx.x * 16;
+        u32x4 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, off + u * 2048, 0, (VARIANT & kNtLoadA) ? kAuxNt : 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, off + u * 2048, 0, (VARIANT & kNtLoadB) ? kAuxNt : 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(A::vec(x[u], y[u]), ro, off + u * 2048, 0, store_aux(VARIANT));
+    }
+    const uint64_t rem = n - nv * V;
+    if (rem && blockIdx.x == nv / kRun && threadIdx.x < rem) {
+        const uint64_t e = nv * V + threadIdx.x;
+        const S *as = reinterpret_cast<const S *>(t.a[seg]);
+        const S *bs = reinterpret_cast<const S *>(t.b[seg]);
+        S *os = reinterpret_cast<S *>(t.out[seg]);
+        os[e] = A::one(as[e], bs[e]);
+    }
+}
+
 // ---- N-input fold (direct schedule) --------------------------------------------------------
 // Accumulator type: fp32 for fp16/bf16 (one rounding at the end), the element type otherwise.
 template <int DT>
@@ -580,8 +624,32 @@ void launch_variant(const SegTable &t, hipStream_t stream, int variant, dim3 gri
     }
 }
 
+template <int DT, int U>
+void launch_run(const SegTable &t, hipStream_t stream, int policy, uint64_t max_n) {
+    constexpr uint64_t V = 16 / sizeof(typename Add<DT>::S);
+    const uint64_t runs = (max_n / V + 128ull * U) / (128ull * U);  // +1 vector of room for the tail
+    DDL_REQUIRE(runs < (1ull << 31), DDL_STATUS_INVALID_ARGUMENT, "segment too large: " << max_n << " elements");
+    const dim3 grid((unsigned)runs, t.count);
+    switch (policy) {  // the cache-bit combinations the N = 1 bench compares
+        case 0: hipLaunchKernelGGL((k_sum2_run<DT, 0, U>), grid, dim3(128), 0, stream, t); break;
+        case kWtStore: hipLaunchKernelGGL((k_sum2_run<DT, kWtStore, U>), grid, dim3(128), 0, stream, t); break;
+        case kNtLoadA | kNtLoadB | kWtStore:
+            hipLaunchKernelGGL((k_sum2_run<DT, kNtLoadA | kNtLoadB | kWtStore, U>), grid, dim3(128), 0, stream, t);
+            break;
+        case kNtLoadA | kNtLoadB | kNtStore:
+            hipLaunchKernelGGL((k_sum2_run<DT, kNtLoadA | kNtLoadB | kNtStore, U>), grid, dim3(128), 0, stream, t);
+            break;
+        default: fail(DDL_STATUS_INVALID_ARGUMENT, "run-form reduce: cache policy " + std::to_string(policy));
+    }
+}
+
 template <int DT>
 void launch_dt(const SegTable &t, hipStream_t stream, int variant, bool aligned, uint64_t max_n) {
+    if (aligned && (variant & kRunForm)) {
+        if (variant & kRun4) launch_run<DT, 4>(t, stream, variant & kVariantMask, max_n);
+        else launch_run<DT, 8>(t, stream, variant & kVariantMask, max_n);
+        return;
+    }
     if (!aligned) {
         uint64_t blocks = (max_n + kThreads * 4 - 1) / (kThreads * 4);
         const uint64_t cap = (uint64_t)device_cu_count() * 8;
@@ -716,7 +784,7 @@ void launch_sum2(const SegTable &t, int dtype, hipStream_t stream, int variant) 
     }
     if (max_n == 0) return;
     if (variant < 0) variant = default_variant((size_t)total_n * es);
-    DDL_REQUIRE(variant <= kVariantMask, DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant " << variant);
+    DDL_REQUIRE(variant <= (kVariantMask | kRunForm | kRun4), DDL_STATUS_INVALID_ARGUMENT, "bad reduce variant " << variant);
     switch (dtype) {
         case DDL_FLOAT: launch_dt<DDL_FLOAT>(t, stream, variant, aligned, max_n); break;
         case DDL_DOUBLE: launch_dt<DDL_DOUBLE>(t, stream, variant, aligned, max_n); break;

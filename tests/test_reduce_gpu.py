@@ -56,6 +56,23 @@ def test_variants_agree(lib, oracle, gpu, variant, dt):
     assert from_dev(to, a).tobytes() == oracle.sum2(dt, a, b).tobytes()
 
 
+@pytest.mark.parametrize('variant', [32, 32 | 16, 32 | 19, 32 | 7, 96 | 7, 96 | 19])
+@pytest.mark.parametrize('dt', [DT_FLOAT, DT_HALF, DT_BFLOAT16, 3, 2], ids=lambda d: str(d))
+@pytest.mark.parametrize('n', [1, 7, 128 * 4 * 8 - 1, 128 * 4 * 8 + 5, (1 << 20) + 77])
+def test_run_form_variants_agree(lib, oracle, gpu, variant, dt, n):
+    """The run form of the two-input reduce (variant bit 32: a workgroup streams an 8-tile run of a,
+    then of b; bit 64: 4-tile runs), in place and out of place, ragged lengths around a run."""
+    a, b = random_input(dt, n, 33), random_input(dt, n, 34)
+    ta, tb = to_dev(a, gpu), to_dev(b, gpu)
+    to = torch.empty_like(ta)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.ddl_reduce_sum2_variant(variant, to.data_ptr(), ta.data_ptr(), tb.data_ptr(), n, dt, s) == 0
+    assert lib.ddl_reduce_sum2_variant(variant, ta.data_ptr(), ta.data_ptr(), tb.data_ptr(), n, dt, s) == 0
+    torch.cuda.synchronize()
+    want = oracle.sum2(dt, a, b).tobytes()
+    assert from_dev(to, a).tobytes() == want and from_dev(ta, a).tobytes() == want
+
+
 @pytest.mark.parametrize('offset', [1, 2, 3])
 def test_misaligned_buffers(lib, oracle, gpu, offset):
     """Sub-tensor views that are not 16-byte aligned take the scalar path, same result."""
