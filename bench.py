@@ -380,7 +380,9 @@ def single_gpu(args):
                    'bucket_bytes': S, 'parallelism': 'none (1 GPU)'},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'k_sum2_tile<DDL_FLOAT, default variant>', 'kernel_ms': round(kernel_ms, 4),
+                     'kernel': ('k_sum2_run<DDL_FLOAT, default variant, 4 tiles>' if 32 <= args.bucket_mib < 128 and
+                                args.variant < 0 else 'k_sum2_tile<DDL_FLOAT, default variant>'),
+                     'kernel_ms': round(kernel_ms, 4),
                      'algorithmic_bytes_per_launch': 3 * S,
                      'frac_of_measured_copy_peak': round(achieved / HBM_MEASURED_GBS, 4)},
     }

@@ -163,9 +163,10 @@ enum ReduceVariant : int {
     kLdsStageB = 8, // operand b staged through LDS by global_load_lds_dwordx4
     kWtStore = 16,  // write-through stores of out (sc0 sc1: the line leaves the XCD's L2)
     kVariantMask = 31,
-    // run form (r05 A/B, measurement only): one workgroup per run of 8 tiles (kRun4: 4 tiles), a's
-    // run loaded, then b's, then the stores — each workgroup on one stream at a time, as the fold's
-    // run form (cache bits from the low bits; the LDS staging bit is not combined with it)
+    // run form (r05): one workgroup per run of 8 tiles (kRun4: 4 tiles), a's run loaded, then
+    // b's, then the stores — each workgroup on one stream at a time, as the fold's run form (cache
+    // bits from the low bits; the LDS staging bit is not combined with it). default_variant takes
+    // it with 4-tile runs from 32 to 128 MiB.
     kRunForm = 32,
     kRun4 = 64,
 };

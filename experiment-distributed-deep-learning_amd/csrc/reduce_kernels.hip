@@ -748,18 +748,23 @@ void launch_sumN_batch(const SegTableN *t, int count, int dtype, hipStream_t str
 void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) { launch_sumN_batch(&t, 1, dtype, stream); }
 
 // Standalone reduce (acc += in over whole buckets) of `bytes` per operand, by bucket size
-// (3 rotating buffer sets per size, profiles/r02/reduce_policy/):
+// (3 rotating buffer sets per size, profiles/r02/reduce_policy/, profiles/r05/s6/):
 //   * from 256 MiB every access is non-temporal: the bucket streams through once (6.8 TB/s at
 //     256 MiB; write-through stores 0.5-0.8 % slower there);
 //   * 32-256 MiB: non-temporal loads, write-through stores (64 MiB: 7.5 vs 6.6 TB/s all-nt;
-//     128 MiB: 6.9 vs 6.7);
+//     128 MiB: 6.9 vs 6.7); below 128 MiB in the run form with 4-tile runs (r05,
+//     tools/reduce_run_ab.py: 32 MiB 6.32 vs 5.97 TB/s for the tile form, 64 MiB 6.88 vs 6.50 —
+//     where part of the 3 x 3 operand sets stays in the Infinity Cache, a workgroup streaming one
+//     operand at a time wins; from 128 MiB, pure HBM streaming, the tile form does: 6.70 vs 6.27
+//     at 256 MiB, 6.72 vs 6.17 at 512 MiB);
 //   * below 32 MiB: plain loads — the operands of a small bucket are likely still in the
 //     Infinity Cache from whoever produced them — and write-through stores (16 MiB: 6.7 vs 6.4
-//     TB/s plain stores).
-constexpr size_t kNtMinBytes = 32u << 20, kNtStoreMinBytes = 256u << 20;
+//     TB/s plain stores; the run form ties there, 6.15 vs 6.10).
+constexpr size_t kNtMinBytes = 32u << 20, kRunMaxBytes = 128u << 20, kNtStoreMinBytes = 256u << 20;
 int default_variant(size_t bytes) {
     if (bytes >= kNtStoreMinBytes) return kNtLoadA | kNtLoadB | kNtStore;
-    if (bytes >= kNtMinBytes) return kNtLoadA | kNtLoadB | kWtStore;
+    if (bytes >= kRunMaxBytes) return kNtLoadA | kNtLoadB | kWtStore;
+    if (bytes >= kNtMinBytes) return kRunForm | kRun4 | kNtLoadA | kNtLoadB | kWtStore;
     return kWtStore;
 }
 
