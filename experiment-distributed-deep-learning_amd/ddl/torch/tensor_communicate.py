@@ -12,6 +12,7 @@ synchronise the host. A host (CPU) tensor â€” the reference's deployment case â€
 through pinned memory to the GPU, reduced there and copied back.
 """
 import bisect
+import collections
 import ctypes
 import itertools
 import threading
@@ -194,7 +195,7 @@ class _Completion:
     dropped without wait() cannot free memory the engine still reads or writes; the engine frees
     the group once its owner let go AND every slot completed."""
     __slots__ = ('ptr', 'count', 'keep', 'final', '__weakref__')
-    _inflight = []  # groups with slots still pending: keep their tensors alive
+    _inflight = collections.deque()  # groups in submission order, slots maybe pending: their tensors
     _inflight_lock = threading.Lock()
 
     def __init__(self, count: int, keep):
@@ -205,14 +206,13 @@ class _Completion:
         self.count, self.keep, self.final = count, keep, None
         weakref.finalize(self, lib.ddl_completion_destroy, self.ptr)
         with _Completion._inflight_lock:
-            live = []
-            for g in _Completion._inflight:
-                if lib.ddl_completion_poll(g.ptr, None, 0) > 0:
-                    live.append(g)
-                else:
-                    g.keep = None
-            live.append(self)
-            _Completion._inflight = live
+            # release the oldest groups that completed (the engine completes rounds in submission
+            # order, so the sweep stops at the first pending one: O(1) amortised per submission,
+            # also with one group per gradient under overlap_backward)
+            q = _Completion._inflight
+            while q and (q[0].keep is None or lib.ddl_completion_poll(q[0].ptr, None, 0) == 0):
+                q.popleft().keep = None
+            q.append(self)
 
     def slots(self, first: int = 0, count: int = None):
         """The `user` pointers of slots [first, first + count) (a ctypes array)."""
