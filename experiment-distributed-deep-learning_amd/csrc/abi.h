@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "common.h"
+#include "engine.h"
 
 namespace ddl {
 namespace abi {
@@ -47,6 +48,24 @@ inline std::vector<std::string> split_endpoints(const char *endpoints) {
         pos = sc + 1;
     }
     return eps;
+}
+
+// A tuning table (TuneResult) into the C-ABI's arrays: per candidate {algo, rings, slice_bytes,
+// max_slices} and its agreed milliseconds (ddl_tune_result, ddl_local_tune, ddl_rccl_loopback_tune).
+inline void export_tune(const TuneResult &r, int *chosen, int *count, long long *configs, float *ms, int max_candidates) {
+    DDL_REQUIRE(chosen && count, DDL_STATUS_INVALID_ARGUMENT, "null output");
+    *chosen = r.chosen;
+    *count = (int)r.candidates.size();
+    for (int i = 0; i < *count && i < max_candidates; ++i) {
+        const RingConfig &c = r.candidates[i];
+        if (configs) {
+            configs[4 * i + 0] = c.algo;
+            configs[4 * i + 1] = c.rings;
+            configs[4 * i + 2] = (long long)c.slice_bytes;
+            configs[4 * i + 3] = c.max_slices;
+        }
+        if (ms) ms[i] = r.ms[i];
+    }
 }
 
 }  // namespace abi

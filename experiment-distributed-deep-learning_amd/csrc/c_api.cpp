@@ -296,24 +296,6 @@ int ddl_comm_transport(ddl_communicator_id id, int *kind, int *ranks) {
     });
 }
 
-namespace {
-void export_tune(const TuneResult &r, int *chosen, int *count, long long *configs, float *ms, int max_candidates) {
-    DDL_REQUIRE(chosen && count, DDL_STATUS_INVALID_ARGUMENT, "null output");
-    *chosen = r.chosen;
-    *count = (int)r.candidates.size();
-    for (int i = 0; i < *count && i < max_candidates; ++i) {
-        const RingConfig &c = r.candidates[i];
-        if (configs) {
-            configs[4 * i + 0] = c.algo;
-            configs[4 * i + 1] = c.rings;
-            configs[4 * i + 2] = (long long)c.slice_bytes;
-            configs[4 * i + 3] = c.max_slices;
-        }
-        if (ms) ms[i] = r.ms[i];
-    }
-}
-}  // namespace
-
 int ddl_tune_result(ddl_communicator_id id, size_t bucket_bytes, int *chosen, int *count, long long *configs,
                     float *ms, int max_candidates) {
     return guarded([&] {

@@ -155,23 +155,7 @@ struct RegisterFinalize {
     RegisterFinalize() { add_finalize_hook(&testing_finalize); }
 } g_register_finalize;
 
-void export_tune(const TuneResult &r, int *chosen, int *count, long long *configs, float *ms, int max_candidates) {
-    DDL_REQUIRE(chosen && count, DDL_STATUS_INVALID_ARGUMENT, "null output");
-    *chosen = r.chosen;
-    *count = (int)r.candidates.size();
-    for (int i = 0; i < *count && i < max_candidates; ++i) {
-        const RingConfig &c = r.candidates[i];
-        if (configs) {
-            configs[4 * i + 0] = c.algo;
-            configs[4 * i + 1] = c.rings;
-            configs[4 * i + 2] = (long long)c.slice_bytes;
-            configs[4 * i + 3] = c.max_slices;
-        }
-        if (ms) ms[i] = r.ms[i];
-    }
-}
 }  // namespace
-
 
 extern "C" {
 
