@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BARGS="--steps 30 --warmup 5 --no-sweep --no-cpu-baseline --no-forced-data-plane ${EXTRA_BARGS:-}"
+BARGS="--steps 30 --warmup 5 --no-sweep --no-cpu-baseline --no-forced-data-plane --no-host-steady ${EXTRA_BARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 bench.py $BARGS > $OUT/bench_trace.json 2> $OUT/trace.err
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/trace.err; exit $rc; }
 for C in FETCH_SIZE WRITE_SIZE; do

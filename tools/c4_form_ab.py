@@ -1,6 +1,7 @@
 """C4 fp16 fold (2 MiB chunk, P = 8) in the tile vs the run form, bench.fold_roofline timing (measurement)."""
 import sys, os, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib', 'libddl_amd_testing.so'))  # the testing build (raw kernels, test transport)
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
 import torch, bench
 from ddl.torch.cpp_backend import CPPBackend

@@ -12,6 +12,7 @@ import time
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib', 'libddl_amd_testing.so'))  # the testing build (raw kernels, test transport)
 sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
 from ddl.torch.cpp_backend import CPPBackend  # noqa: E402

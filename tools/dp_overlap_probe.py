@@ -16,6 +16,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib', 'libddl_amd_testing.so'))  # the testing build (raw kernels, test transport)
 for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), os.path.join(ROOT, 'tools')):
     sys.path.insert(0, p)
 

@@ -5,6 +5,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib', 'libddl_amd_testing.so'))  # the testing build (raw kernels, test transport)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
 import torch  # noqa: E402

@@ -13,6 +13,7 @@ import time
 import multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib', 'libddl_amd_testing.so'))  # the testing build (raw kernels, test transport)
 sys.path.insert(0, os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'))
 
 KEYS = [f'grad_{i:05d}' for i in range(int(os.environ.get('NEG_KEYS', 4096)))]

@@ -11,6 +11,9 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
+# the workers need the test transport: the testing build (the spawned processes inherit this)
+os.environ.setdefault('ddl_lib', os.path.join(ROOT, 'experiment-distributed-deep-learning_amd', 'lib',
+                                              'libddl_amd_testing.so'))
 
 
 def _free_port():
