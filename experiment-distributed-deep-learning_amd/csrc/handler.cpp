@@ -346,9 +346,9 @@ RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
                     "keyed requests at size > 1 need the communicator's token ring (ddl_control_connect for the "
                     "world; split_communicator builds one for every split)");
         // the private data-plane communicator made with the ring (Communicator::enable_keyed)
-        data_ = owner_->keyed_data();
+        data_ = owner_->keyed_data().get();
     } else {
-        data_ = owner_->shared_from_this();
+        data_ = owner_;
     }
     // the fusion pack / unpack kernels overlap other plans' RCCL kernels at size > 1: the same CU
     // mask as the executors' compute streams (config compute_cu_mask; pack / unpack keep their

@@ -292,7 +292,10 @@ private:
 
     Communicator *owner_;
     ControlChannel *ch_ = nullptr;        // the owner's token ring (size > 1)
-    std::shared_ptr<Communicator> data_;  // private data-plane communicator
+    // the data plane: the owner's private keyed communicator at size > 1, the owner itself at
+    // size 1. Not owning: the owner holds keyed_data_ and destroys this handler first; an owning
+    // pointer to the owner was a cycle that kept a detached size-1 split (and these threads) alive
+    Communicator *data_ = nullptr;
     hipStream_t stream_ = nullptr;
     // multi-request plans: pack -> allreduce -> unpack, pipelined in sub-plans above
     // fusion_pipeline_bytes (fusion.h); its buffer 0 also packs broadcast / allgather plans

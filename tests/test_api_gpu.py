@@ -3,6 +3,8 @@ Communicator, allreduce / allreduce_gradient, keyed async requests with fusion, 
 data-parallel optimizer wrapper. At size 1 the sum is the tensor itself (the reference hangs
 there; the build defines out = in)."""
 import ctypes
+import gc
+import os
 
 import numpy as np
 import pytest
@@ -285,6 +287,30 @@ def test_split_size1(world):
     x = torch.arange(10.0, device='cuda')
     assert torch.equal(allreduce(x, sub), x)
     sub.detach()
+
+
+def test_split_size1_keyed_detach_joins_handler(world):
+    """A size-1 split that ran keyed requests starts a request handler (two threads); detach must
+    destroy the split and join them. r05's soak found rank 4 at P = 5 (a size-1 pair) gaining two
+    threads per round: the handler held an owning pointer to its own communicator, a cycle."""
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+
+    def keyed_round(i):
+        sub = world.split_communicator(0)
+        xs = [torch.full((100 + j,), float(i + j), device='cuda') for j in range(3)]
+        for hd, x in zip(allreduce_async_batch(xs, [f'leak_{j}' for j in range(3)], sub), xs):
+            assert torch.equal(hd.wait(timeout=60), x)
+        sub.detach()
+
+    def threads():
+        gc.collect()
+        return len(os.listdir('/proc/self/task'))
+
+    keyed_round(0)  # lazily started pools / threads settle first
+    n0 = threads()
+    for i in range(1, 6):
+        keyed_round(i)
+    assert threads() <= n0 + 1, (n0, threads())
 
 
 def test_rccl_comparator_entry_size1(world, lib):
