@@ -820,9 +820,9 @@ def keyed_host_c5_steady(comm, steps=10, warm=2, k=4096, budget_s=25.0):
     memcpy out, MPIRingTokenCommunication.cc:575-588), `steps` consecutive batches in one process:
       * fresh: a NEW tensor set every step (the old one freed), registration cache off — a loop
         that reduces freshly computed CPU tensors — through the torch mirror
-        (allreduce_async_batch: one Python done() per tensor, Handle.wait per tensor);
+        (allreduce_async_batch: one native completion group for the batch, Handle.wait per tensor);
       * fresh_native: the same sets through the C-ABI directly (no done callback, ddl_wait_all):
-        the difference to `fresh` is the Python completion path;
+        the difference to `fresh` is the mirror's Python (handles, argument arrays, per-tensor waits);
       * fresh_registered: `fresh` with the registration cache on (host_register_cache_bytes):
         every step registers its new pages, the freed ones leave the cache via the torch mirror's
         storage finalizers;

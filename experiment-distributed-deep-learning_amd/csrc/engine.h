@@ -150,7 +150,7 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
                       const std::function<void(const RingConfig &)> &run,
                       const std::function<void(float *, int)> &agree_max);
 
-class Communicator : public std::enable_shared_from_this<Communicator> {
+class Communicator {
 public:
     // `hooks` (test harness only, ddl_init_test_transport): groups go to host callbacks, `tag`
     // names this communicator to them, `world_ranks[i]` is the world rank of rank i (empty: the
