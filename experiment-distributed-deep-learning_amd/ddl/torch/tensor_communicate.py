@@ -161,6 +161,7 @@ def allgather(tensor: torch.Tensor, communicator: Communicator = None) -> torch.
 # ---- keyed asynchronous requests -----------------------------------------------------------
 class Handle:
     """Completion handle of a keyed request (the TF op's pending `done` callback)."""
+    __slots__ = ('key', 'output', '_keep', '_event', 'status', '__dict__', '__weakref__')
 
     def __init__(self, key: str, output: torch.Tensor, keep_alive):
         self.key = key
@@ -263,6 +264,7 @@ def _native_done():
 
 class _NativeHandle(Handle):
     """Handle of a request completed through a completion group (no Python done callback)."""
+    __slots__ = ('_group', '_index')
 
     def __init__(self, key: str, output: torch.Tensor, keep_alive, group: _Completion, index: int):
         # (no threading.Event: the slot is the completion)
@@ -419,23 +421,31 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     k = len(tensors)
     if k == 0:
         return []
-    mems = [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
+    in_place = all(o is t for t, o in zip(tensors, outputs))  # the DP wrapper's form
+    mems = [memory_kind(t, 'allreduce_async_batch input') for t in tensors] if in_place else \
+        [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
     if cb.MEMORY_HOST in mems:
         _watch_host([x for i, m in enumerate(mems) if m == cb.MEMORY_HOST for x in (tensors[i], outputs[i])])
     # one completion group for the batch: the engine completes every request natively (no
-    # Python done() per tensor)
+    # Python done() per tensor); the group keeps every tensor until the batch has completed, so
+    # the handles hold only their outputs
     group = _Completion(k, (tensors, outputs))
-    handles = [_NativeHandle(n, o, (t, o), group, i) for i, (n, t, o) in enumerate(zip(names, tensors, outputs))]
+    handles = [_NativeHandle(n, o, None, group, i) for i, (n, o) in enumerate(zip(names, outputs))]
     done, slots = _native_done(), group.slots()
-    for mem in sorted(set(mems)):
-        idx = [i for i in range(k) if mems[i] == mem]
+    kinds = sorted(set(mems))
+    for mem in kinds:
+        if len(kinds) == 1:  # one memory kind (the usual batch): the arrays straight from the lists
+            idx, ts, os_, nm, users = range(k), tensors, outputs, names, slots
+        else:
+            idx = [i for i in range(k) if mems[i] == mem]
+            ts, os_, nm = [tensors[i] for i in idx], [outputs[i] for i in idx], [names[i] for i in idx]
+            users = (ctypes.c_void_p * len(idx))(*[slots[i] for i in idx])
         m = len(idx)
-        keys = (ctypes.c_char_p * m)(*[names[i].encode() for i in idx])
-        ins = (ctypes.c_void_p * m)(*[tensors[i].data_ptr() for i in idx])
-        outs = (ctypes.c_void_p * m)(*[outputs[i].data_ptr() for i in idx])
-        ns = (ctypes.c_size_t * m)(*[tensors[i].numel() for i in idx])
-        dts = (ctypes.c_int * m)(*[ddl_dtype(tensors[i]) for i in idx])
-        users = (ctypes.c_void_p * m)(*[slots[i] for i in idx])
+        keys = (ctypes.c_char_p * m)(*[n.encode() for n in nm])
+        ins = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ts])
+        outs = ins if in_place else (ctypes.c_void_p * m)(*[o.data_ptr() for o in os_])
+        ns = (ctypes.c_size_t * m)(*[t.numel() for t in ts])
+        dts = (ctypes.c_int * m)(*[ddl_dtype(t) for t in ts])
         st = CPPBackend.c_api().ddl_allreduce_submit_batch_mem(
             communicator.id, m, keys, ins, outs, ns, dts, cb.OP_SUM, mem, stream_handle_for(tensors[idx[0]]),
             done, users)
