@@ -59,7 +59,7 @@ int ddl_init(int rank, int size, int device, const void *unique_id, size_t len) 
         DDL_REQUIRE(!Registry::get().initialized(), DDL_STATUS_INVALID_ARGUMENT, "already initialized");
         DDL_HIP(hipSetDevice(device));
         ncclComm_t nc = size > 1 ? rccl_init_rank(rank, size, unique_id, len) : nullptr;
-        Registry::get().set_world(std::make_shared<Communicator>(rank, size, device, nc));
+        Registry::get().set_world(new_communicator(rank, size, device, nc));
         DDL_LOG(1, "initialized rank " << rank << "/" << size << " on device " << device
                                        << (size > 1 ? std::string(" rccl=") + rccl().path : ""));
     });

@@ -175,7 +175,7 @@ int ddl_init_test_transport(int rank, int size, int device, ddl_test_group_fn gr
         hooks->max = max;
         hooks->user = user;
         hooks->make_transport = &make_callback_transport;
-        Registry::get().set_world(std::make_shared<Communicator>(rank, size, device, nullptr, hooks, 0));
+        Registry::get().set_world(new_communicator(rank, size, device, nullptr, hooks, 0));
         DDL_LOG(1, "initialized rank " << rank << "/" << size << " on device " << device << " (test transport)");
     });
 }

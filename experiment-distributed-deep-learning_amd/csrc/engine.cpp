@@ -668,17 +668,17 @@ std::shared_ptr<Communicator> Communicator::split(int color, int key, bool keyed
         DDL_REQUIRE(color >= 0, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
         std::vector<int> wr;
         for (int q : members) wr.push_back(world_ranks_.empty() ? q : world_ranks_[q]);
-        c = std::make_shared<Communicator>(me, s, device_, nullptr, s > 1 ? hooks_ : nullptr, tag, wr);
+        c = new_communicator(me, s, device_, nullptr, s > 1 ? hooks_ : nullptr, tag, wr);
     } else if (nccl_) {
         int r = 0, n = 0;
         ncclComm_t nc = rccl_split(nccl_, color, key, &r, &n);
         DDL_REQUIRE(nc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
         DDL_REQUIRE(r == me && n == s, DDL_STATUS_COMM_ERROR,
                     "ncclCommSplit gave rank " << r << " of " << n << ", the split exchange " << me << " of " << s);
-        c = std::make_shared<Communicator>(r, n, device_, nc);
+        c = new_communicator(r, n, device_, nc);
     } else {
         DDL_REQUIRE(color >= 0, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
-        c = std::make_shared<Communicator>(0, 1, device_, nullptr);
+        c = new_communicator(0, 1, device_, nullptr);
     }
     // 4) its token ring and keyed data plane (collective over the new communicator)
     if (keyed && s > 1) {
@@ -763,6 +763,16 @@ RequestHandler &Communicator::handler() {
 }
 
 // ---- registry ------------------------------------------------------------------------------
+thread_local bool t_handler_thread = false;
+
+void CommunicatorDeleter::operator()(Communicator *c) const {
+    if (!t_handler_thread) {
+        delete c;
+        return;
+    }
+    std::thread([c] { delete c; }).detach();
+}
+
 Registry &Registry::get() {
     static Registry *r = new Registry();  // leaked on purpose: no static-destruction order issues
     return *r;

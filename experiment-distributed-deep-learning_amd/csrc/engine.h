@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "control.h"
@@ -288,6 +289,22 @@ private:
     void *slots_[kHostSlots] = {};
     size_t slot_bytes_ = 0;
 };
+
+// Set on a request handler's engine and completion threads. The last reference to a communicator
+// dropped on such a thread (a done() callback that detaches its own communicator, or any C-ABI
+// call from a callback racing a detach) must not run the destructor there: ~RequestHandler joins
+// those threads. CommunicatorDeleter hands the destruction to a thread of its own instead.
+extern thread_local bool t_handler_thread;
+
+struct CommunicatorDeleter {
+    void operator()(Communicator *c) const;
+};
+
+// every Communicator is owned through this (make_shared would bypass the deleter)
+template <class... A>
+std::shared_ptr<Communicator> new_communicator(A &&...a) {
+    return std::shared_ptr<Communicator>(new Communicator(std::forward<A>(a)...), CommunicatorDeleter{});
+}
 
 class Registry {
 public:

@@ -498,6 +498,7 @@ void RequestHandler::fail_all_(int status) {
 }
 
 void RequestHandler::main_() {
+    t_handler_thread = true;  // engine.h: no communicator is destroyed on this thread
     try {
         DDL_HIP(hipSetDevice(owner_->device()));
         // the engine thread takes a share of every host pack / unpack: it and the copy threads
@@ -1735,6 +1736,7 @@ void RequestHandler::complete_(Round &rd) {
 }
 
 void RequestHandler::completer_() {
+    t_handler_thread = true;  // done() callbacks run here (engine.h)
     (void)hipSetDevice(owner_->device());
     for (;;) {
         Round rd;

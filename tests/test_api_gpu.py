@@ -313,6 +313,37 @@ def test_split_size1_keyed_detach_joins_handler(world):
     assert threads() <= n0 + 1, (n0, threads())
 
 
+def test_done_callback_may_detach_its_communicator(world):
+    """A done() that detaches its own communicator drops the last reference on the handler's
+    completion thread, and ~RequestHandler joins that thread: the engine hands the destruction to
+    a thread of its own (engine.h, CommunicatorDeleter). The process survives, the callback's
+    detach returns, and the handler's threads end."""
+    import time
+
+    from ddl.torch import cpp_backend as cb
+    from ddl.torch.util import ddl_dtype
+    api = cb.CPPBackend.c_api()
+    sub = world.split_communicator(0)
+    seen = []
+
+    @cb.DONE_FN
+    def done(status, user):
+        seen.append(status)
+        api.detach_communicator(sub.id)
+        seen.append('detached')
+
+    n0 = len(os.listdir('/proc/self/task'))  # before the split's handler starts (lazily)
+    t = torch.ones(64, device='cuda')
+    assert api.ddl_allreduce_submit(sub.id, b'detach_me', t.data_ptr(), t.data_ptr(), 64, ddl_dtype(t), 0,
+                                    torch.cuda.current_stream().cuda_stream, done, 0) == 0
+    deadline = time.time() + 30
+    while time.time() < deadline and (len(seen) < 2 or len(os.listdir('/proc/self/task')) > n0):
+        time.sleep(0.05)
+    assert seen == [0, 'detached'], seen
+    assert len(os.listdir('/proc/self/task')) <= n0
+    assert api.communicator_size(sub.id) == -1  # gone from the registry
+
+
 def test_rccl_comparator_entry_size1(world, lib):
     x = torch.randn(1000, device='cuda')
     y = torch.empty_like(x)
