@@ -1061,74 +1061,74 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
     // caller may free those outputs; drain() also clears the lane's error, so it cannot surface in
     // a later plan's wait
     try {
-    for (size_t i = 0; i < nchunks; ++i) {
-        const int k = (int)(i % kHostSlots);
-        const size_t off = cut[i], n = cut[i + 1] - off;
-        // the device slot's last user may still be in flight (a device unpack)
-        if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
-        if (upload) {
-            // the pinned slot's last upload must have left it (device-unpack plans do not wait
-            // for their D2H on the host)
-            clk::time_point t0 = clk::now();
-            if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
-            config().host_wait_ns.fetch_add(ns_since(t0));
-            t0 = clk::now();
-            pieces.clear();
-            host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
-            pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
-            DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
-            config().host_pack_ns.fetch_add(ns_since(t0));
-        }
-        DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
-        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
-        const clk::time_point t_coll = clk::now();
-        const long long fault = g_host_coll_fault.load();
-        if (fault >= 0 && (long long)i >= fault) {  // test hook (ddl_testing_host_coll_fault)
-            g_host_coll_fault = -1;
-            fail(DDL_STATUS_COMM_ERROR, "test fault: host plan collective of chunk " + std::to_string(i));
-        }
-        coll(dslot_[k], n / es);
-        config().host_coll_ns.fetch_add(ns_since(t_coll));
-        DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
-        DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
-        if (device_unpack) {
-            // the unpack kernel writes the chunk's pieces straight into the pinned outputs over
-            // PCIe; it lays piece j at the rounded sum of the pieces before it, which is its
-            // offset in the padded stream (chunks start at multiples of 256, so a cut never
-            // falls inside a segment's padding)
-            dst.clear();
-            len.clear();
-            size_t flat = 0;
-            for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
-                 j < segs.size() && starts[j] < off + n; ++j) {
-                const size_t lo = std::max(off, starts[j]), hi = std::min(off + n, starts[j] + segs[j].bytes);
-                if (hi <= lo) continue;
-                DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "device-unpack chunk layout");
-                dst.push_back(segs[j].ddst + (lo - starts[j]));  // the device's address of the output
-                len.push_back(hi - lo);
-                flat += round256(hi - lo);
+        for (size_t i = 0; i < nchunks; ++i) {
+            const int k = (int)(i % kHostSlots);
+            const size_t off = cut[i], n = cut[i + 1] - off;
+            // the device slot's last user may still be in flight (a device unpack)
+            if (slot_used_[k]) DDL_HIP(hipStreamWaitEvent(h2d_, hev_[3 * k + 2], 0));
+            if (upload) {
+                // the pinned slot's last upload must have left it (device-unpack plans do not wait
+                // for their D2H on the host)
+                clk::time_point t0 = clk::now();
+                if (slot_used_[k]) DDL_HIP(hipEventSynchronize(hev_[3 * k]));
+                config().host_wait_ns.fetch_add(ns_since(t0));
+                t0 = clk::now();
+                pieces.clear();
+                host_pieces_(segs, starts, off, n, static_cast<char *>(pin_[k]), true, pieces);
+                pool_->run(pieces);  // packs chunk i while the device works on chunks i-1, i-2, ...
+                DDL_HIP(hipMemcpyAsync(dslot_[k], pin_[k], n, hipMemcpyHostToDevice, h2d_));
+                config().host_pack_ns.fetch_add(ns_since(t0));
             }
-            fp_.copier.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
-        } else {
-            if (i >= (size_t)kHostSlots) wait_unpack(i - kHostSlots);  // download slot k free again
-            const clk::time_point t_post = clk::now();
-            DDL_HIP(hipMemcpyAsync(pout_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
-            config().host_d2h_post_ns.fetch_add(ns_since(t_post));
+            DDL_HIP(hipEventRecord(hev_[3 * k], h2d_));
+            DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * k], 0));
+            const clk::time_point t_coll = clk::now();
+            const long long fault = g_host_coll_fault.load();
+            if (fault >= 0 && (long long)i >= fault) {  // test hook (ddl_testing_host_coll_fault)
+                g_host_coll_fault = -1;
+                fail(DDL_STATUS_COMM_ERROR, "test fault: host plan collective of chunk " + std::to_string(i));
+            }
+            coll(dslot_[k], n / es);
+            config().host_coll_ns.fetch_add(ns_since(t_coll));
+            DDL_HIP(hipEventRecord(hev_[3 * k + 1], stream_));
+            DDL_HIP(hipStreamWaitEvent(d2h_, hev_[3 * k + 1], 0));
+            if (device_unpack) {
+                // the unpack kernel writes the chunk's pieces straight into the pinned outputs over
+                // PCIe; it lays piece j at the rounded sum of the pieces before it, which is its
+                // offset in the padded stream (chunks start at multiples of 256, so a cut never
+                // falls inside a segment's padding)
+                dst.clear();
+                len.clear();
+                size_t flat = 0;
+                for (size_t j = (size_t)(std::upper_bound(starts.begin(), starts.end(), off) - starts.begin()) - 1;
+                     j < segs.size() && starts[j] < off + n; ++j) {
+                    const size_t lo = std::max(off, starts[j]), hi = std::min(off + n, starts[j] + segs[j].bytes);
+                    if (hi <= lo) continue;
+                    DDL_REQUIRE(flat == lo - off, DDL_STATUS_ERROR_UNKNOWN, "device-unpack chunk layout");
+                    dst.push_back(segs[j].ddst + (lo - starts[j]));  // the device's address of the output
+                    len.push_back(hi - lo);
+                    flat += round256(hi - lo);
+                }
+                fp_.copier.run(1, dslot_[k], dst.data(), len.data(), (int)dst.size(), d2h_);
+            } else {
+                if (i >= (size_t)kHostSlots) wait_unpack(i - kHostSlots);  // download slot k free again
+                const clk::time_point t_post = clk::now();
+                DDL_HIP(hipMemcpyAsync(pout_[k], dslot_[k], n, hipMemcpyDeviceToHost, d2h_));
+                config().host_d2h_post_ns.fetch_add(ns_since(t_post));
+            }
+            DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
+            slot_used_[k] = true;
+            if (!device_unpack) {
+                const clk::time_point t_sub = clk::now();
+                unpack_async(i);
+                config().host_unpack_submit_ns.fetch_add(ns_since(t_sub));
+            }
         }
-        DDL_HIP(hipEventRecord(hev_[3 * k + 2], d2h_));
-        slot_used_[k] = true;
-        if (!device_unpack) {
-            const clk::time_point t_sub = clk::now();
-            unpack_async(i);
-            config().host_unpack_submit_ns.fetch_add(ns_since(t_sub));
+        if (device_unpack) {
+            // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
+            DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * ((nchunks - 1) % kHostSlots) + 2], 0));
+            return;
         }
-    }
-    if (device_unpack) {
-        // the plan's event (recorded on stream_ next) covers the last unpack, hence every unpack
-        DDL_HIP(hipStreamWaitEvent(stream_, hev_[3 * ((nchunks - 1) % kHostSlots) + 2], 0));
-        return;
-    }
-    for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) wait_unpack(j);
+        for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) wait_unpack(j);
     } catch (...) {
         lane_->drain();
         throw;
