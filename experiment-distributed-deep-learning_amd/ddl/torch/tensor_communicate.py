@@ -397,7 +397,7 @@ def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
     group = _Completion(1, (tensor, out))
-    h = _NativeHandle(name, out, (tensor, out), group, 0)
+    h = _NativeHandle(name, out, None, group, 0)  # the group holds the tensors
     st = CPPBackend.c_api().ddl_allreduce_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(),
         ddl_dtype(tensor), cb.OP_SUM, mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
@@ -466,7 +466,7 @@ def broadcast_async(tensor: torch.Tensor, name: str, root_rank: int, communicato
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
     group = _Completion(1, (tensor, out))
-    h = _NativeHandle(name, out, (tensor, out), group, 0)
+    h = _NativeHandle(name, out, None, group, 0)  # the group holds the tensors
     st = CPPBackend.c_api().ddl_broadcast_submit_mem(
         communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(), ddl_dtype(tensor),
         int(root_rank), mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
