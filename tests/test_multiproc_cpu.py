@@ -9,6 +9,7 @@
   intersection of the registered keys (RingTokenCommunicateHandler.cc:133-318 semantics).
 """
 import ctypes
+import datetime
 import os
 import socket
 import sys
@@ -37,89 +38,132 @@ def _setup_paths():
             sys.path.insert(0, p)
 
 
-def _ring_worker(rank, world, port, dt, n, algo, ref_order, q):
+def _ring_case(lib, h, ora, rank, world, dt, n, algo, ref_order):
+    """One program executed over gloo; True when this rank ends with the oracle's bytes."""
+    assert lib.ddl_set_config(b'algo', algo) == 0
+    assert lib.ddl_set_config(b'reference_order', ref_order) == 0
+    xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
+    prog = h.ring_program(lib, rank, world, n, dt)
+    R, _ = h.ring_shape(lib, n, dt, world)
+    st = h.staging_size([prog], world)
+    bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
+    view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
+    for t in sorted(set(prog[:, 0].tolist())):
+        rows = prog[prog[:, 0] == t]
+        for row in rows[rows[:, 1] == 4]:  # device copies (buffer 0 -> dst)
+            _, _, _, _, b, off, cnt, soff = row
+            bufs[b][off:off + cnt] = bufs[0][soff:soff + cnt]
+        for row in rows[rows[:, 1] == 11]:  # allgather (gather-fold): every rank's block
+            _, _, sb, so, rb, ro, cnt, _ = row
+            parts = [torch.empty(int(cnt), dtype=view(bufs[sb][:1]).dtype) for _ in range(world)]
+            dist.all_gather(parts, view(bufs[sb][so:so + cnt].copy()))
+            for qq, part in enumerate(parts):
+                dst = bufs[rb][ro + qq * cnt:ro + (qq + 1) * cnt]
+                dst[:] = part.numpy().view(dst.dtype)
+        reqs = []
+        for row in rows[rows[:, 1] == 1]:  # recvs first, then sends: no deadlock in gloo
+            _, _, peer, ring, b, off, cnt, _ = row
+            reqs.append(dist.irecv(view(bufs[b][off:off + cnt]), src=int(peer), tag=int(ring)))
+        for row in rows[rows[:, 1] == 0]:
+            _, _, peer, ring, b, off, cnt, _ = row
+            reqs.append(dist.isend(view(bufs[b][off:off + cnt].copy()), dst=int(peer), tag=int(ring)))
+        for r in reqs:
+            r.wait()
+        for row in rows[rows[:, 1] == 2]:
+            _, _, _, _, b, off, cnt, soff = row
+            bufs[1][off:off + cnt] = ora.sum2(dt, bufs[0][off:off + cnt], bufs[2][soff:soff + cnt])
+        h.apply_folds(ora, dt, rows, bufs)
+    if ref_order and (algo != 0 or world > 2):  # MPICH's own order (a P = 2 ring is exact)
+        want = ora.fold_ref_order(dt, xs)
+    else:
+        want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo in (2, 3) else
+                ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
+    return bufs[1].tobytes() == want.tobytes()
+
+
+def _ring_worker(rank, world, port, cases, q):
+    """Every case of one (world, reference_order) set in one process group: spawning the ranks
+    (a fresh interpreter importing torch) costs seconds, a case milliseconds. A case that raises
+    ends the run (the other ranks may be waiting in its exchange); the cases not reached fail
+    with its error."""
+    res, err, case = {}, '', 'setup'
     try:
         _setup_paths()
         import _helpers as h
         from ddl.torch.cpp_backend import CPPBackend
         lib = CPPBackend.c_api()
         ora = h.Oracle()
-        assert lib.ddl_set_config(b'algo', algo) == 0
-        assert lib.ddl_set_config(b'reference_order', ref_order) == 0
-        dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
-        xs = [h.random_input(dt, n, 1234 + 7919 * r) for r in range(world)]
-        prog = h.ring_program(lib, rank, world, n, dt)
-        R, _ = h.ring_shape(lib, n, dt, world)
-        st = h.staging_size([prog], world)
-        bufs = [xs[rank].copy(), np.zeros_like(xs[rank]), np.zeros(st, dtype=xs[rank].dtype)]
-        view = (lambda a: torch.from_numpy(a.view(np.int16)) if a.dtype == np.uint16 else torch.from_numpy(a))
-        for t in sorted(set(prog[:, 0].tolist())):
-            rows = prog[prog[:, 0] == t]
-            for row in rows[rows[:, 1] == 4]:  # device copies (buffer 0 -> dst)
-                _, _, _, _, b, off, cnt, soff = row
-                bufs[b][off:off + cnt] = bufs[0][soff:soff + cnt]
-            for row in rows[rows[:, 1] == 11]:  # allgather (gather-fold): every rank's block
-                _, _, sb, so, rb, ro, cnt, _ = row
-                parts = [torch.empty(int(cnt), dtype=view(bufs[sb][:1]).dtype) for _ in range(world)]
-                dist.all_gather(parts, view(bufs[sb][so:so + cnt].copy()))
-                for qq, part in enumerate(parts):
-                    dst = bufs[rb][ro + qq * cnt:ro + (qq + 1) * cnt]
-                    dst[:] = part.numpy().view(dst.dtype)
-            reqs = []
-            for row in rows[rows[:, 1] == 1]:  # recvs first, then sends: no deadlock in gloo
-                _, _, peer, ring, b, off, cnt, _ = row
-                reqs.append(dist.irecv(view(bufs[b][off:off + cnt]), src=int(peer), tag=int(ring)))
-            for row in rows[rows[:, 1] == 0]:
-                _, _, peer, ring, b, off, cnt, _ = row
-                reqs.append(dist.isend(view(bufs[b][off:off + cnt].copy()), dst=int(peer), tag=int(ring)))
-            for r in reqs:
-                r.wait()
-            for row in rows[rows[:, 1] == 2]:
-                _, _, _, _, b, off, cnt, soff = row
-                bufs[1][off:off + cnt] = ora.sum2(dt, bufs[0][off:off + cnt], bufs[2][soff:soff + cnt])
-            h.apply_folds(ora, dt, rows, bufs)
-        if ref_order and (algo != 0 or world > 2):  # MPICH's own order (a P = 2 ring is exact)
-            want = ora.fold_ref_order(dt, xs)
-        else:
-            want = (ora.allreduce_direct(dt, xs) if algo == 1 else ora.fold(dt, xs) if algo in (2, 3) else
-                    ora.allreduce_ring(dt, xs, h.ring_perms(lib, world, R)))
-        ok = bufs[1].tobytes() == want.tobytes()
+        dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=120))  # a peer that failed: no long hang
+        for case in cases:
+            res[case] = _ring_case(lib, h, ora, rank, world, *case)
         dist.destroy_process_group()
-        q.put((rank, ok, ''))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, False, repr(e)))
+        err = f'{case}: {e!r}'
+    q.put((rank, res, err))
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2, 3])
+RING_CASES = [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)]
+RING_ALGOS = [0, 1, 2, 3]
+REF_CASES = [(1, 50_000), (1, 300), (2, 4099), (1, 128 * 840)]
+REF_ALGOS = [0, 1, 2, 3, 4]
+
+
+@pytest.mark.parametrize('algo', RING_ALGOS)
 @pytest.mark.parametrize('world', [2, 3])
-@pytest.mark.parametrize('dt,n', [(1, 50_000), (3, 4099), (19, 33_333), (2, 1)])
+@pytest.mark.parametrize('dt,n', RING_CASES)
 def test_ring_program_over_gloo(world, dt, n, algo):
     """reference_order 0: the ring / left-fold orders."""
-    _run_ring_workers(world, dt, n, algo, 0)
+    _check_ring_case(world, dt, n, algo, 0)
 
 
-@pytest.mark.parametrize('algo', [0, 1, 2, 3, 4])
+@pytest.mark.parametrize('algo', REF_ALGOS)
 @pytest.mark.parametrize('world', [2, 3])
-@pytest.mark.parametrize('dt,n', [(1, 50_000), (1, 300), (2, 4099), (1, 128 * 840)])
+@pytest.mark.parametrize('dt,n', REF_CASES)
 def test_reference_order_program_over_gloo(world, dt, n, algo):
     """reference_order 1 (the default): every rank ends with MPICH's own order (binomial tree at
     <= 2048 bytes, the pre-fold + pairwise tree above), whichever schedule is asked for."""
-    _run_ring_workers(world, dt, n, algo, 1)
+    _check_ring_case(world, dt, n, algo, 1)
 
 
-def _run_ring_workers(world, dt, n, algo, ref_order):
+_RING_RUNS = {}  # (world, reference_order) -> {case: [ok per rank]}, errors
+
+
+def _check_ring_case(world, dt, n, algo, ref_order):
+    key = (world, ref_order)
+    if key not in _RING_RUNS:
+        cases = [(d, m, a, ref_order) for d, m in (RING_CASES if ref_order == 0 else REF_CASES)
+                 for a in (RING_ALGOS if ref_order == 0 else REF_ALGOS)]
+        _RING_RUNS[key] = _run_ring_workers(world, cases)
+    results, errors = _RING_RUNS[key]
+    oks = results.get((dt, n, algo, ref_order))
+    assert oks is not None and len(oks) == world, f'case not run: {errors}'
+    for rank, ok in enumerate(oks):
+        assert ok, f'rank {rank}: result differs from the oracle'
+
+
+def _run_ring_workers(world, cases):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, dt, n, algo, ref_order, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, cases, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, ok, err in res:
-        assert ok, f'rank {rank}: {err or "result differs from the ring-order oracle"}'
+    results, errors = {}, []
+    try:
+        for _ in procs:
+            rank, res, err = q.get(timeout=600)
+            if err:
+                errors.append(f'rank {rank}: {err}')
+            for case, ok in res.items():
+                results.setdefault(case, [None] * world)[rank] = ok
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    results = {c: v for c, v in results.items() if None not in v}
+    return results, errors
 
 
 def _control_worker(rank, world, keysets, eps_q, go_q, out_q):
