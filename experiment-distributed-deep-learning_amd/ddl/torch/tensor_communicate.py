@@ -252,6 +252,7 @@ class _Completion:
 
 
 _NATIVE_DONE = []
+_STATUS_ERROR_UNKNOWN = 2  # include/ddl_amd.h DDL_STATUS_ERROR_UNKNOWN
 
 
 def _native_done():
@@ -396,11 +397,13 @@ def allreduce_async(tensor: torch.Tensor, name: str, communicator: Communicator 
     mem = _same_memory(tensor, out, 'allreduce_async')
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
+    # argument errors first: a group whose slot is never submitted would stay pending
+    key, dt, stream = name.encode(), ddl_dtype(tensor), stream_handle_for(tensor)
     group = _Completion(1, (tensor, out))
     h = _NativeHandle(name, out, None, group, 0)  # the group holds the tensors
     st = CPPBackend.c_api().ddl_allreduce_submit_mem(
-        communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(),
-        ddl_dtype(tensor), cb.OP_SUM, mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
+        communicator.id, key, tensor.data_ptr(), out.data_ptr(), tensor.numel(), dt, cb.OP_SUM, mem, stream,
+        _native_done(), group.slots()[0])
     if st != cb.STATUS_OK:
         group.fail([0], st)
         check(st, 'ddl_allreduce_submit_mem')
@@ -424,6 +427,8 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     in_place = all(o is t for t, o in zip(tensors, outputs))  # the DP wrapper's form
     mems = [memory_kind(t, 'allreduce_async_batch input') for t in tensors] if in_place else \
         [_same_memory(t, o, 'allreduce_async_batch') for t, o in zip(tensors, outputs)]
+    # argument errors first: slots of a group that are never submitted would stay pending
+    keys_all, dts_all = [n.encode() for n in names], [ddl_dtype(t) for t in tensors]
     if cb.MEMORY_HOST in mems:
         _watch_host([x for i, m in enumerate(mems) if m == cb.MEMORY_HOST for x in (tensors[i], outputs[i])])
     # one completion group for the batch: the engine completes every request natively (no
@@ -435,22 +440,25 @@ def allreduce_async_batch(tensors, names, communicator: Communicator = None, out
     kinds = sorted(set(mems))
     for mem in kinds:
         if len(kinds) == 1:  # one memory kind (the usual batch): the arrays straight from the lists
-            idx, ts, os_, nm, users = range(k), tensors, outputs, names, slots
+            idx, ts, os_, ks, ds, users = range(k), tensors, outputs, keys_all, dts_all, slots
         else:
             idx = [i for i in range(k) if mems[i] == mem]
-            ts, os_, nm = [tensors[i] for i in idx], [outputs[i] for i in idx], [names[i] for i in idx]
+            ts, os_ = [tensors[i] for i in idx], [outputs[i] for i in idx]
+            ks, ds = [keys_all[i] for i in idx], [dts_all[i] for i in idx]
             users = (ctypes.c_void_p * len(idx))(*[slots[i] for i in idx])
         m = len(idx)
-        keys = (ctypes.c_char_p * m)(*[n.encode() for n in nm])
-        ins = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ts])
-        outs = ins if in_place else (ctypes.c_void_p * m)(*[o.data_ptr() for o in os_])
-        ns = (ctypes.c_size_t * m)(*[t.numel() for t in ts])
-        dts = (ctypes.c_int * m)(*[ddl_dtype(t) for t in ts])
-        st = CPPBackend.c_api().ddl_allreduce_submit_batch_mem(
-            communicator.id, m, keys, ins, outs, ns, dts, cb.OP_SUM, mem, stream_handle_for(tensors[idx[0]]),
-            done, users)
+        rest = [i for i in range(k) if mems[i] >= mem]  # this submission and the ones not made
+        try:
+            ins = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ts])
+            outs = ins if in_place else (ctypes.c_void_p * m)(*[o.data_ptr() for o in os_])
+            st = CPPBackend.c_api().ddl_allreduce_submit_batch_mem(
+                communicator.id, m, (ctypes.c_char_p * m)(*ks), ins, outs,
+                (ctypes.c_size_t * m)(*[t.numel() for t in ts]), (ctypes.c_int * m)(*ds), cb.OP_SUM, mem,
+                stream_handle_for(tensors[idx[0]]), done, users)
+        except BaseException:
+            group.fail(rest, _STATUS_ERROR_UNKNOWN)  # not submitted: no slot may stay pending
+            raise
         if st != cb.STATUS_OK:
-            rest = [i for i in range(k) if mems[i] >= mem]  # this submission and the ones not made
             group.fail(rest, st)
             check(st, 'ddl_allreduce_submit_batch_mem')
     return handles
@@ -465,11 +473,12 @@ def broadcast_async(tensor: torch.Tensor, name: str, root_rank: int, communicato
     mem = _same_memory(tensor, out, 'broadcast_async')
     if mem == cb.MEMORY_HOST:
         _watch_host((tensor, out))
+    key, dt, stream, root = name.encode(), ddl_dtype(tensor), stream_handle_for(tensor), int(root_rank)
     group = _Completion(1, (tensor, out))
     h = _NativeHandle(name, out, None, group, 0)  # the group holds the tensors
     st = CPPBackend.c_api().ddl_broadcast_submit_mem(
-        communicator.id, name.encode(), tensor.data_ptr(), out.data_ptr(), tensor.numel(), ddl_dtype(tensor),
-        int(root_rank), mem, stream_handle_for(tensor), _native_done(), group.slots()[0])
+        communicator.id, key, tensor.data_ptr(), out.data_ptr(), tensor.numel(), dt, root, mem, stream,
+        _native_done(), group.slots()[0])
     if st != cb.STATUS_OK:
         group.fail([0], st)
         check(st, 'ddl_broadcast_submit_mem')
