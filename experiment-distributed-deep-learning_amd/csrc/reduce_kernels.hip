@@ -748,24 +748,38 @@ void launch_sumN_batch(const SegTableN *t, int count, int dtype, hipStream_t str
 void launch_sumN(const SegTableN &t, int dtype, hipStream_t stream) { launch_sumN_batch(&t, 1, dtype, stream); }
 
 // Standalone reduce (acc += in over whole buckets) of `bytes` per operand, by bucket size
-// (3 rotating buffer sets per size, profiles/r02/reduce_policy/, profiles/r05/s6/):
-//   * from 256 MiB every access is non-temporal: the bucket streams through once (6.8 TB/s at
-//     256 MiB; write-through stores 0.5-0.8 % slower there);
-//   * 32-256 MiB: non-temporal loads, write-through stores (64 MiB: 7.5 vs 6.6 TB/s all-nt;
-//     128 MiB: 6.9 vs 6.7); below 128 MiB in the run form with 4-tile runs (r05,
-//     tools/reduce_run_ab.py: 32 MiB 6.32 vs 5.97 TB/s for the tile form, 64 MiB 6.88 vs 6.50 —
-//     where part of the 3 x 3 operand sets stays in the Infinity Cache, a workgroup streaming one
-//     operand at a time wins; from 128 MiB, pure HBM streaming, the tile form does: 6.70 vs 6.27
-//     at 256 MiB, 6.72 vs 6.17 at 512 MiB);
-//   * below 32 MiB: plain loads — the operands of a small bucket are likely still in the
-//     Infinity Cache from whoever produced them — and write-through stores (16 MiB: 6.7 vs 6.4
-//     TB/s plain stores; the run form ties there, 6.15 vs 6.10).
-constexpr size_t kNtMinBytes = 32u << 20, kRunMaxBytes = 128u << 20, kNtStoreMinBytes = 256u << 20;
+// (3 rotating buffer sets per size, interleaved A/Bs: profiles/r02/reduce_policy/, profiles/r05/s6/,
+// profiles/r05/s15/):
+//   * from 256 MiB every access is non-temporal: the bucket streams through once (6.7-6.8 TB/s at
+//     256 MiB; write-through stores 0.5-0.8 % slower there; the run form 6.27 vs 6.70);
+//   * 96-256 MiB: the tile form, non-temporal loads, write-through stores (96 / 112 / 128 MiB: 6.32-6.46 /
+//     6.37-6.45 / 6.51-6.60 TB/s vs 6.27-6.31 / 6.30-6.32 / 6.27-6.35 for the run form);
+//   * 12-96 MiB: the run form with 4-tile runs (a workgroup streams one operand at a time) and
+//     write-through stores, where part of the operand sets stays in the Infinity Cache; its loads
+//     non-temporal except from 22 to 42 MiB, where plain loads measured faster on three boxes
+//     (24 / 28 / 32 / 36 MiB: 6.39-6.47 / 6.49-6.60 / 6.57-6.66 / 6.65-6.69 TB/s vs 6.15-6.25 /
+//     6.26-6.27 / 6.31-6.41 / 6.44-6.45 non-temporal); non-temporal wins at 12-20 MiB (16 MiB:
+//     6.04-6.46 vs 5.78-6.03) and from 44 MiB (64 MiB 6.87-6.89, 80 MiB 6.91-6.99 vs 5.5-5.8
+//     plain); against the tile form with plain loads, r05's rule below 32 MiB: 16 MiB 6.04-6.46 vs
+//     5.78-5.89, 32 MiB 6.57-6.66 vs 6.39-6.66;
+//   * below 12 MiB: the tile form, plain loads — the operands of a small bucket are likely still
+//     in the Infinity Cache from whoever produced them — and write-through stores (8 MiB: 5.93-5.95
+//     TB/s vs 4.7-6.3 for the run forms).
+struct VariantBand {
+    size_t below;  // bytes per operand
+    int variant;
+};
+constexpr VariantBand kReduceBands[] = {
+    {12u << 20, kWtStore},
+    {22u << 20, kRunForm | kRun4 | kNtLoadA | kNtLoadB | kWtStore},
+    {42u << 20, kRunForm | kRun4 | kWtStore},
+    {96u << 20, kRunForm | kRun4 | kNtLoadA | kNtLoadB | kWtStore},
+    {256u << 20, kNtLoadA | kNtLoadB | kWtStore},
+};
 int default_variant(size_t bytes) {
-    if (bytes >= kNtStoreMinBytes) return kNtLoadA | kNtLoadB | kNtStore;
-    if (bytes >= kRunMaxBytes) return kNtLoadA | kNtLoadB | kWtStore;
-    if (bytes >= kNtMinBytes) return kRunForm | kRun4 | kNtLoadA | kNtLoadB | kWtStore;
-    return kWtStore;
+    for (const VariantBand &b : kReduceBands)
+        if (bytes < b.below) return b.variant;
+    return kNtLoadA | kNtLoadB | kNtStore;
 }
 
 // Ring reduce-scatter step: a = the rank's own gradient (read once: non-temporal), b = the slice

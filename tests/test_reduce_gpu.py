@@ -286,12 +286,14 @@ def test_reduce_fold_ordered_rejects_bad_order(lib, gpu):
 
 
 # C2's headline sizes: the bench's 256 MiB and 1 GiB launches, at full
-# size, in every cache-policy band default_variant picks (reduce_kernels.hip: below 32 MiB plain
-# loads + write-through stores, 32-256 MiB non-temporal loads + write-through stores, from 256 MiB
-# all non-temporal). Integer-valued fp32 in (-2^22, 2^22): every sum is exact in fp32, so the WHOLE
-# output is checked against the exact sum; then random data against the oracle's MPI_SUM on a
-# strided sample of the same launch.
-C2_SIZES = [(16 << 20) // 4 + 7, (64 << 20) // 4 + 5, (256 << 20) // 4, (1 << 30) // 4 + 13]
+# size, and a size in every band default_variant picks (reduce_kernels.hip kReduceBands: below 12 MiB
+# the tile form with plain loads; 12-22 MiB the run form, non-temporal loads; 22-42 MiB the run form,
+# plain loads; 42-96 MiB the run form, non-temporal loads; 96-256 MiB the tile form, non-temporal
+# loads — all with write-through stores; from 256 MiB all non-temporal). Integer-valued fp32 in
+# (-2^22, 2^22): every sum is exact in fp32, so the WHOLE output is checked against the exact sum;
+# then random data against the oracle's MPI_SUM on a strided sample of the same launch.
+C2_SIZES = [(8 << 20) // 4 + 9, (16 << 20) // 4 + 7, (32 << 20) // 4 + 3, (64 << 20) // 4 + 5,
+            (100 << 20) // 4 + 1, (256 << 20) // 4, (1 << 30) // 4 + 13]
 
 
 @pytest.mark.parametrize('in_place', [True, False], ids=['local', 'sum2'])

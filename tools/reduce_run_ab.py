@@ -18,12 +18,12 @@ import torch  # noqa: E402
 from ddl.torch.cpp_backend import CPPBackend, check  # noqa: E402
 
 
-def policy(nbytes):  # reduce_kernels.hip default_variant
+def policy(nbytes):  # the cache bits of reduce_kernels.hip default_variant (kReduceBands), form aside
     if nbytes >= 256 << 20:
         return 7
-    if nbytes >= 32 << 20:
-        return 19
-    return 16
+    if nbytes < 12 << 20 or (22 << 20) <= nbytes < (42 << 20):
+        return 16
+    return 19
 
 
 def main():
