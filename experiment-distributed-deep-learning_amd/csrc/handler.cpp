@@ -485,14 +485,16 @@ std::atomic<long long> g_host_coll_fault{-1};
 void set_testing_host_coll_fault(long long chunk) { g_host_coll_fault = chunk; }
 
 void RequestHandler::fail_all_(int status) {
-    std::map<ReqId, Request> left;
+    std::vector<Request> left;
     {
         std::lock_guard<std::mutex> g(mu_);
-        left.swap(pending_);
+        left.reserve(pending_.size());
+        for (auto &kv : pending_) left.push_back(std::move(kv.second));
+        pending_.clear();  // the nodes go back to the pool under mu_
         std::fill(pend_flag_.begin(), pend_flag_.end(), 0);
     }
-    for (auto &kv : left) {
-        if (kv.second.done) kv.second.done(status, kv.second.user);
+    for (Request &r : left) {
+        if (r.done) r.done(status, r.user);
     }
     idle_cv_.notify_all();
 }

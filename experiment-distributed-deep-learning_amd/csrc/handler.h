@@ -24,6 +24,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <memory_resource>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -341,7 +342,11 @@ private:
     std::mutex mu_;
     std::condition_variable cv_;       // new registrations / stop
     std::condition_variable idle_cv_;  // completions
-    std::map<ReqId, Request> pending_;  // (type name, key) order
+    // the pending map's nodes come from a pool, allocated and freed under mu_ only: a 4096-request
+    // batch's sorted inserts and its take walk ran 2-3x faster than with the process heap
+    // (CPU micro-benchmark; r05 s22 on the box)
+    std::pmr::unsynchronized_pool_resource pending_pool_;
+    std::pmr::map<ReqId, Request> pending_{&pending_pool_};  // (type name, key) order
     // id table mirror (indices of the ring's cache): parsed ids, key -> index per type,
     // and which indices are pending here — a cached round is intersected by index
     std::vector<ReqId> cache_req_;
