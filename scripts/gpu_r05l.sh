@@ -1,6 +1,7 @@
 #!/bin/bash
 # r05 s24: same-box A/B of the keyed batch's host phases, the library before the pooled pending map
-# (built from 8610599 into lib_ab/, not committed) against the current one, alternated 3 times.
+# (built from 8610599 into lib_ab/ by hand, not committed, removed after the run) against the
+# current one, alternated 3 times.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-r05s24}; mkdir -p $O
 OLD=$PWD/experiment-distributed-deep-learning_amd/lib_ab/libddl_amd_testing_prepool.so
