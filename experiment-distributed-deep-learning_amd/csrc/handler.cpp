@@ -422,7 +422,7 @@ void validate(const Request &r, int size) {
 // A request whose id was agreed before gets its id-table index (under mu_).
 void RequestHandler::mark_cached_(const ReqId &id, Request &r) {
     r.cidx = -1;
-    if (id.order < 0 || id.order >= 3) return;
+    if (id.order < 0 || id.order >= 3 || cache_by_key_[id.order].empty()) return;  // (no hashing at size 1)
     auto it = cache_by_key_[id.order].find(id.key);
     if (it == cache_by_key_[id.order].end()) return;
     r.cidx = it->second;
@@ -524,8 +524,12 @@ void RequestHandler::main_() {
                     if (cycle_us > 0)
                         cv_.wait_for(lk, std::chrono::microseconds(cycle_us), [this] { return stop_; });
                     if (stop_) break;
-                    for (auto &kv : pending_)
-                        if (kv.first.order == pending_.begin()->first.order) keys.push_back(kv.first);
+                    if (P == 1) {  // (rank 0 of a ring builds its proposal in root_round_)
+                        keys.reserve(pending_.size());
+                        const int order = pending_.begin()->first.order;
+                        for (auto &kv : pending_)
+                            if (kv.first.order == order) keys.push_back(kv.first);
+                    }
                 }
                 if (P == 1) execute_(keys);
                 else root_round_();  // negotiation lap times: DDL_LOG level 3 in root_round_
