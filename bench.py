@@ -972,24 +972,29 @@ def multi_gpu(args):
     state = {'out': None, 'leg': 'main'}  # rank 0's result so far; the leg in progress
 
     def hung():
-        # a hung collective must not eat the driver's whole scaling run: once the headline
-        # measurement exists, rank 0 prints it with the unfinished leg named, and every rank
-        # exits 0; before that, exit 3
+        # a hung collective must not eat the driver's whole scaling run, and must not pass for a
+        # good one: once the headline measurement exists, rank 0 prints it with the unfinished
+        # leg named in `incomplete`; every rank then exits WATCHDOG_RC.
+        # Ranks other than 0 wait a moment first so a launcher that kills the job on the first
+        # non-zero exit does not kill rank 0 before its line is out. A hang in teardown, after
+        # the complete line was printed, exits WATCHDOG_TEARDOWN_RC.
         sys.stderr.write(f'[bench rank {rank}] watchdog: leg {state["leg"]!r} not done after '
                          f'{args.watchdog_s:.0f} s, aborting\n')
         sys.stderr.flush()
         if state.get('printed'):
-            os._exit(0)
-        if state['out'] is not None:
-            if rank == 0:
-                state['out']['incomplete'] = f'watchdog after {args.watchdog_s:.0f} s in leg {state["leg"]}'
-                emit(state['out'])
-            os._exit(0)
-        os._exit(3)
+            os._exit(WATCHDOG_TEARDOWN_RC)
+        if state['out'] is not None and rank == 0:
+            state['out']['incomplete'] = f'watchdog after {args.watchdog_s:.0f} s in leg {state["leg"]}'
+            emit(state['out'])
+        if rank != 0:
+            time.sleep(3.0)
+        os._exit(WATCHDOG_RC)
 
     dog = threading.Timer(args.watchdog_s, hung)
     dog.daemon = True
     dog.start()
+    if os.environ.get('DDL_BENCH_WATCHDOG_SELFTEST') == '1':
+        _watchdog_selftest(args, state, rank, world)  # never returns: the watchdog ends the process
     if not args.rehearse and torch.cuda.device_count() < world:  # counting does not initialise the GPU
         sys.stderr.write(f'[bench rank {rank}] {world} ranks need {world} GPUs, this box has '
                          f'{torch.cuda.device_count()} (use --rehearse to run the N>1 legs on one GPU)\n')
@@ -1472,6 +1477,29 @@ def emit(obj):
     os.write(fd, line)
 
 
+WATCHDOG_RC = 3           # a leg hung: the line (if any) carries `incomplete`
+WATCHDOG_TEARDOWN_RC = 4  # the complete line was printed, then teardown hung
+
+
+def _watchdog_selftest(args, state, rank, world):
+    """CPU test hook for the N>1 watchdog (tests/test_bench_cpu.py): the ranks meet over gloo,
+    rank 0 holds a stand-in headline (`selftest` marks it), then every rank but 0 stalls in leg
+    'selftest_hang' while rank 0 waits for it in a barrier — a hung collective. The watchdog
+    must end every rank with WATCHDOG_RC and rank 0's line must carry `incomplete`."""
+    import torch.distributed as dist
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29533')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    state['out'] = {'metric': 'watchdog selftest', 'value': None, 'n_gpus': world, 'selftest': True}
+    dist.barrier()
+    state['leg'] = 'selftest_hang'
+    if rank != 0:
+        time.sleep(10 * args.watchdog_s + 60)
+    dist.barrier()
+    time.sleep(10 * args.watchdog_s + 60)
+    os._exit(0)  # not reached while the watchdog works
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -1496,6 +1524,7 @@ def spawn_ranks(args):
                                       start_new_session=True))
     deadline = time.time() + args.watchdog_s + 120
     rc = 0
+    stop_at = None  # after a rank's watchdog fired, the others get a grace period to fire theirs
     try:
         live = list(procs)
         while live:
@@ -1506,9 +1535,14 @@ def spawn_ranks(args):
                 live.remove(p)
                 if code != 0 and rc == 0:
                     rc = code if code > 0 else 128 - code
-                    sys.stderr.write(f'[bench] rank {procs.index(p)} exited with {code}; stopping the others\n')
-                    for q in live:
-                        os.killpg(q.pid, signal.SIGTERM)
+                    grace = 15.0 if code in (WATCHDOG_RC, WATCHDOG_TEARDOWN_RC) else 0.0
+                    sys.stderr.write(f'[bench] rank {procs.index(p)} exited with {code}; stopping the others'
+                                     f'{f" in {grace:.0f} s" if grace else ""}\n')
+                    stop_at = time.time() + grace
+            if stop_at is not None and time.time() >= stop_at:
+                for q in live:
+                    os.killpg(q.pid, signal.SIGTERM)
+                stop_at = float('inf')
             if time.time() > deadline:
                 sys.stderr.write('[bench] ranks still running past the watchdog; killing them\n')
                 for q in live:

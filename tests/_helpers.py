@@ -409,3 +409,40 @@ def hip_runtime():
         f = getattr(hip, name)
         f.restype, f.argtypes = res, args
     return hip
+
+
+GOLDEN_FULLSIZE = os.path.join(ROOT, 'tests', 'golden', 'golden_fullsize.json')
+
+
+def fullsize_cases():
+    """MPICH 3.3.2's full-size outputs, pinned by hash (tests/golden/make_golden.py --fullsize):
+    [(name, P, n, sha256, {index: value})]."""
+    import json
+    with open(GOLDEN_FULLSIZE) as f:
+        cases = json.load(f)['cases']
+    return [(k, c['P'], c['n'], c['sha256'], {int(i): v for i, v in c['samples'].items()})
+            for k, c in sorted(cases.items())]
+
+
+def fullsize_inputs(P, n):
+    """The full-size cases' rank inputs, regenerated from make_golden.py's seed rule
+    (default_rng(1234 + 7919 * rank).standard_normal(n) as fp32)."""
+    return [np.random.default_rng(1234 + 7919 * r).standard_normal(n).astype(np.float32) for r in range(P)]
+
+
+def sha256(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def fp16_single_rounding_bound(P, y, mag):
+    """|y - Σx| bound of an fp16 allreduce that folds all P inputs in fp32 and rounds ONCE (the
+    direct schedule, reference_order 1: DESIGN §3): ulp16(y)/2 for the one rounding plus
+    (P-1)·2^-24·Σ|x| for the fp32 fold. ulp16 is taken at the output's own binade (a sum just
+    below a power of two can round up into the next one); subnormals have ulp 2^-24. (A ring that
+    rounds at every hop would need (P-1)·2^-11·Σ|x|: 8192x looser, VERDICT r5 weak #1.)"""
+    import torch
+    a = y.double().abs()
+    _, e = torch.frexp(a)  # a = m * 2^e, m in [0.5, 1)
+    ulp = torch.where(a > 0, torch.exp2((e - 11).double()), torch.full_like(a, 2.0 ** -24)).clamp_min(2.0 ** -24)
+    return ulp / 2 + (P - 1) * 2.0 ** -24 * mag

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, FROM_NP, NAME, config, random_input, ring_perms,
+from _helpers import (ALL_DTYPES, DT_FLOAT, DT_HALF, FROM_NP, NAME, config, fp16_single_rounding_bound, random_input, ring_perms,
                       ring_shape)
 
 pytestmark = pytest.mark.gpu
@@ -199,15 +199,24 @@ def test_full_size_256mib_properties(lib, gpu):
 
 
 def test_fp16_tolerance_vs_fp64(lib, oracle, gpu):
-    """fp16 (no reference oracle: the reference rejects it): one rounding per hop, so
-    |y - round16(sum64)| <= (P-1) * u16 * sum|x| + ulp16/2 with u16 = 2^-11."""
+    """fp16 (no reference oracle: the reference rejects it). Reference order at P = 8 runs the
+    direct schedule: all inputs folded in fp32, ONE rounding, so
+    |y - sum64| <= ulp16(y)/2 + (P-1) * 2^-24 * sum|x|, and y equals the oracle's fp16 rule bit for
+    bit. reference_order 0 (a ring, rounding at every hop) keeps the per-hop bound
+    (P-1) * 2^-11 * sum|x| + ulp16/2."""
     P, n = 8, 1 << 20
     xs = [random_input(DT_HALF, n, 500 + r) for r in range(P)]
-    out = run_local(lib, gpu, xs)[0].astype(np.float64)
     exact = np.sum([x.astype(np.float64) for x in xs], axis=0)
+    mag = np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0)
+    with config(lib, reference_order=1):
+        y = run_local(lib, gpu, xs)[0]
+    assert y.tobytes() == oracle.fold_ref_order(DT_HALF, xs).tobytes()
+    bound = fp16_single_rounding_bound(P, torch.from_numpy(y), torch.from_numpy(mag)).numpy()
+    assert np.all(np.abs(y.astype(np.float64) - exact) <= bound)
+    with config(lib, reference_order=0):
+        out = run_local(lib, gpu, xs)[0].astype(np.float64)
     ulp = np.spacing(np.abs(exact).astype(np.float16)).astype(np.float64)
-    bound = (P - 1) * 2.0 ** -11 * np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0) + ulp / 2
-    assert np.all(np.abs(out - exact) <= bound)
+    assert np.all(np.abs(out - exact) <= (P - 1) * 2.0 ** -11 * mag + ulp / 2)
 
 
 def test_repeated_calls_reuse_resources(lib, oracle, gpu):

@@ -24,7 +24,8 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, config, random_input, ring_perms, ring_shape
+from _helpers import (DT_DOUBLE, DT_FLOAT, DT_HALF, DT_INT32, NAME, config, fp16_single_rounding_bound, random_input,
+                      ring_perms, ring_shape, sha256)
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -121,34 +122,31 @@ def test_thread_world_c3_full_size(lib, oracle, gpu, algo):
 def test_thread_world_c4_fp16_full_size(lib, oracle, gpu):
     """C4 through the production executor: 64 buckets of 16 MiB fp16 per rank (1 GiB), P = 8, each
     bucket one asynchronous thread-world allreduce in place, back to back with no host
-    synchronisation in between (as a DDP bucket stream issues them). Every rank within the stated
-    fp16 bound |y - sum| <= (P-1) * 2^-11 * sum|x| + ulp16(sum)/2 of the exact (fp64) sum, all ranks
-    identical; and bucket 0 bit-exact vs the oracle's fp16 fold (rank order in fp32, one rounding)."""
+    synchronisation in between (as a DDP bucket stream issues them). Every rank within the direct
+    schedule's single-rounding bound |y - sum| <= ulp16(y)/2 + (P-1) * 2^-24 * sum|x| of the exact
+    (fp64) sum, all ranks identical, and every bucket bit-exact vs the oracle's fp16 fold (MPICH
+    order in fp32, one rounding), compared by sha256 per bucket."""
     P, nb, buckets = 8, (16 << 20) // 2, 64
     g = torch.Generator(device=gpu).manual_seed(44)
     with config(lib, algo=1, reference_order=1, tune=0, slice_bytes=2 << 20):
         sets = []
         for b in range(buckets):
             ins = [(torch.randn(nb, device=gpu, generator=g) * 0.1).half() for _ in range(P)]
+            want = sha256(oracle.fold_ref_order(DT_HALF, [t.cpu().numpy() for t in ins]))
             x64 = torch.stack(ins).double()
-            sets.append((ins, x64.sum(0), x64.abs().sum(0)))
+            sets.append((ins, x64.sum(0), x64.abs().sum(0), want))
             del x64
-            if b == 0:
-                xs0 = [t.cpu().numpy() for t in ins]
         torch.cuda.synchronize()
-        for ins, _, _ in sets:
+        for ins, _, _, _ in sets:
             _thread_allreduce(lib, ins, ins, nb, DT_HALF)
         torch.cuda.synchronize()
-    want0 = oracle.fold_ref_order(DT_HALF, xs0)
-    assert sets[0][0][0].cpu().numpy().tobytes() == want0.tobytes()
     worst = 0.0
-    for b, (ins, exact, mag) in enumerate(sets):
-        _, e = torch.frexp(exact.half().abs().double())  # |round16(sum)| = m * 2^e, m in [0.5, 1)
-        ulp = torch.exp2((e - 11).double()).clamp_min(2.0 ** -24)
-        bound = (P - 1) * 2.0 ** -11 * mag + ulp / 2
+    for b, (ins, exact, mag, want) in enumerate(sets):
+        bound = fp16_single_rounding_bound(P, ins[0], mag)
         err = (ins[0].double() - exact).abs()
         assert bool((err <= bound).all()), b
         worst = max(worst, float((err / bound.clamp_min(1e-30)).max()))
+        assert sha256(ins[0].cpu().numpy()) == want, b
         for t in ins[1:]:
             assert torch.equal(t, ins[0]), b
     assert worst <= 1.0
