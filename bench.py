@@ -770,7 +770,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None, warm_st
             warm.append(round((time.perf_counter() - t1) * 1e3, 2))
         plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
         tl_keys = (b'host_pack_us', b'host_wait_us', b'host_unpack_us', b'host_check_us', b'host_plan_us',
-                   b'host_coll_us', b'host_d2h_post_us', b'host_unpack_submit_us')
+                   b'host_coll_us', b'host_d2h_post_us', b'host_unpack_submit_us', b'host_lane_d2h_wait_us',
+                   b'host_lane_copy_us', b'host_lane_copy_bytes', b'host_lane_jobs')
         tl0 = [lib.ddl_get_config(kk) for kk in tl_keys]
         cg0 = cgroup_cpu()
         t0 = time.perf_counter()
@@ -795,7 +796,8 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None, warm_st
         timeline = {'pack_ms': round(tl[0], 3), 'slot_wait_ms': round(tl[1], 3), 'unpack_ms': round(tl[2], 3),
                     'other_ms': round(dt * 1e3 - sum(tl[:3]), 3), 'check_ms': round(tl[3], 3),
                     'plan_ms': round(tl[4], 3), 'rest_ms': round(dt * 1e3 - tl[3] - tl[4], 3),
-                    'coll_post_ms': round(tl[5], 3), 'd2h_post_ms': round(tl[6], 3), 'unpack_submit_ms': round(tl[7], 3)}
+                    'coll_post_ms': round(tl[5], 3), 'd2h_post_ms': round(tl[6], 3), 'unpack_submit_ms': round(tl[7], 3),
+                    **lane_split(tl[8], tl[9], tl[10] * 1e3, tl[11] * 1e3)}
         registered = {'host_registered_bytes': int(lib.ddl_get_config(b'host_registered_bytes')),
                       'host_register_failures': int(lib.ddl_get_config(b'host_register_failures'))}
     finally:
@@ -812,6 +814,19 @@ def keyed_host_c5(lib, comm, steps, k=4096, pinned=False, settings=None, warm_st
             'warmup_steps_ms': warm, 'cgroup_cpu': cgroup,
             'settings': {kk: v for kk, v in settings.items() if kk != 'one_rank_shortcut'},
             **(registered if 'host_register_cache_bytes' in settings else {})}
+
+
+LANE_KEYS = (b'host_lane_d2h_wait_us', b'host_lane_copy_us', b'host_lane_copy_bytes', b'host_lane_jobs')
+
+
+def lane_split(wait_ms, copy_ms, copy_bytes, jobs):
+    """The unpack lane's two phases per step, on the lane thread: polling each
+    staged chunk's D2H event (lane_d2h_wait_ms: the DMA still running) and the pinned download
+    slot -> pageable output memcpy with the copy threads (lane_copy_ms, at lane_copy_GBs). Their
+    sum is the lane's busy time; the engine thread's unpack_ms is the part of it it waited for."""
+    return {'lane_d2h_wait_ms': round(wait_ms, 3), 'lane_copy_ms': round(copy_ms, 3),
+            'lane_copy_bytes': int(copy_bytes), 'lane_jobs': int(jobs),
+            'lane_copy_GBs': round(copy_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None}
 
 
 def keyed_host_c5_steady(comm, steps=10, warm=2, k=4096, budget_s=25.0):
@@ -878,6 +893,8 @@ def keyed_host_c5_steady(comm, steps=10, warm=2, k=4096, budget_s=25.0):
                     cur = None  # the old set goes first (its finalizers release cached ranges)
                     cur, seed = make(s), s
                     alloc.append((time.perf_counter() - t1) * 1e3)
+                if s == warm:
+                    lane0 = [lib.ddl_get_config(kk) for kk in LANE_KEYS]
                 t1 = time.perf_counter()
                 step(cur)
                 dt = (time.perf_counter() - t1) * 1e3
@@ -895,6 +912,8 @@ def keyed_host_c5_steady(comm, steps=10, warm=2, k=4096, budget_s=25.0):
                          'new_set_ms_median': round(sorted(alloc)[len(alloc) // 2], 1) if alloc else None,
                          'values_ok': ok,
                          'host_registered_bytes_after': int(lib.ddl_get_config(b'host_registered_bytes'))}
+            lane = [(lib.ddl_get_config(kk) - v) / len(ts) for kk, v in zip(LANE_KEYS, lane0)]
+            res[mode]['engine_thread'] = lane_split(lane[0] / 1e3, lane[1] / 1e3, lane[2], lane[3])
             check(lib.ddl_set_config(b'host_register_cache_bytes', 0), 'ddl_set_config')  # releases every range
     finally:
         for kk, v in old.items():
@@ -1191,6 +1210,39 @@ def multi_gpu(args):
             sub.detach()
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['compute_cu_mask_ab'] = repr(e)[:400]
+    # RCCL channel (CTA) bounds (config rccl_min_ctas / rccl_max_ctas = ncclConfig_t.minCTAs /
+    # maxCTAs): the headline allreduce on a split communicator created under
+    # each setting, beside the world's (RCCL's own channel count). Whether the direct schedule's
+    # P-1 concurrent sends / receives fill P-1 xGMI links depends on the p2p channels RCCL gives
+    # them, which these bounds cap; DESIGN §8 reads the default off this field. Every rank sets
+    # the same values in the same order (shared tunables).
+    state['leg'] = 'rccl_cta_sweep'
+    try:
+        if not args.no_config_sweep:
+            cta = []
+            reps = max(5, args.steps // 2)
+            t_world = timed_fn(lambda: step(0), reps, 3)
+            for lo, hi in ((8, 8), (16, 16), (32, 32), (64, 64)):
+                check(lib.ddl_set_config(b'rccl_min_ctas', lo), 'ddl_set_config')
+                check(lib.ddl_set_config(b'rccl_max_ctas', hi), 'ddl_set_config')
+                try:
+                    sub = comm.split_communicator(0, rank)
+                finally:
+                    check(lib.ddl_set_config(b'rccl_min_ctas', 0), 'ddl_set_config')
+                    check(lib.ddl_set_config(b'rccl_max_ctas', 0), 'ddl_set_config')
+
+                def sub_step(sub=sub):
+                    check(lib.ddl_allreduce(sub.id, send.data_ptr(), recv.data_ptr(), n, DT_FLOAT, 0,
+                                            stream.cuda_stream), 'ddl_allreduce (cta split)')
+                t = timed_fn(sub_step, reps, 3)  # the first warmup call tunes the new communicator
+                cta.append({'min_ctas': lo, 'max_ctas': hi, 'ms': round(t * 1e3, 4),
+                            'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2),
+                            'speedup_vs_default': round(t_world / t, 4)})
+                sub.detach()
+                out['rccl_cta_sweep'] = {'default_ms': round(t_world * 1e3, 4), 'bucket_bytes': S,
+                                         'settings': cta}
+    except Exception as e:  # a failed optional leg must not cost the headline line
+        out.setdefault('leg_errors', {})['rccl_cta_sweep'] = repr(e)[:400]
     # fixed schedules, tuner off (every rank sets the same values in the same order: the
     # schedule must be identical on all ranks)
     state['leg'] = 'schedule_sweep'

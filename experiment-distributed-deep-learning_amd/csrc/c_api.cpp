@@ -101,6 +101,8 @@ int ddl_control_stats(long long *string_rounds, long long *cached_rounds) {
 int ddl_finalize(void) {
     return guarded([&] {
         Registry::get().clear();
+        DDL_REQUIRE(wait_deferred_deletions(60000), DDL_STATUS_ERROR_UNKNOWN,
+                    "a communicator released by its own handler thread is still being destroyed after 60 s");
         standalone_control() = std::make_shared<ControlChannel>();
         run_finalize_hooks();
     });
@@ -158,6 +160,10 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, DDL_STATUS_INVALID_ARGUMENT,
                         "compute_cu_mask must be 0 (all CUs), 2, 4 or 8 (every n-th CU left to RCCL)");
             c.compute_cu_mask = value;
+        } else if (k == "rccl_min_ctas" || k == "rccl_max_ctas") {
+            DDL_REQUIRE(value >= 0 && value <= 256, DDL_STATUS_INVALID_ARGUMENT,
+                        k << " must be 0 (RCCL's default) or a channel count in [1, 256]");
+            (k == "rccl_min_ctas" ? c.rccl_min_ctas : c.rccl_max_ctas) = value;
         } else if (k == "fold_form") {
             DDL_REQUIRE(value >= 0 && value <= 2, DDL_STATUS_INVALID_ARGUMENT,
                         "fold_form must be 0 (auto), 1 (tile form) or 2 (run form)");
@@ -198,6 +204,10 @@ long long ddl_get_config(const char *key) {
     if (k == "host_coll_us") return c.host_coll_ns / 1000;      // statistic, not settable
     if (k == "host_d2h_post_us") return c.host_d2h_post_ns / 1000;  // statistic, not settable
     if (k == "host_unpack_submit_us") return c.host_unpack_submit_ns / 1000;  // statistic, not settable
+    if (k == "host_lane_d2h_wait_us") return c.host_lane_d2h_wait_ns / 1000;  // statistic, not settable
+    if (k == "host_lane_copy_us") return c.host_lane_copy_ns / 1000;          // statistic, not settable
+    if (k == "host_lane_copy_bytes") return c.host_lane_copy_bytes;           // statistic, not settable
+    if (k == "host_lane_jobs") return c.host_lane_jobs;                       // statistic, not settable
     if (k == "fusion_pipeline_bytes") return c.fusion_pipeline_bytes;
     if (k == "one_rank_shortcut") return c.one_rank_shortcut;
     if (k == "pipeline_rounds") return c.pipeline_rounds;
@@ -205,6 +215,8 @@ long long ddl_get_config(const char *key) {
     if (k == "capture_mode") return c.capture_mode;
     if (k == "fold_form") return get_fold_form();
     if (k == "compute_cu_mask") return c.compute_cu_mask;
+    if (k == "rccl_min_ctas") return c.rccl_min_ctas;
+    if (k == "rccl_max_ctas") return c.rccl_max_ctas;
     return -1;
 }
 

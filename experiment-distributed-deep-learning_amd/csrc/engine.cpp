@@ -2,6 +2,8 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -39,7 +41,8 @@ Config &config() {
 uint64_t Config::shared_hash() const {
     const long long v[] = {algo.load(), slice_bytes.load(), rings.load(), max_slices.load(),
                            fusion_threshold_bytes.load(), tune.load(), fusion_pipeline_bytes.load(),
-                           reference_order.load(), host_chunk_bytes.load()};
+                           reference_order.load(), host_chunk_bytes.load(), rccl_min_ctas.load(),
+                           rccl_max_ctas.load()};
     uint64_t h = 1469598103934665603ull;  // FNV-1a over the values' bytes
     for (long long x : v)
         for (int b = 0; b < 8; ++b) {
@@ -205,7 +208,8 @@ void check_config_agreement(int rank, const std::vector<uint64_t> &hashes) {
     if (same) return;
     std::ostringstream os;
     os << "shared tunables differ between ranks (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, "
-          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes must be set alike on every rank); "
+          "tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes, rccl_min_ctas, rccl_max_ctas must be "
+          "set alike on every rank); "
           "config hash per rank:";
     for (size_t q = 0; q < hashes.size(); ++q)
         os << " " << q << (q == (size_t)rank ? "*" : "") << "=" << std::hex << hashes[q] << std::dec;
@@ -699,19 +703,42 @@ void Communicator::enable_keyed(std::shared_ptr<ControlChannel> ch) {
     if (size_ > 1 && !keyed_data_) keyed_data_ = split(0, rank_, false);
 }
 
+// The ncclConfig_t of a new communicator: RCCL's defaults but for the CTA bounds the config
+// names (0 = undefined). *custom says whether anything differs from ncclCommInitRank's defaults.
+static ncclConfig_t rccl_comm_config(bool *custom) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    const long long lo = config().rccl_min_ctas.load(), hi = config().rccl_max_ctas.load();
+    DDL_REQUIRE(!lo || !hi || lo <= hi, DDL_STATUS_INVALID_ARGUMENT,
+                "rccl_min_ctas " << lo << " > rccl_max_ctas " << hi);
+    if (lo) cfg.minCTAs = (int)lo;
+    if (hi) cfg.maxCTAs = (int)hi;
+    *custom = lo || hi;
+    return cfg;
+}
+
 ncclComm_t rccl_init_rank(int rank, int size, const void *unique_id, size_t len) {
     DDL_REQUIRE(unique_id && len >= sizeof(ncclUniqueId), DDL_STATUS_INVALID_ARGUMENT,
                 "unique id of " << sizeof(ncclUniqueId) << " bytes required");
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof id);
     ncclComm_t nc = nullptr;
-    rccl_check(rccl().CommInitRank(&nc, size, id, rank), "ncclCommInitRank");
+    bool custom = false;
+    ncclConfig_t cfg = rccl_comm_config(&custom);
+    if (rccl().CommInitRankConfig) {
+        rccl_check(rccl().CommInitRankConfig(&nc, size, id, rank, &cfg), "ncclCommInitRankConfig");
+    } else {
+        DDL_REQUIRE(!custom, DDL_STATUS_COMM_ERROR,
+                    "rccl_min_ctas / rccl_max_ctas need ncclCommInitRankConfig, which " << rccl().path << " lacks");
+        rccl_check(rccl().CommInitRank(&nc, size, id, rank), "ncclCommInitRank");
+    }
     return nc;
 }
 
 ncclComm_t rccl_split(ncclComm_t parent, int color, int key, int *rank, int *size) {
     ncclComm_t nc = nullptr;
-    rccl_check(rccl().CommSplit(parent, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, nullptr), "ncclCommSplit");
+    bool custom = false;
+    ncclConfig_t cfg = rccl_comm_config(&custom);
+    rccl_check(rccl().CommSplit(parent, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &nc, &cfg), "ncclCommSplit");
     if (!nc) return nullptr;
     rccl_check(rccl().CommCount(nc, size), "ncclCommCount");
     rccl_check(rccl().CommUserRank(nc, rank), "ncclCommUserRank");
@@ -765,12 +792,47 @@ RequestHandler &Communicator::handler() {
 // ---- registry ------------------------------------------------------------------------------
 thread_local bool t_handler_thread = false;
 
+// Deferred deletions (a communicator whose last owner was one of its own handler's threads: its
+// destructor joins those threads, so it runs on a thread of its own). They are counted, and
+// ddl_finalize and process exit wait for them: the destructor's SHUT_DOWN lap,
+// ncclCommDestroy and hipStreamDestroy must not race HIP / RCCL teardown or finalize hooks.
+// Heap-allocated and never freed, so the exit hook never sees them destroyed.
+namespace {
+struct Reaper {
+    std::mutex mu;
+    std::condition_variable cv;
+    int pending = 0;
+};
+Reaper &reaper() {
+    static Reaper *r = new Reaper();
+    return *r;
+}
+void wait_deferred_deletions_at_exit() { wait_deferred_deletions(10000); }
+}  // namespace
+
+bool wait_deferred_deletions(long long limit_ms) {
+    Reaper &r = reaper();
+    std::unique_lock<std::mutex> g(r.mu);
+    return r.cv.wait_for(g, std::chrono::milliseconds(limit_ms), [&] { return r.pending == 0; });
+}
+
 void CommunicatorDeleter::operator()(Communicator *c) const {
     if (!t_handler_thread) {
         delete c;
         return;
     }
-    std::thread([c] { delete c; }).detach();
+    static const bool at_exit = std::atexit(wait_deferred_deletions_at_exit) == 0;
+    (void)at_exit;
+    Reaper &r = reaper();
+    {
+        std::lock_guard<std::mutex> g(r.mu);
+        ++r.pending;
+    }
+    std::thread([c, &r] {
+        delete c;
+        std::lock_guard<std::mutex> g(r.mu);
+        if (--r.pending == 0) r.cv.notify_all();
+    }).detach();
 }
 
 Registry &Registry::get() {

@@ -81,6 +81,14 @@ struct Config {
     std::atomic<long long> host_coll_ns{0};
     std::atomic<long long> host_d2h_post_ns{0};
     std::atomic<long long> host_unpack_submit_ns{0};
+    // the unpack lane's jobs (staged outputs of keyed host plans), on the lane's thread: polling
+    // the chunk's D2H event (host_lane_d2h_wait_us), then the pinned download slot -> output
+    // memcpy with the copy threads (host_lane_copy_us, host_lane_copy_bytes), per job
+    // (host_lane_jobs)
+    std::atomic<long long> host_lane_d2h_wait_ns{0};
+    std::atomic<long long> host_lane_copy_ns{0};
+    std::atomic<long long> host_lane_copy_bytes{0};
+    std::atomic<long long> host_lane_jobs{0};
     // autotune the schedule per bucket-size class on first use (P > 1): 1 on, 0 use the
     // fields above as set
     std::atomic<long long> tune{1};
@@ -115,11 +123,21 @@ struct Config {
     // sharing one GPU ran their collectives 2.6x slower with it — off until a node
     // measures it (bench leg compute_cu_mask_ab). Read when an executor is created; local.
     std::atomic<long long> compute_cu_mask{0};
+    // RCCL communicator configuration (ncclConfig_t.minCTAs / maxCTAs): the
+    // bounds on the channel (CTA) count RCCL gives a communicator, which also caps its p2p
+    // channels — whether the direct schedule's 7 concurrent sends and receives per tick fill
+    // 7 xGMI links depends on it. 0 = NCCL_CONFIG_UNDEF_INT (RCCL's own choice, the default).
+    // Read when a communicator is created (ddl_init, ddl_comm_split, the keyed data plane's
+    // private split); shared (in shared_hash): ranks with different channel counts would post
+    // mismatched RCCL kernels.
+    std::atomic<long long> rccl_min_ctas{0};
+    std::atomic<long long> rccl_max_ctas{0};
     // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'
     // programs, the fusion plans and the host chunks): algo, slice_bytes, rings, max_slices,
-    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes.
+    // fusion_threshold_bytes, tune, fusion_pipeline_bytes, reference_order, host_chunk_bytes,
+    // rccl_min_ctas, rccl_max_ctas.
     // Never 0 or kCfgMismatch. Local tunables (log_level, cycle_time_us, host_copy_threads,
     // host_zero_copy, pipeline_rounds, one_rank_shortcut) are not in it.
     uint64_t shared_hash() const;
@@ -299,6 +317,9 @@ extern thread_local bool t_handler_thread;
 struct CommunicatorDeleter {
     void operator()(Communicator *c) const;
 };
+// Waits up to limit_ms for the communicators being deleted off their handlers' threads; false on
+// timeout. ddl_finalize calls it (and an exit hook, 10 s).
+bool wait_deferred_deletions(long long limit_ms);
 
 // every Communicator is owned through this (make_shared would bypass the deleter)
 template <class... A>

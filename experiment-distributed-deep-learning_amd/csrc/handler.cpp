@@ -1046,12 +1046,23 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         host_pieces_(segs, starts, cut[j], cut[j + 1] - cut[j], static_cast<char *>(pout_[k]), false, pc);
         const hipEvent_t landed = hev_[3 * k + 2];  // re-recorded only after this job (wait_unpack)
         CopyPool *op = out_pool_.get();
-        unpacked[j] = lane_->submit([dev, landed, op, pc = std::move(pc)] {
+        unpacked[j] = lane_->submit([dev, landed, op, ns_since, pc = std::move(pc)] {
             DeviceGuard g(dev);
-            // D2H of chunk j landed (polled: see wait_plan)
+            // D2H of chunk j landed (polled: see wait_plan). The lane's two phases are timed apart
+            // (config "host_lane_d2h_wait_us" / "host_lane_copy_us" / "host_lane_copy_bytes",
+            // VERDICT r5 next #4): the wait says how long the DMA kept the lane, the copy what
+            // rate the pinned download slot -> pageable output memcpy reaches
+            clk::time_point t0 = clk::now();
             const hipError_t q = wait_plan(landed);
+            config().host_lane_d2h_wait_ns.fetch_add(ns_since(t0));
             DDL_REQUIRE(q == hipSuccess, DDL_STATUS_HIP_ERROR, "D2H of a staged chunk: " << hipGetErrorString(q));
+            t0 = clk::now();
             op->run(pc);
+            config().host_lane_copy_ns.fetch_add(ns_since(t0));
+            long long bytes = 0;
+            for (const CopyPool::Piece &p : pc) bytes += (long long)p.bytes;
+            config().host_lane_copy_bytes.fetch_add(bytes);
+            config().host_lane_jobs.fetch_add(1);
         });
     };
     auto wait_unpack = [&](size_t j) {
@@ -1137,6 +1148,13 @@ void RequestHandler::host_staged_(const std::vector<HostSeg> &segs, size_t es, b
         for (size_t j = nchunks > (size_t)kHostSlots ? nchunks - kHostSlots : 0; j < nchunks; ++j) wait_unpack(j);
     } catch (...) {
         lane_->drain();
+        // device-unpack plans: copier kernels of the chunks already posted on d2h_ write into the
+        // caller's pinned outputs; they must finish before done(error) lets the caller free those
+        // (ADVICE r5). The H2D / compute work of posted chunks reads the caller's inputs and the
+        // slots: drained too, so the next plan starts from idle streams.
+        (void)hipStreamSynchronize(h2d_);
+        (void)hipStreamSynchronize(stream_);
+        (void)hipStreamSynchronize(d2h_);
         throw;
     }
 }

@@ -74,6 +74,8 @@ const RcclApi &rccl() {
             bind(h, api.CommCount, "ncclCommCount");
             bind(h, api.CommUserRank, "ncclCommUserRank");
             bind(h, api.GetErrorString, "ncclGetErrorString");
+            api.CommInitRankConfig =
+                reinterpret_cast<decltype(api.CommInitRankConfig)>(dlsym(h, "ncclCommInitRankConfig"));
             api.path = path.c_str();
         } catch (const Error &e) {
             err = e.msg;

@@ -77,9 +77,17 @@ class LearningRateSchedule:
     `on_epoch_begin(epoch)`, `on_batch_begin(batch)` / `on_batch_end(batch)` around every step,
     `on_epoch_end(epoch, logs)`. Between `start_epoch` and `end_epoch` every parameter group's lr
     is `initial_lr * multiplier(epoch)` — at the first batch of an epoch with `staircase`, else
-    at every batch with the fractional epoch `epoch + batch / steps_per_epoch`. With
-    `momentum_correction` a group's momentum (SGD's `momentum`, what Keras' `optimizer.momentum`
-    is) is scaled by new_lr / old_lr for that one batch and restored after it.
+    at every batch with the fractional epoch `epoch + batch / steps_per_epoch`.
+
+    `momentum_correction` (Goyal et al.; reference :58-66) scales a group's momentum by
+    new_lr / old_lr for the one batch whose lr changed and restores it after. It exists for
+    optimizers that keep the lr INSIDE the velocity, as Keras' SGD does (v = m*v - lr*g): there an
+    lr change would otherwise reach the step only gradually. torch's SGD keeps it outside
+    (buf = m*buf + g; p -= lr*buf), so an lr change takes effect at once and rescaling the momentum
+    would change the dynamics instead of preserving them. Default None = automatic: on
+    only for an optimizer that declares `lr_scaled_velocity = True`; every torch.optim optimizer
+    gets no correction — which is what the reference's correction achieves on Keras. True forces
+    it (an optimizer that stores lr-scaled velocity without declaring it), False turns it off.
 
     `initial_lr`: None takes each group's lr at `on_train_begin` (the reference reads the
     optimizer's single lr); a number sets every group from it. `steps_per_epoch`: needed unless
@@ -87,11 +95,13 @@ class LearningRateSchedule:
     'samples' and 'batch_size', :29-43)."""
 
     def __init__(self, optimizer, multiplier, start_epoch=0, end_epoch=None, staircase=True,
-                 momentum_correction=True, steps_per_epoch=None, initial_lr=None):
+                 momentum_correction=None, steps_per_epoch=None, initial_lr=None):
         self.optimizer = optimizer
         self.start_epoch = start_epoch
         self.end_epoch = end_epoch
         self.staircase = staircase
+        if momentum_correction is None:
+            momentum_correction = bool(getattr(optimizer, 'lr_scaled_velocity', False))
         self.momentum_correction = momentum_correction
         self.initial_lr = initial_lr
         self.restore_momentum = None
@@ -168,7 +178,7 @@ class LearningRateWarmup(LearningRateSchedule):
     e the fractional epoch. The scripts scale the base lr by the size first (the reference's
     examples/data_parallelism.py:73-101). `verbose` prints only on rank 0."""
 
-    def __init__(self, optimizer, warmup_epochs=5, momentum_correction=True, steps_per_epoch=None, verbose=0,
+    def __init__(self, optimizer, warmup_epochs=5, momentum_correction=None, steps_per_epoch=None, verbose=0,
                  initial_lr=None, communicator: Communicator = None):
         comm = Communicator.world() if communicator is None else communicator
 

@@ -198,6 +198,7 @@ class _Completion:
     __slots__ = ('ptr', 'count', 'keep', 'final', '__weakref__')
     _inflight = collections.deque()  # groups in submission order, slots maybe pending: their tensors
     _inflight_lock = threading.Lock()
+    _sweep_at = 64  # a full sweep of _inflight once it holds this many groups (then 2x the survivors)
 
     def __init__(self, count: int, keep):
         lib = CPPBackend.c_api()
@@ -207,12 +208,24 @@ class _Completion:
         self.count, self.keep, self.final = count, keep, None
         weakref.finalize(self, lib.ddl_completion_destroy, self.ptr)
         with _Completion._inflight_lock:
-            # release the oldest groups that completed (the engine completes rounds in submission
-            # order, so the sweep stops at the first pending one: O(1) amortised per submission,
-            # also with one group per gradient under overlap_backward)
+            # release the groups that completed. Most complete in submission order (one
+            # communicator's rounds), so the head is swept at every submission; but keyed requests
+            # complete only once every rank registered the key, and communicators complete
+            # independently, so a pending group may sit in front of completed ones:
+            # once the deque doubled since the last full sweep, every group is looked at. O(1)
+            # amortised per submission either way.
             q = _Completion._inflight
             while q and (q[0].keep is None or lib.ddl_completion_poll(q[0].ptr, None, 0) == 0):
                 q.popleft().keep = None
+            if len(q) >= _Completion._sweep_at:
+                live = collections.deque()
+                for g in q:
+                    if g.keep is None or lib.ddl_completion_poll(g.ptr, None, 0) == 0:
+                        g.keep = None
+                    else:
+                        live.append(g)
+                _Completion._inflight = q = live
+                _Completion._sweep_at = max(64, 2 * len(live))
             q.append(self)
 
     def slots(self, first: int = 0, count: int = None):

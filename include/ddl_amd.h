@@ -151,7 +151,11 @@ int ddl_is_initialized(void);
  * 2nd CU, which stay free for RCCL; each masked stream takes a hardware queue of its own; read
  * when a communicator's executor / handler is created), "fold_form" (0, default:
  * the N-input fold in its run form from 4 MiB chunks of 7+ inputs, its tile form otherwise; 1 /
- * 2: always the tile / run form),
+ * 2: always the tile / run form), "rccl_min_ctas" / "rccl_max_ctas" (0, default: RCCL's own
+ * choice, NCCL_CONFIG_UNDEF_INT; 1..256: ncclConfig_t.minCTAs / maxCTAs of every RCCL
+ * communicator created afterwards — ddl_init's ncclCommInitRankConfig, ddl_comm_split's and the
+ * keyed data plane's ncclCommSplit — bounding its channel count and with it the p2p channels the
+ * direct schedule's concurrent sends and receives spread over; shared tunables),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "pipeline_rounds" (1,
@@ -165,7 +169,8 @@ int ddl_is_initialized(void);
  * slice size) per bucket-size class (floor(log2 bytes)) the first time it sees that class: a
  * collective timing of a fixed candidate list on scratch buffers, max over ranks, argmin.
  * The shared tunables (algo, slice_bytes, rings, max_slices, fusion_threshold_bytes, tune,
- * fusion_pipeline_bytes, reference_order, host_chunk_bytes) must be equal on every rank of a
+ * fusion_pipeline_bytes, reference_order, host_chunk_bytes, rccl_min_ctas, rccl_max_ctas) must
+ * be equal on every rank of a
  * communicator. Direct collectives: the ranks exchange a hash of them at a communicator's first
  * collective and at the next collective after this rank's values changed; a mismatch found there
  * fails that collective on every rank with DDL_STATUS_CONFIG_MISMATCH instead of building

@@ -175,6 +175,12 @@ def test_config_roundtrip(lib):
     assert lib.ddl_set_config(b'compute_cu_mask', 3) == 3
     for v in (2, 4, 8, 0):
         assert lib.ddl_set_config(b'compute_cu_mask', v) == 0 and lib.ddl_get_config(b'compute_cu_mask') == v
+    # RCCL communicator CTA bounds (ncclConfig_t.minCTAs / maxCTAs): 0 = RCCL's default
+    for key in (b'rccl_min_ctas', b'rccl_max_ctas'):
+        assert lib.ddl_get_config(key) == 0
+        assert lib.ddl_set_config(key, -1) == 3 and lib.ddl_set_config(key, 257) == 3
+        for v in (1, 32, 256, 0):
+            assert lib.ddl_set_config(key, v) == 0 and lib.ddl_get_config(key) == v
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
     assert lib.ddl_set_config(b'fold_form', 3) == 3

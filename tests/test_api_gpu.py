@@ -469,14 +469,17 @@ def test_keyed_host_requests_data_plane(world, lib, chunk, memory):
             lib.ddl_set_config(k, v)
 
 
-def test_host_plan_failure_drains_unpacks(world, lib):
+@pytest.mark.parametrize('zero_copy', [0, 1])
+def test_host_plan_failure_drains_unpacks(world, lib, zero_copy):
     """a host plan whose staging loop fails midway — here its collective at
     chunk 8, past the 4 download slots, so unpack jobs of earlier chunks are queued on the unpack
     lane — reports the error only once every unpack already submitted has written its chunk:
     after done(error) the output never changes again (the caller may free it then). Chunks 0-7
     hold the input, the rest is untouched. A failed keyed collective stops its communicator's
     handler by design (later submissions there are refused), so the fault runs on a split
-    communicator of its own; the world's handler keeps working."""
+    communicator of its own; the world's handler keeps working. ADVICE r5: also with pinned
+    tensors and host_zero_copy 1, where the unpack kernel writes the outputs over PCIe from d2h_ —
+    those kernels must have finished before done(error) too."""
     import time
 
     import _helpers as h
@@ -485,9 +488,12 @@ def test_host_plan_failure_drains_unpacks(world, lib):
     chunk = 256 << 10
     x = torch.arange(3_000_017, dtype=torch.float32)
     out = torch.full_like(x, -7.0)
+    if zero_copy:
+        x, out = x.pin_memory(), out.pin_memory()
+    plans0 = lib.ddl_get_config(b'host_zero_copy_plans')
     sub = world.split_communicator(0)
     try:
-        with h.config(lib, one_rank_shortcut=0, host_chunk_bytes=chunk, host_zero_copy=0):
+        with h.config(lib, one_rank_shortcut=0, host_chunk_bytes=chunk, host_zero_copy=zero_copy):
             assert lib.ddl_testing_host_coll_fault(8) == 0
             try:
                 hd = allreduce_async(x, 'fault_plan', sub, output=out)
@@ -498,6 +504,7 @@ def test_host_plan_failure_drains_unpacks(world, lib):
                 assert torch.equal(out, snap), 'the output changed after done(error)'
             finally:
                 assert lib.ddl_testing_host_coll_fault(-1) == 0
+            assert (lib.ddl_get_config(b'host_zero_copy_plans') > plans0) == bool(zero_copy)
             k = 8 * chunk // 4
             assert torch.equal(out[:k], x[:k])
             assert bool((out[k:] == -7.0).all())

@@ -3,7 +3,9 @@ src/py/ddl/tensorflow/keras/parallelism/data/lr_warm_up_callback.py:6-124) again
 
     lr(epoch e, batch b) = initial_lr / size * ((e + (b + 1) / steps) * (size - 1) / warmup + 1)
 
-for e < warmup, the momentum scaled by new_lr / old_lr during the batch and restored after it, the
+for e < warmup; torch SGD's momentum left alone (its velocity does not hold the lr),
+and with the correction forced (an optimizer keeping lr-scaled velocity, as Keras' SGD) the momentum
+scaled by new_lr / old_lr during the batch and restored after it; the
 lr left at initial_lr once the warm-up ends, and the closing message printed on rank 0 only. The
 callbacks communicate nothing; they read the communicator's size and rank. Sizes 1, 2 and 8: in one
 process with a stand-in communicator, and as gloo process groups whose ranks compare traces."""
@@ -31,14 +33,15 @@ def _expected(initial, size, warmup, steps, e, b):
     return initial / size * ((e + (b + 1) / steps) * (size - 1) / warmup + 1)
 
 
-def _train(comm, epochs=3, steps=4, warmup=2, lr=0.4, momentum=0.9, verbose=1):
+def _train(comm, epochs=3, steps=4, warmup=2, lr=0.4, momentum=0.9, verbose=1, correction=None):
     """A Keras-shaped loop over an SGD optimizer with two parameter groups; returns, per batch,
     (lr of each group during the batch, momentum during the batch, momentum after it), the logs'
     lr per epoch and what was printed."""
     from ddl.torch.parallelism.data import LearningRateWarmup
     w1, w2 = torch.nn.Parameter(torch.ones(3)), torch.nn.Parameter(torch.ones(2))
     opt = torch.optim.SGD([{'params': [w1]}, {'params': [w2], 'lr': lr / 2}], lr=lr, momentum=momentum)
-    cb = LearningRateWarmup(opt, warmup_epochs=warmup, steps_per_epoch=steps, verbose=verbose, communicator=comm)
+    cb = LearningRateWarmup(opt, warmup_epochs=warmup, steps_per_epoch=steps, verbose=verbose, communicator=comm,
+                            momentum_correction=correction)
     trace, logs_lr = [], []
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
@@ -58,14 +61,18 @@ def _train(comm, epochs=3, steps=4, warmup=2, lr=0.4, momentum=0.9, verbose=1):
     return trace, logs_lr, buf.getvalue()
 
 
-def _check_trace(trace, logs_lr, printed, size, rank, epochs=3, steps=4, warmup=2, lr=0.4, momentum=0.9):
+def _check_trace(trace, logs_lr, printed, size, rank, epochs=3, steps=4, warmup=2, lr=0.4, momentum=0.9,
+                 corrected=False):
     prev = [lr, lr / 2]
     for i, (lrs, m_during, m_after) in enumerate(trace):
         e, b = divmod(i, steps)
         if e < warmup:
             want = [_expected(lr, size, warmup, steps, e, b), _expected(lr / 2, size, warmup, steps, e, b)]
             assert lrs == pytest.approx(want, rel=1e-12), (e, b)
-            assert m_during == pytest.approx(momentum * want[0] / prev[0], rel=1e-12), (e, b)
+            if corrected:
+                assert m_during == pytest.approx(momentum * want[0] / prev[0], rel=1e-12), (e, b)
+            else:  # torch SGD: lr outside the velocity, nothing to correct
+                assert m_during == momentum, (e, b)
         else:  # after the warm-up the lr stays where the last warm-up batch left it: initial_lr
             want = prev
             assert lrs == pytest.approx([lr, lr / 2], rel=1e-12), (e, b)
@@ -84,6 +91,24 @@ def test_warmup_formula_in_process(size, rank):
     sys.path.insert(0, PKG)
     trace, logs_lr, printed = _train(_Comm(rank, size))
     _check_trace(trace, logs_lr, printed, size, rank)
+
+
+@pytest.mark.parametrize('size', [2, 8])
+def test_momentum_correction_only_for_lr_scaled_velocity(size):
+    """Default: torch.optim.SGD gets no momentum rescale (its first warm-up batch would otherwise
+    drop momentum to about m / size). An optimizer declaring lr_scaled_velocity gets the
+    reference's correction automatically; momentum_correction=True forces it."""
+    sys.path.insert(0, PKG)
+    from ddl.torch.parallelism.data import LearningRateWarmup
+    trace, logs_lr, printed = _train(_Comm(0, size), correction=True)
+    _check_trace(trace, logs_lr, printed, size, 0, corrected=True)
+    w = torch.nn.Parameter(torch.ones(2))
+    opt = torch.optim.SGD([w], lr=0.4, momentum=0.9)
+    assert not LearningRateWarmup(opt, steps_per_epoch=4, communicator=_Comm(0, size)).momentum_correction
+    opt.lr_scaled_velocity = True
+    assert LearningRateWarmup(opt, steps_per_epoch=4, communicator=_Comm(0, size)).momentum_correction
+    assert not LearningRateWarmup(opt, steps_per_epoch=4, communicator=_Comm(0, size),
+                                  momentum_correction=False).momentum_correction
 
 
 def test_schedule_staircase_constant_multiplier_and_autodetect():

@@ -107,6 +107,28 @@ def test_torch_mirror_handles_over_a_group(lib):
     assert h.wait() is a and one.keep is None and one.final == [0]
 
 
+def test_completed_groups_behind_a_pending_one_are_released(lib):
+    """groups complete out of submission order (keyed requests wait for every rank,
+    communicators complete independently). A group left pending at the head must not pin the
+    tensors of the completed groups behind it: once the deque doubled since the last full sweep,
+    every completed group goes, and the deque stays bounded."""
+    import torch
+
+    from ddl.torch import tensor_communicate as tc
+    stuck = tc._Completion(1, (torch.zeros(1),))  # never completed until the end
+    done = []
+    for i in range(300):
+        g = tc._Completion(1, (torch.zeros(1),))
+        lib.ddl_completion_done(0, g.slots()[0])
+        done.append(g)
+    assert stuck in tc._Completion._inflight
+    assert len(tc._Completion._inflight) < 130, len(tc._Completion._inflight)
+    assert sum(g.keep is not None for g in done) < 130
+    lib.ddl_completion_done(0, stuck.slots()[0])
+    tc._Completion(0, ())
+    assert stuck not in tc._Completion._inflight and stuck.keep is None
+
+
 def test_native_completion_is_cheaper_than_python_callbacks(lib):
     """4096 completions fired from a native thread (an ordinary ddl_done_fn caller), then waited
     for handle by handle through the mirror: the whole batch in a few ms (a Python done() per
