@@ -44,6 +44,7 @@ def parse():
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--bucket-mib', type=int, default=256)
+    ap.add_argument('--no-cta-sweep', action='store_true', help='N>1: skip the RCCL channel-bound sweep')
     ap.add_argument('--no-sweep', action='store_true')
     ap.add_argument('--no-variants', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -1090,10 +1091,7 @@ def multi_gpu(args):
     check(lib.ddl_tune_result(comm.id, S, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms, 32),
           'ddl_tune_result')
     if chosen.value >= 0:
-        cands = [{'algo': algo_name(cfgs[4 * i]), 'rings': cfgs[4 * i + 1],
-                  'slice_KiB': cfgs[4 * i + 2] >> 10, 'max_slices': cfgs[4 * i + 3],
-                  'ms': round(tms[i], 4)} for i in range(min(count.value, 32))]
-        tune = {'chosen': cands[chosen.value], 'candidates': cands}
+        tune = tuner_table(chosen, count, cfgs, tms)
     # correctness spot check: every rank's sum must match (checksum of checksums)
     step(0)
     torch.cuda.synchronize()
@@ -1216,9 +1214,13 @@ def multi_gpu(args):
     # P-1 concurrent sends / receives fill P-1 xGMI links depends on the p2p channels RCCL gives
     # them, which these bounds cap; DESIGN §8 reads the default off this field. Every rank sets
     # the same values in the same order (shared tunables).
+    # The tuner is off for the whole leg (every rank alike), so the world and each split run the
+    # same configured schedule and only the channel bounds differ.
     state['leg'] = 'rccl_cta_sweep'
+    tune_before = lib.ddl_get_config(b'tune')
     try:
-        if not args.no_config_sweep:
+        if not args.no_cta_sweep:
+            check(lib.ddl_set_config(b'tune', 0), 'ddl_set_config')
             cta = []
             reps = max(5, args.steps // 2)
             t_world = timed_fn(lambda: step(0), reps, 3)
@@ -1239,10 +1241,12 @@ def multi_gpu(args):
                             'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2),
                             'speedup_vs_default': round(t_world / t, 4)})
                 sub.detach()
-                out['rccl_cta_sweep'] = {'default_ms': round(t_world * 1e3, 4), 'bucket_bytes': S,
+                out['rccl_cta_sweep'] = {'default_ms': round(t_world * 1e3, 4), 'bucket_bytes': S, 'tune': 0,
                                          'settings': cta}
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['rccl_cta_sweep'] = repr(e)[:400]
+    finally:
+        lib.ddl_set_config(b'tune', tune_before)
     # fixed schedules, tuner off (every rank sets the same values in the same order: the
     # schedule must be identical on all ranks)
     state['leg'] = 'schedule_sweep'
@@ -1289,6 +1293,13 @@ def multi_gpu(args):
                                        'algbw_GiBs': round((1 << 30) / GiB / t, 2),
                                        'busbw_GBs': round(2 * (world - 1) / world * (1 << 30) / t / 1e9, 2),
                                        'path': 'one ddl_allreduce per bucket: ' + executor_path}
+            # the tuner's table for the 16 MiB class (its candidates include 4 and 8 slices per
+            # chunk, so a slice's fold can run under the next slice's reduce-scatter)
+            c4_chosen, c4_count = ctypes.c_int(-1), ctypes.c_int(0)
+            check(lib.ddl_tune_result(comm.id, 16 << 20, ctypes.byref(c4_chosen), ctypes.byref(c4_count), cfgs, tms,
+                                      32), 'ddl_tune_result')
+            if c4_chosen.value >= 0:
+                out['c4_fp16_64x16MiB']['tuner'] = tuner_table(c4_chosen, c4_count, cfgs, tms)
             # the same 64 buckets as ONE grouped call (ddl_allreduce_batch): one RCCL group per tick for
             # every bucket, the folds of 8 buckets per launch; bit-identical sums
             V = ctypes.c_void_p * 64
@@ -1436,6 +1447,13 @@ def multi_gpu(args):
     finalize()
     dist.destroy_process_group()
     dog.cancel()
+
+
+def tuner_table(chosen, count, cfgs, tms):
+    """ddl_tune_result's record as {'chosen', 'candidates'} (slice_KiB per chunk slice)."""
+    cands = [{'algo': algo_name(cfgs[4 * i]), 'rings': cfgs[4 * i + 1], 'slice_KiB': cfgs[4 * i + 2] >> 10,
+              'max_slices': cfgs[4 * i + 3], 'ms': round(tms[i], 4)} for i in range(min(count.value, 32))]
+    return {'chosen': cands[chosen.value], 'candidates': cands}
 
 
 ALGO_NAMES = ('ring', 'direct', 'oneshot', 'gatherfold', 'direct_gather')  # schedule.h enum Algo

@@ -337,6 +337,11 @@ std::vector<RingConfig> tune_candidates(int P, size_t bytes, const RingConfig &b
         add(kAlgoDirect, 1, 512u << 10, 16);
         add(kAlgoDirect, 1, 8u << 20, 8);
         add(kAlgoDirect, 1, 64u << 20, 8);
+        // chunks of up to 4 MiB (a 16 MiB fp16 C4 bucket at P = 8: 2 MiB chunks) also in 8 slices
+        // of 256 KiB, so the fold of slice k runs under the reduce-scatter of slice k+1 and only
+        // the last eighth of the chunk's fold stays on the bucket's critical path (VERDICT r5
+        // next #6; 512 KiB gives 4). More groups cost RCCL group latency: the tuner decides.
+        if (bytes <= (size_t)P * (4u << 20)) add(kAlgoDirect, 1, 256u << 10, 16);
         // the same reduce-scatter, the allgather as one ncclAllGather (RCCL's collective
         // kernels instead of K groups of 2(P-1) p2p ops), where the chunks are equal
         if (direct_gather_eligible(bytes, 1, P)) {

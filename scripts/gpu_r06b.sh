@@ -1,7 +1,7 @@
 #!/bin/bash
 # r06 s2: the whole GPU suite after the RCCL config plumbing, the unpack-lane instrumentation, the
 # device-unpack failure drain and the deferred-deletion reaper; smoke; the N=1 bench (host legs
-# carry the lane split); the lane copy probe; an N=2 rehearsal (the CTA sweep leg runs).
+# carry the lane split); the lane copy probe; the N=8 rehearsal (the CTA sweep and the C4 tuner table).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r06/s2; mkdir -p $O
 crashed() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
@@ -17,6 +17,4 @@ if crashed $rc; then exit $rc; fi
 timeout -k 10 200 tools/bin/lane_copy_probe > $O/lane_copy_probe.jsonl 2> $O/lane_copy_probe.err
 rc=$?; echo "lane probe rc=$rc"; cat $O/lane_copy_probe.jsonl
 if crashed $rc; then exit $rc; fi
-timeout -k 10 600 python bench.py --gpus 2 --rehearse --steps 6 --warmup 2 > $O/rehearse2.json 2> $O/rehearse2.err
-rc=$?; echo "rehearse2 rc=$rc"; tail -c 400 $O/rehearse2.json; echo
-exit $rc
+NS=8 LIMIT=560 TAG=r06/s2 bash scripts/gpu_rehearse.sh

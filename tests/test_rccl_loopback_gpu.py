@@ -172,6 +172,29 @@ def test_rccl_loopback_tuner_agreement(loop, gpu):
     assert all(tms[i] > 0 for i in range(min(count.value, 16)))
 
 
+def test_rccl_loopback_tuner_offers_sliced_c4_folds(loop, oracle, gpu):
+    """a 16 MiB fp16 bucket at P = 8 (C4's, 2 MiB chunks) is tuned over
+    direct candidates that cut each chunk into 4 and 8 slices (512 / 256 KiB), so a slice's fold
+    can overlap the next slice's reduce-scatter; every candidate, run with the tuner off, sums
+    bit-exact vs the oracle's fp16 rule (MPICH order in fp32, one rounding)."""
+    lib = loop
+    P, n = 8, (16 << 20) // 2
+    s = torch.cuda.current_stream().cuda_stream
+    chosen, count = ctypes.c_int(-1), ctypes.c_int(0)
+    cfgs, tms = (ctypes.c_longlong * 128)(), (ctypes.c_float * 32)()
+    assert lib.ddl_rccl_loopback_tune(P, n, DT_HALF, s, ctypes.byref(chosen), ctypes.byref(count), cfgs, tms,
+                                      32) == 0, lib.ddl_last_error()
+    cands = [tuple(cfgs[4 * i:4 * i + 4]) for i in range(min(count.value, 32))]
+    direct = {c[2] for c in cands if c[0] == 1}
+    assert {512 << 10, 256 << 10} <= direct, cands
+    xs = [random_input(DT_HALF, n, 900 + r) for r in range(P)]
+    want = oracle.fold_ref_order(DT_HALF, xs).tobytes()
+    for slice_bytes in (512 << 10, 256 << 10):
+        with config(lib, tune=0, algo=1, slice_bytes=slice_bytes, max_slices=16):
+            for o in run_loop(lib, gpu, xs, DT_HALF):
+                assert o.tobytes() == want, slice_bytes
+
+
 def test_rccl_loopback_split(loop, oracle, gpu):
     """ncclCommSplit at size 1 (the handler's private data communicator and every
     split_communicator go through it): color 0 gives rank 0 of 1, and the split communicator
