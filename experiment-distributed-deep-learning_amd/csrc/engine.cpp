@@ -30,6 +30,9 @@ Config &config() {
         if (const char *e = std::getenv("DDL_RINGS")) cfg->rings = std::atoll(e);
         if (const char *e = std::getenv("DDL_MAX_SLICES")) cfg->max_slices = std::atoll(e);
         if (const char *e = std::getenv("DDL_FUSION_THRESHOLD")) cfg->fusion_threshold_bytes = std::atoll(e);
+        // RCCL channel bounds for a deployment that sets them per job (0..256, as ddl_set_config)
+        if (const char *e = std::getenv("DDL_RCCL_MIN_CTAS")) cfg->rccl_min_ctas = std::max(0ll, std::min(256ll, std::atoll(e)));
+        if (const char *e = std::getenv("DDL_RCCL_MAX_CTAS")) cfg->rccl_max_ctas = std::max(0ll, std::min(256ll, std::atoll(e)));
         if (const char *e = std::getenv("DDL_LOG_LEVEL")) cfg->log_level = std::atoll(e);
         if (const char *e = std::getenv("DDL_CYCLE_TIME_US")) cfg->cycle_time_us = std::atoll(e);
         if (const char *e = std::getenv("DDL_TUNE")) cfg->tune = std::atoll(e);
