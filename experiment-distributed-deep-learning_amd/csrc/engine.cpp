@@ -819,6 +819,9 @@ void wait_deferred_deletions_at_exit() { wait_deferred_deletions(10000); }
 }  // namespace
 
 bool wait_deferred_deletions(long long limit_ms) {
+    // on a handler thread (ddl_finalize from a done() callback) the deletions may be joining this
+    // very thread: waiting would deadlock, so they are left to finish on their own
+    if (t_handler_thread) return true;
     Reaper &r = reaper();
     std::unique_lock<std::mutex> g(r.mu);
     return r.cv.wait_for(g, std::chrono::milliseconds(limit_ms), [&] { return r.pending == 0; });

@@ -296,11 +296,11 @@ def test_reduce_sumN_kernel_all_input_counts(lib, oracle, gpu):
         assert outs[0].tobytes() == want.tobytes(), P
 
 
-@pytest.mark.parametrize('P,ncand', [(2, 4), (4, 12), (8, 12)])
+@pytest.mark.parametrize('P,ncand', [(2, 4), (4, 13), (8, 13)])
 def test_local_autotune_candidates(lib, gpu, P, ncand):
     """The autotuner's procedure on P virtual ranks: the configured schedule is candidate 0,
     every candidate is timed, the chosen one is the fastest (4 MiB: equal chunks at P = 4, 8, so
-    the direct-gather candidates too)."""
+    the direct-gather candidates too; chunks <= 4 MiB, so direct with 256 KiB slices too)."""
     chosen, count = ctypes.c_int(), ctypes.c_int()
     cfgs = (ctypes.c_longlong * 64)()
     ms = (ctypes.c_float * 16)()
@@ -315,6 +315,8 @@ def test_local_autotune_candidates(lib, gpu, P, ncand):
     assert times[chosen.value] == min(times)
     algos = {cfgs[4 * i] for i in range(count.value)}
     assert algos == ({0, 1, 4} if P > 2 else {0})
+    if P > 2:
+        assert (1, 256 << 10) in {(cfgs[4 * i], cfgs[4 * i + 2]) for i in range(count.value)}
 
 
 # ---- one-shot schedule: algo = 2 --------------------------------------------------------------
