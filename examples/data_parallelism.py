@@ -53,12 +53,12 @@ def synthetic(samples, shape, seed=0):
 
 
 def get_processing_data(data, communicator):
-    samples_per_rank = len(data) // communicator.size
-    begin = communicator.rank * samples_per_rank
-    end = begin + samples_per_rank
-    if communicator.rank == communicator.size - 1 and end < len(data):
-        end = len(data)
-    return data[begin:end, ...]
+    """This rank's shard (reference examples/data_parallelism.py:47-53): equal contiguous shares of
+    len(data) // size samples in rank order, the remainder going to the last rank."""
+    share = len(data) // communicator.size
+    lo = share * communicator.rank
+    hi = len(data) if communicator.rank + 1 == communicator.size else lo + share
+    return data[lo:hi]
 
 
 def main():

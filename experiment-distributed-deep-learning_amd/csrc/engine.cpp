@@ -839,11 +839,19 @@ void CommunicatorDeleter::operator()(Communicator *c) const {
         std::lock_guard<std::mutex> g(r.mu);
         ++r.pending;
     }
-    std::thread([c, &r] {
-        delete c;
+    try {
+        std::thread([c, &r] {
+            delete c;
+            std::lock_guard<std::mutex> g(r.mu);
+            if (--r.pending == 0) r.cv.notify_all();
+        }).detach();
+    } catch (const std::exception &e) {
+        // no thread to be had: deleting here would join this very thread, so the communicator is
+        // left allocated (its handler keeps running until exit) rather than deadlock
+        DDL_LOG(0, "communicator " << c << " leaked: no thread for its deferred deletion (" << e.what() << ")");
         std::lock_guard<std::mutex> g(r.mu);
         if (--r.pending == 0) r.cv.notify_all();
-    }).detach();
+    }
 }
 
 Registry &Registry::get() {
