@@ -606,9 +606,24 @@ CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allred
           check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]
 
 
-def worker(rank, world, port, q, only=None):
+def rccl_sockets_env(rank, world):
+    """Environment that lets P processes on ONE GPU form a real multi-rank RCCL communicator:
+    RCCL refuses two ranks of a communicator on one device only when it sees them on the same host
+    (same host hash and bus id, "Duplicate GPU detected"). NCCL_HOSTID gives every rank a host of
+    its own, so RCCL connects them through its network transport — sockets on the loopback
+    interface — instead of xGMI. Everything above the wire is the production path: ddl_init's
+    ncclCommInitRankConfig at size P, ncclCommSplit across ranks, RcclTransport's send / recv
+    pairs between processes, ncclAllGather, the tuner's ncclAllReduce(MAX). Test infrastructure
+    only (the rates are a socket's, not xGMI's)."""
+    return {'NCCL_HOSTID': f'ddl-test-host-{rank}-of-{world}', 'NCCL_SOCKET_IFNAME': 'lo',
+            'NCCL_IB_DISABLE': '1'}
+
+
+def worker(rank, world, port, q, only=None, transport='gloo'):
     results = []
     try:
+        if transport == 'rccl':  # before anything initialises RCCL in this process
+            os.environ.update(rccl_sockets_env(rank, world))
         for p in (os.path.join(ROOT, 'experiment-distributed-deep-learning_amd'), HERE, os.path.join(ROOT, 'tools')):
             if p not in sys.path:
                 sys.path.insert(0, p)
@@ -629,9 +644,17 @@ def worker(rank, world, port, q, only=None):
         for env, key in (('DDL_MP_NUMA_BIND', b'host_numa_bind'), ('DDL_MP_CU_MASK', b'compute_cu_mask')):
             if os.environ.get(env):
                 check(lib.ddl_set_config(key, int(os.environ[env])), 'ddl_set_config')
-        cbs = gloo_transport.init_world(lib, dist, torch, rank, world)  # noqa: F841 (keep alive)
+        if transport == 'rccl':
+            from ddl.torch.communicator import init
+            init(rank, world, 0)  # the product's bootstrap: ddl_init over a real RCCL communicator
+            cbs = None
+        else:
+            cbs = gloo_transport.init_world(lib, dist, torch, rank, world)  # noqa: F841 (keep alive)
         comm = Communicator.world()
         assert comm.size == world and comm.rank == rank
+        kind, tranks = ctypes.c_int(), ctypes.c_int()
+        check(lib.ddl_comm_transport(comm.id, ctypes.byref(kind), ctypes.byref(tranks)), 'ddl_comm_transport')
+        assert (kind.value, tranks.value) == ((1, world) if transport == 'rccl' else (2, world)), (kind, tranks)
         # the configured schedule unless a check turns the tuner on (check_tuned_exact): tuning
         # every new size class through gloo host copies is what makes these runs slow at P = 8
         check(lib.ddl_set_config(b'tune', 0), 'ddl_set_config')
