@@ -64,6 +64,10 @@ def parse():
                     help='N>1 on ONE GPU: run every leg with the point-to-point groups over gloo host copies '
                          '(test-harness transport, tools/gloo_transport.py) instead of RCCL; exercises the '
                          'bench code, its numbers are not measurements')
+    ap.add_argument('--rehearse-rccl', action='store_true',
+                    help='N>1 on ONE GPU over REAL multi-rank RCCL communicators: every rank gets its own '
+                         'NCCL_HOSTID, so RCCL accepts N ranks on one device and connects them with its socket '
+                         'transport over loopback; the node\'s code path end to end, its numbers are a socket\'s')
     ap.add_argument('--watchdog-s', type=float, default=420.0, help='N>1: abort a hung run after this')
     ap.add_argument('--force-multi', action='store_true', help='run the N>1 code path even at world size 1')
     ap.add_argument('--cpu-seconds', type=float, default=6.0)
@@ -987,7 +991,11 @@ def multi_gpu(args):
     from ddl.torch.cpp_backend import CPPBackend, check
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
-    local = 0 if args.rehearse else int(os.environ.get('LOCAL_RANK', rank))
+    one_gpu = args.rehearse or args.rehearse_rccl  # every rank on cuda:0
+    local = 0 if one_gpu else int(os.environ.get('LOCAL_RANK', rank))
+    if args.rehearse_rccl:  # before anything initialises RCCL in this process (tests/_mp_gpu_worker.py)
+        os.environ.update({'NCCL_HOSTID': f'ddl-bench-host-{rank}-of-{world}', 'NCCL_SOCKET_IFNAME': 'lo',
+                           'NCCL_IB_DISABLE': '1'})
 
     state = {'out': None, 'leg': 'main'}  # rank 0's result so far; the leg in progress
 
@@ -1015,7 +1023,7 @@ def multi_gpu(args):
     dog.start()
     if os.environ.get('DDL_BENCH_WATCHDOG_SELFTEST') == '1':
         _watchdog_selftest(args, state, rank, world)  # never returns: the watchdog ends the process
-    if not args.rehearse and torch.cuda.device_count() < world:  # counting does not initialise the GPU
+    if not one_gpu and torch.cuda.device_count() < world:  # counting does not initialise the GPU
         sys.stderr.write(f'[bench rank {rank}] {world} ranks need {world} GPUs, this box has '
                          f'{torch.cuda.device_count()} (use --rehearse to run the N>1 legs on one GPU)\n')
         sys.exit(2)
@@ -1028,6 +1036,9 @@ def multi_gpu(args):
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import gloo_transport
         state['callbacks'] = gloo_transport.init_world(lib, dist, torch, rank, world, device=local)
+    elif args.rehearse_rccl:  # the product's bootstrap on cuda:0 (init reads LOCAL_RANK otherwise)
+        from ddl.torch.communicator import init as ddl_world_init
+        ddl_world_init(rank, world, 0)
     comm = Communicator.world()
     kind, tranks = ctypes.c_int(), ctypes.c_int()
     check(lib.ddl_comm_transport(comm.id, ctypes.byref(kind), ctypes.byref(tranks)), 'ddl_comm_transport')
@@ -1153,6 +1164,9 @@ def multi_gpu(args):
     }
     if args.rehearse:
         out['rehearsal'] = 'point-to-point over gloo host copies on one GPU: exercises the N>1 legs, NOT a measurement'
+    elif args.rehearse_rccl:
+        out['rehearsal'] = ('real multi-rank RCCL communicators on one GPU (NCCL_HOSTID per rank: RCCL\'s socket '
+                            'transport over loopback): the node\'s code path end to end, NOT an xGMI measurement')
     state['out'] = out  # from here on a hung optional leg still reports the headline result
     # parity on this node first, so no optional leg can hide it: every rank's result equals
     # MPI_Allreduce's (MPICH 3.3.2 order) bit for bit, on both sides of MPICH's 2048-byte switch
@@ -1340,7 +1354,7 @@ def multi_gpu(args):
     state['leg'] = 'host_resident'
     try:
         if not args.no_host:
-            out['host_resident'] = host_resident_rate(lib, comm, S, reps=4, warm_calls=1 if args.rehearse else 20)
+            out['host_resident'] = host_resident_rate(lib, comm, S, reps=4, warm_calls=1 if one_gpu else 20)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['host_resident'] = repr(e)[:400]
     state['leg'] = 'fusion_c5'
@@ -1366,7 +1380,7 @@ def multi_gpu(args):
     try:
         if not args.no_fusion and not args.no_host:
             out['keyed_host_c5_pinned'] = keyed_host_c5(lib, comm, steps=2, pinned=True,
-                                                        warm_steps=1 if args.rehearse else 3)
+                                                        warm_steps=1 if one_gpu else 3)
     except Exception as e:  # a failed optional leg must not cost the headline line
         out.setdefault('leg_errors', {})['keyed_host_c5_pinned'] = repr(e)[:400]
     # the metric's curve: allreduce GiB/s vs bucket size at this N, the engine (autotuned per

@@ -219,6 +219,33 @@ def check_split_communicators_keyed(ctx):
     same.detach()
 
 
+def check_rccl_channel_bounds(ctx):
+    """Config rccl_min_ctas / rccl_max_ctas: a split created under channel
+    bounds (over RCCL: ncclCommSplit with ncclConfig_t.minCTAs / maxCTAs; the test transport ignores
+    them) carries the default schedule and a keyed batch bit-exact vs MPICH's order, for two
+    settings; the world keeps working after the bounds are restored."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allreduce, allreduce_async_batch
+    for lo, hi in ((2, 2), (8, 16)):
+        with h.config(lib, rccl_min_ctas=lo, rccl_max_ctas=hi):
+            sub = comm.split_communicator(0, r)
+        try:
+            for n in (1000, 300_001):
+                xs = [h.random_input(h.DT_FLOAT, n, 555 + 7 * lo + q + n) for q in range(P)]
+                got = allreduce(torch.from_numpy(xs[r]).cuda(), sub).cpu().numpy()
+                assert got.tobytes() == ora.fold_ref_order(h.DT_FLOAT, xs).tobytes(), (lo, hi, n)
+            xs = [[h.random_input(h.DT_DOUBLE, 5000 + i, 90 + 10 * i + q) for q in range(P)] for i in range(3)]
+            hs = allreduce_async_batch([torch.from_numpy(x[r]).cuda() for x in xs], ['cta_a', 'cta_b', 'cta_c'], sub)
+            gb = sum(x[0].nbytes for x in xs)
+            for hd, x in zip(hs, xs):
+                assert hd.wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_DOUBLE, x, gb).tobytes()
+        finally:
+            sub.detach()
+    x = torch.full((16,), float(r), device='cuda')
+    assert torch.equal(allreduce(x, comm), torch.full((16,), float(P * (P - 1) // 2), device='cuda'))
+
+
 def check_keyed_host_requests(ctx):
     """Keyed requests on host (CPU) tensors — the reference's only kind (its op is DEVICE_CPU,
     AllreduceOp.cc:68): fused per dtype, staged through pinned 64 KiB chunks (many chunks, the
@@ -601,7 +628,8 @@ FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resou
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,
           check_keyed_fusion,
-          check_keyed_reference_order, check_split_communicators_keyed, check_keyed_host_requests,
+          check_keyed_reference_order, check_split_communicators_keyed, check_rccl_channel_bounds,
+          check_keyed_host_requests,
           check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model,
           check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]
 
