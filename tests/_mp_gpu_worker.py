@@ -702,8 +702,12 @@ def worker(rank, world, port, q, only=None, transport='gloo'):
                 fn(ctx)
                 results.append((fn.__name__, True, ''))
                 if rank == 0:
-                    sys.stderr.write(f'[P={world}] {fn.__name__}: {time.perf_counter() - t0:.1f} s\n')
+                    line = f'[P={world} {transport}] {fn.__name__}: {time.perf_counter() - t0:.1f} s\n'
+                    sys.stderr.write(line)
                     sys.stderr.flush()
+                    if os.environ.get('DDL_MP_PROGRESS_FILE'):  # long GPU runs: progress outside pytest's capture
+                        with open(os.environ['DDL_MP_PROGRESS_FILE'], 'a') as f:
+                            f.write(line)
             except Exception:
                 results.append((fn.__name__, False, traceback.format_exc()[-1500:]))
                 break  # a failed collective leaves the ranks out of step: stop here
