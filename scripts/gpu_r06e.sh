@@ -3,7 +3,7 @@
 # stacks every 60 s if a rank stalls; a heartbeat keeps the run visibly alive.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r06/s5; mkdir -p $O
-export NCCL_DEBUG=WARN DDL_MP_PROGRESS_FILE=$PWD/$O/progress.txt DDL_MP_STACKS_S=90
+export ddl_lib=$PWD/experiment-distributed-deep-learning_amd/lib/libddl_amd_testing.so NCCL_DEBUG=WARN DDL_MP_PROGRESS_FILE=$PWD/$O/progress.txt DDL_MP_STACKS_S=90
 for P in 4 5; do
   timeout -k 10 420 python -u -c "
 import sys, time; sys.path.insert(0, 'tests')
