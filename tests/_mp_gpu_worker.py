@@ -643,8 +643,10 @@ def rccl_sockets_env(rank, world):
     ncclCommInitRankConfig at size P, ncclCommSplit across ranks, RcclTransport's send / recv
     pairs between processes, ncclAllGather, the tuner's ncclAllReduce(MAX). Test infrastructure
     only (the rates are a socket's, not xGMI's)."""
-    return {'NCCL_HOSTID': f'ddl-test-host-{rank}-of-{world}', 'NCCL_SOCKET_IFNAME': 'lo',
-            'NCCL_IB_DISABLE': '1'}
+    env = {'NCCL_HOSTID': f'ddl-test-host-{rank}-of-{world}', 'NCCL_SOCKET_IFNAME': 'lo', 'NCCL_IB_DISABLE': '1'}
+    if os.environ.get('DDL_MP_HW_QUEUES'):  # hardware queues per rank process (HIP reads it at init)
+        env['GPU_MAX_HW_QUEUES'] = os.environ['DDL_MP_HW_QUEUES']
+    return env
 
 
 def worker(rank, world, port, q, only=None, transport='gloo'):
