@@ -103,6 +103,7 @@ int ddl_finalize(void) {
         Registry::get().clear();
         DDL_REQUIRE(wait_deferred_deletions(60000), DDL_STATUS_ERROR_UNKNOWN,
                     "a communicator released by its own handler thread is still being destroyed after 60 s");
+        free_retired();
         standalone_control() = std::make_shared<ControlChannel>();
         run_finalize_hooks();
     });

@@ -223,4 +223,20 @@ private:
     size_t next_ = 0;
 };
 
+// Memory a data path outgrew (r06). hipFree / hipHostFree synchronise the whole device, and on a
+// thread that posts RCCL work that can deadlock the ranks once two communicators are in flight:
+// rank A's handler of communicator X blocks in hipFree until its in-flight kernel of communicator
+// Y finishes, which waits for rank B's Y kernel, which B's handler of Y has not posted because it
+// is blocked the same way behind its X kernel, which waits for A's X work (found with multi-rank
+// RCCL communicators on one GPU, tests/test_multiproc_rccl_gpu.py). So buffers that grow during
+// operation (staging, fusion buffers, pinned slots, tuning scratch) hand their old allocation here
+// instead of freeing it; ddl_finalize frees the lot once every communicator is gone. Growth is
+// geometric, so what waits here is less than twice the final sizes.
+void retire_device(void *p);
+void retire_host(void *p);
+void free_retired();
+// Device scratch of at least `bytes` for the calling thread on the current device (the control
+// collectives: config agreement, the tuner's max, split records) — no allocation per call.
+void *thread_scratch(size_t bytes);
+
 }  // namespace ddl

@@ -104,6 +104,8 @@ Communicator::~Communicator() {
     exec_.reset();
     for (void *s : slots_)
         if (s) (void)hipFree(s);
+    if (tune_a_) (void)hipFree(tune_a_);
+    if (tune_b_) (void)hipFree(tune_b_);
     for (hipStream_t s : {h2d_, ring_, d2h_, ctl_stream_})
         if (s) (void)hipStreamDestroy(s);
     if (nccl_) (void)rccl().CommDestroy(nccl_);
@@ -411,16 +413,19 @@ TuneResult run_tuning(int P, size_t bytes, hipStream_t stream, const RingConfig 
 // each candidate (one ncclAllReduce of nc floats), so all ranks pick the same schedule.
 TuneResult Communicator::tune_(size_t n, int dtype, hipStream_t stream, const RingConfig &base) {
     const size_t bytes = n * dtype_size(dtype);
-    void *a = nullptr, *b = nullptr;
-    auto cleanup = [&] {
-        (void)hipStreamSynchronize(stream);
-        if (a) (void)hipFree(a);
-        if (b) (void)hipFree(b);
-    };
+    auto cleanup = [&] { (void)hipStreamSynchronize(stream); };
+    if (tune_cap_ < bytes) {  // grow-only scratch, the outgrown pair retired (no hipFree while others run)
+        retire_device(tune_a_);
+        retire_device(tune_b_);
+        tune_a_ = tune_b_ = nullptr;
+        tune_cap_ = 0;
+        DDL_HIP(hipMalloc(&tune_a_, bytes));
+        DDL_HIP(hipMalloc(&tune_b_, bytes));
+        tune_cap_ = bytes;
+    }
+    void *a = tune_a_, *b = tune_b_;
     TuneResult res;
     try {
-        DDL_HIP(hipMalloc(&a, bytes));
-        DDL_HIP(hipMalloc(&b, bytes));
         DDL_HIP(hipMemsetAsync(a, 0, bytes, stream));
         res = run_tuning(
             size_, bytes, stream, base, [&](const RingConfig &c) { exec_->allreduce(a, b, n, dtype, stream, c); },
@@ -537,11 +542,10 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
         DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
     }
     if (slot_bytes_ < chunk) {
-        for (void *&sl : slots_)
-            if (sl) {
-                DDL_HIP(hipFree(sl));
-                sl = nullptr;
-            }
+        for (void *&sl : slots_) {  // outgrown: kept until ddl_finalize (retire_device)
+            retire_device(sl);
+            sl = nullptr;
+        }
         for (void *&sl : slots_) DDL_HIP(hipMalloc(&sl, chunk));
         slot_bytes_ = chunk;
     }
@@ -640,12 +644,11 @@ std::shared_ptr<Communicator> Communicator::split(int color, int key, bool keyed
         hipStream_t s = nullptr;
         auto release = [&] {
             if (s) (void)hipStreamSynchronize(s);
-            if (d) (void)hipFree(d);
             if (s) (void)hipStreamDestroy(s);
         };
         try {
             DDL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            DDL_HIP(hipMalloc(&d, sizeof(SplitRecord) * size_));
+            d = thread_scratch(sizeof(SplitRecord) * size_);
             char *base = static_cast<char *>(d);
             DDL_HIP(hipMemcpyAsync(base + sizeof(SplitRecord) * rank_, &mine, sizeof mine, hipMemcpyHostToDevice, s));
             std::vector<size_t> cnt(size_, sizeof(SplitRecord) / 8), dsp(size_);
@@ -755,8 +758,7 @@ ncclComm_t rccl_split(ncclComm_t parent, int color, int key, int *rank, int *siz
 
 void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stream) {
     DDL_REQUIRE(count > 0 && count <= 1024, DDL_STATUS_INVALID_ARGUMENT, "max of " << count << " floats");
-    float *d = nullptr;
-    DDL_HIP(hipMalloc(&d, sizeof(float) * count));
+    float *d = static_cast<float *>(thread_scratch(sizeof(float) * count));
     try {
         DDL_HIP(hipMemcpyAsync(d, values, sizeof(float) * count, hipMemcpyHostToDevice, stream));
         rccl_check(rccl().AllReduce(d, d, count, ncclFloat32, ncclMax, comm, stream), "ncclAllReduce(max)");
@@ -764,15 +766,12 @@ void rccl_max_floats(ncclComm_t comm, float *values, int count, hipStream_t stre
         DDL_HIP(hipStreamSynchronize(stream));
     } catch (...) {
         (void)hipStreamSynchronize(stream);
-        (void)hipFree(d);
         throw;
     }
-    DDL_HIP(hipFree(d));
 }
 
 void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, hipStream_t stream) {
-    uint64_t *d = nullptr;
-    DDL_HIP(hipMalloc(&d, sizeof(uint64_t) * size));
+    uint64_t *d = static_cast<uint64_t *>(thread_scratch(sizeof(uint64_t) * size));
     try {
         DDL_HIP(hipMemcpyAsync(d + rank, values + rank, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
         rccl_check(rccl().AllGather(d + rank, d, sizeof(uint64_t), ncclInt8, comm, stream), "ncclAllGather(config)");
@@ -780,10 +779,8 @@ void rccl_allgather_u64(ncclComm_t comm, uint64_t *values, int size, int rank, h
         DDL_HIP(hipStreamSynchronize(stream));
     } catch (...) {
         (void)hipStreamSynchronize(stream);
-        (void)hipFree(d);
         throw;
     }
-    DDL_HIP(hipFree(d));
 }
 
 RequestHandler *Communicator::handler_if_created() {
@@ -825,6 +822,64 @@ bool wait_deferred_deletions(long long limit_ms) {
     Reaper &r = reaper();
     std::unique_lock<std::mutex> g(r.mu);
     return r.cv.wait_for(g, std::chrono::milliseconds(limit_ms), [&] { return r.pending == 0; });
+}
+
+namespace {
+struct Retired {
+    std::mutex mu;
+    std::vector<void *> dev, host;
+};
+Retired &retired() {
+    static Retired *r = new Retired();  // never destroyed: threads may retire at exit
+    return *r;
+}
+struct ThreadScratch {
+    std::vector<std::pair<void *, size_t>> per_device;  // index = device ordinal
+    ~ThreadScratch() {
+        for (auto &p : per_device)
+            if (p.first) retire_device(p.first);
+    }
+};
+thread_local ThreadScratch t_scratch;
+}  // namespace
+
+void retire_device(void *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(retired().mu);
+    retired().dev.push_back(p);
+}
+
+void retire_host(void *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(retired().mu);
+    retired().host.push_back(p);
+}
+
+void free_retired() {
+    std::vector<void *> dev, host;
+    {
+        std::lock_guard<std::mutex> g(retired().mu);
+        dev.swap(retired().dev);
+        host.swap(retired().host);
+    }
+    for (void *p : dev) (void)hipFree(p);
+    for (void *p : host) (void)hipHostFree(p);
+}
+
+void *thread_scratch(size_t bytes) {
+    int dev = 0;
+    DDL_HIP(hipGetDevice(&dev));
+    auto &v = t_scratch.per_device;
+    if ((size_t)dev >= v.size()) v.resize((size_t)dev + 1, {nullptr, 0});
+    auto &slot = v[(size_t)dev];
+    if (slot.second < bytes) {
+        retire_device(slot.first);  // a stream may still read it: kept until ddl_finalize
+        slot = {nullptr, 0};
+        const size_t sz = std::max<size_t>(bytes, 16384);
+        DDL_HIP(hipMalloc(&slot.first, sz));
+        slot.second = sz;
+    }
+    return slot.first;
 }
 
 void CommunicatorDeleter::operator()(Communicator *c) const {

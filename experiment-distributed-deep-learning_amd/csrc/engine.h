@@ -306,6 +306,9 @@ private:
     static constexpr int kHostSlots = 4;
     void *slots_[kHostSlots] = {};
     size_t slot_bytes_ = 0;
+    // the tuner's scratch buckets (grow-only, retired on growth: no hipFree while others run)
+    void *tune_a_ = nullptr, *tune_b_ = nullptr;
+    size_t tune_cap_ = 0;
 };
 
 // Set on a request handler's engine and completion threads. The last reference to a communicator
@@ -320,6 +323,7 @@ struct CommunicatorDeleter {
 // Waits up to limit_ms for the communicators being deleted off their handlers' threads; false on
 // timeout. ddl_finalize calls it (and an exit hook, 10 s).
 bool wait_deferred_deletions(long long limit_ms);
+
 
 // every Communicator is owned through this (make_shared would bypass the deleter)
 template <class... A>

@@ -1,6 +1,8 @@
 // executor.cpp — see executor.h.
 #include "executor.h"
 
+#include "engine.h"
+
 #include "deptrace.h"
 
 #include <algorithm>
@@ -115,10 +117,10 @@ void *RankResources::ensure_staging(size_t bytes, bool capturing) {
             staging_ = nullptr;
             staging_captured_ = false;
         } else if (staging_) {
-            // a previous call may still read it on the device
-            DDL_HIP(hipStreamSynchronize(comm));
-            DDL_HIP(hipStreamSynchronize(compute));
-            DDL_HIP(hipFree(staging_));
+            // a previous call may still read it on the device; and hipFree would synchronise the
+            // whole device, which can deadlock against other communicators' RCCL kernels: kept
+            // until ddl_finalize (retire_device)
+            retire_device(staging_);
             staging_ = nullptr;
         }
         size_t sz = bytes + bytes / 4;  // grow with headroom (the reference grows x1.5, MPIRTC.cc:13)

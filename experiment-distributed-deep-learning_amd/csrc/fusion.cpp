@@ -2,6 +2,7 @@
 #include "fusion.h"
 
 #include "deptrace.h"
+#include "engine.h"
 
 namespace ddl {
 
@@ -17,9 +18,8 @@ void *FusionPipe::ensure(int i, size_t need, hipStream_t stream) {
     void *&buf = buf_[i];
     size_t &cap = cap_[i];
     if (need > cap) {
-        if (buf) {
-            DDL_HIP(hipStreamSynchronize(stream));
-            DDL_HIP(hipFree(buf));
+        if (buf) {  // may still be read on the device; no hipFree on a data path (engine.h retire_device)
+            retire_device(buf);
             buf = nullptr;
             cap = 0;
         }

@@ -833,9 +833,8 @@ void RequestHandler::member_round_(Token &t) {
 
 void *RequestHandler::ensure_(void *&buf, size_t &cap, size_t need) {
     if (need > cap) {
-        if (buf) {
-            DDL_HIP(hipStreamSynchronize(stream_));
-            DDL_HIP(hipFree(buf));
+        if (buf) {  // may still be read on the device; no hipFree on a data path (engine.h retire_device)
+            retire_device(buf);
             buf = nullptr;
             cap = 0;
         }
@@ -957,10 +956,10 @@ size_t RequestHandler::host_slots_(size_t total) {
     if (host_slot_bytes_ < chunk) {
         for (hipStream_t st : {h2d_, d2h_, stream_})
             if (st) DDL_HIP(hipStreamSynchronize(st));
-        for (int k = 0; k < kHostSlots; ++k) {
-            if (pin_[k]) DDL_HIP(hipHostFree(pin_[k]));
-            if (pout_[k]) DDL_HIP(hipHostFree(pout_[k]));
-            if (dslot_[k]) DDL_HIP(hipFree(dslot_[k]));
+        for (int k = 0; k < kHostSlots; ++k) {  // outgrown slots kept until ddl_finalize (engine.h retire_*)
+            retire_host(pin_[k]);
+            retire_host(pout_[k]);
+            retire_device(dslot_[k]);
             pin_[k] = pout_[k] = dslot_[k] = nullptr;
             slot_used_[k] = false;
         }
@@ -1542,7 +1541,7 @@ void RequestHandler::allgather_reqs_(std::vector<Request> &reqs, std::vector<Don
                 void *fb = fp_.ensure(0, std::max<size_t>(blk[me], 256), stream_);
                 ensure_(gather_, gather_bytes_, all);
                 if (pin_gather_bytes_ < all) {
-                    if (pin_gather_) DDL_HIP(hipHostFree(pin_gather_));
+                    retire_host(pin_gather_);  // no hipHostFree on a data path (engine.h retire_host)
                     pin_gather_ = nullptr;
                     pin_gather_bytes_ = 0;
                     DDL_HIP(hipHostMalloc(&pin_gather_, all + all / 2, hipHostMallocDefault));

@@ -194,9 +194,9 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     const uint64_t nblk = (tiles + kIdxBlock - 1) / kIdxBlock;
     const size_t table = (size_t)count * sizeof(SegDesc);
     const size_t need = table + nblk * sizeof(uint32_t);  // descriptors, then the block bases
-    if (need > sl.cap) {
-        if (sl.host) DDL_HIP(hipHostFree(sl.host));
-        if (sl.dev) DDL_HIP(hipFree(sl.dev));
+    if (need > sl.cap) {  // outgrown tables kept until ddl_finalize: no hipFree on a data path (engine.h)
+        retire_host(sl.host);
+        retire_device(sl.dev);
         sl.host = sl.dev = nullptr;
         sl.cap = need + need / 2;
         DDL_HIP(hipHostMalloc(&sl.host, sl.cap, hipHostMallocDefault));
@@ -234,7 +234,7 @@ void SegmentCopier::run(int dir, void *flat, void *const *segs, const size_t *by
     if (tiles > 0) {
         const size_t ib = narrow ? (tiles + 3) & ~uint64_t(3) : tiles * sizeof(int);
         if (ib > sl.idx_cap) {
-            if (sl.idx) DDL_HIP(hipFree(sl.idx));
+            retire_device(sl.idx);
             sl.idx = nullptr;
             sl.idx_cap = ib + ib / 2;
             DDL_HIP(hipMalloc(&sl.idx, sl.idx_cap));
