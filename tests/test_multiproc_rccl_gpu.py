@@ -59,3 +59,13 @@ def test_engine_over_multirank_rccl(gpu, world):
     res = _run(world)
     names = [n for n, _, _ in res[0]]
     assert names == [f.__name__ for f in _mp_gpu_worker.CHECKS], names
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_control_link_lost_mid_round_over_rccl(gpu, world):
+    """ADVICE r3's fault case over real RCCL communicators: a control link lost after a member froze
+    its user collectives for a keyed round stops every rank's handler; keyed requests complete with
+    an error and direct collectives return one instead of hanging (check_control_link_lost)."""
+    res = _run(world, ['check_control_link_lost'], timeout=120)
+    for rank, results in res.items():
+        assert [n for n, _, _ in results][:1] == ['check_control_link_lost'], results
