@@ -680,6 +680,14 @@ def keyed_bucket_stream(lib, comm, dev, steps, buckets=32, bucket_bytes=8 << 20)
         return sr.value + cr.value
 
     try:
+        # both modes warmed up before either is timed: the rounds' sizes differ between the modes,
+        # and the first bucket of each new size class tunes the keyed data plane's schedule (a
+        # collective timing pass, seconds over slow transports) — inside whichever mode met it
+        # first (r06: over sockets the first-timed mode read 3-14x slower for that reason alone)
+        for pipelined in (1, 0, 1, 0):
+            check(lib.ddl_set_config(b'pipeline_rounds', pipelined), 'ddl_set_config')
+            step()
+        torch.cuda.synchronize()
         for pipelined in (1, 0):
             check(lib.ddl_set_config(b'pipeline_rounds', pipelined), 'ddl_set_config')
             step()

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-rehearse}; mkdir -p $O
 for N in ${NS:-2 4 8}; do
   start=$(date +%s)
-  timeout -k 10 ${LIMIT:-500} python3 bench.py --gpus $N ${MODE:---rehearse} --steps 3 --warmup 1 --bucket-mib ${MIB:-8} --no-size-sweep --no-config-sweep > $O/rehearse${N}_spawn.json 2> $O/rehearse${N}_spawn.err &
+  timeout -k 10 ${LIMIT:-500} python3 bench.py --gpus $N ${MODE:---rehearse} --steps 3 --warmup 1 --bucket-mib ${MIB:-8} --no-size-sweep --no-config-sweep ${EXTRA:-} > $O/rehearse${N}_spawn.json 2> $O/rehearse${N}_spawn.err &
   pid=$!
   while kill -0 $pid 2>/dev/null; do sleep 30; echo "N=$N alive $(( $(date +%s) - start ))s: $(grep -c . $O/rehearse${N}_spawn.err) stderr lines"; done
   wait $pid; rc=$?; echo "rehearse$N rc=$rc wall=$(( $(date +%s) - start ))s"
