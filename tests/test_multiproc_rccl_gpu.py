@@ -69,3 +69,43 @@ def test_control_link_lost_mid_round_over_rccl(gpu, world):
     res = _run(world, ['check_control_link_lost'], timeout=120)
     for rank, results in res.items():
         assert [n for n, _, _ in results][:1] == ['check_control_link_lost'], results
+
+
+def test_data_parallelism_example_over_two_rccl_ranks():
+    """The reference's DP script on this surface (examples/data_parallelism.py) as two training
+    processes over one real two-rank RCCL communicator, each loading the deployment library alone
+    (no ddl_lib override): the data sharded, the lr scaled by the size and warmed up to it, the
+    initial weights broadcast, every step's gradients averaged through keyed fused allreduces, the
+    metrics averaged — and the loss falls."""
+    import re
+    import subprocess
+    import sys
+
+    import _mp_gpu_worker
+    from conftest import ROOT
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE='2', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port), **_mp_gpu_worker.rccl_sockets_env(r, 2))
+        env.pop('ddl_lib', None)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, 'examples', 'data_parallelism.py'),
+                                       '--epochs', '3', '--samples', '4096', '--warmup_epochs', '2', '--lr', '0.002'],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=300))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for p, (out, err) in zip(procs, outs):
+        assert p.returncode == 0, err[-3000:]
+    out0 = outs[0][0]
+    losses = [float(m) for m in re.findall(r'loss ([0-9.e+-]+)', out0)]
+    lrs = [float(m) for m in re.findall(r'lr ([0-9.e+-]+)', out0)]
+    assert len(losses) == 3 and losses[-1] < losses[0], out0
+    assert lrs[1] == pytest.approx(2 * 0.002, rel=1e-6)  # warmed up to size x lr after 2 epochs
+    assert 'finished gradual learning rate warmup' in out0
