@@ -7,7 +7,7 @@ TAG=${TAG:-full}
 O=gpurun_out/$TAG; mkdir -p $O
 crashed() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 700 python -u -m pytest tests -m gpu -q --maxfail=25 --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  timeout -k 10 1050 python -u -m pytest tests -m gpu -q --maxfail=25 --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1
   rc=$?; echo "pytest_gpu rc=$rc"; tail -3 $O/pytest_gpu.log
   if crashed $rc; then exit $rc; fi
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
