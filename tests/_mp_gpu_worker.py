@@ -623,7 +623,31 @@ def check_resources(ctx):
     sys.stderr.flush()
 
 
-FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resources': check_resources}
+def check_fullsize_mpich_hash(ctx):
+    """Full-size parity over the real transport: every rank regenerates its
+    64 Mi fp32 input of the golden case at this P (tests/golden/golden_fullsize.json: C3 at P = 8,
+    and P = 5 / 7), runs the default schedule (tuner off) and its output must hash to MPICH 3.3.2's."""
+    import _helpers as h
+    torch, lib, comm, P, r = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank']
+    case = [c for c in h.fullsize_cases() if c[1] == P]
+    assert case, f'no full-size golden case at P = {P}'
+    name, _, n, digest, samples = case[0]
+    x = np.random.default_rng(1234 + 7919 * r).standard_normal(n).astype(np.float32)
+    a = torch.from_numpy(x).cuda()
+    del x
+    b = torch.full_like(a, float('nan'))
+    with h.config(lib, tune=0, reference_order=1):
+        st = lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), n, h.DT_FLOAT, 0,
+                               torch.cuda.current_stream().cuda_stream)
+        assert st == 0, lib.ddl_last_error()
+        torch.cuda.synchronize()
+    y = b.cpu().numpy()
+    assert all(float(y[i]) == v for i, v in samples.items()), name
+    assert h.sha256(y) == digest, name
+
+
+FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resources': check_resources,
+                'check_fullsize_mpich_hash': check_fullsize_mpich_hash}
 
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,

@@ -109,3 +109,12 @@ def test_data_parallelism_example_over_two_rccl_ranks():
     assert len(losses) == 3 and losses[-1] < losses[0], out0
     assert lrs[1] == pytest.approx(2 * 0.002, rel=1e-6)  # warmed up to size x lr after 2 epochs
     assert 'finished gradual learning rate warmup' in out0
+
+
+@pytest.mark.parametrize('world', [5, 8])
+def test_full_size_hash_equals_mpich_over_multirank_rccl(gpu, world):
+    """C3 (P = 8, 256 MiB fp32 per rank) and the P = 5 pre-fold at full size through real multi-rank
+    RCCL communicators: every rank's output hashes to MPICH 3.3.2's (check_fullsize_mpich_hash)."""
+    res = _run(world, ['check_fullsize_mpich_hash'], timeout=300)
+    for rank, results in res.items():
+        assert [n for n, _, _ in results][:1] == ['check_fullsize_mpich_hash'], results
