@@ -23,7 +23,15 @@ def _free_port():
     return p
 
 
-def _run(world, only=None, timeout=300.0):
+# P processes of 4 hardware queues each, beside the test process's own, can oversubscribe the GPU's
+# hardware queue slots; the scheduler then time-slices the queues and RCCL's spinning kernels crawl
+# (r06 s13: the P = 5 worker silent for minutes inside the whole suite, 50 s alone). So the suite
+# runs the whole worker at P <= 4 and single-communicator checks at P = 5, 8 with 2 queues per rank;
+# DDL_TEST_RCCL_BIG=1 adds the whole worker at P = 5, 8 (run in sessions: profiles/r06/s8, s9).
+BIG = os.environ.get('DDL_TEST_RCCL_BIG') == '1'
+
+
+def _run(world, only=None, timeout=300.0, hw_queues=None):
     import torch.multiprocessing as mp
 
     import _mp_gpu_worker
@@ -31,8 +39,18 @@ def _run(world, only=None, timeout=300.0):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_mp_gpu_worker.worker, args=(r, world, port, q, only, 'rccl')) for r in range(world)]
-    for p in procs:
-        p.start()
+    old = os.environ.get('DDL_MP_HW_QUEUES')
+    if hw_queues:  # the children read it before HIP starts (rccl_sockets_env)
+        os.environ['DDL_MP_HW_QUEUES'] = str(hw_queues)
+    try:
+        for p in procs:
+            p.start()
+    finally:
+        if hw_queues:
+            if old is None:
+                os.environ.pop('DDL_MP_HW_QUEUES', None)
+            else:
+                os.environ['DDL_MP_HW_QUEUES'] = old
     res = {}
     try:
         for _ in range(world):
@@ -52,7 +70,7 @@ def _run(world, only=None, timeout=300.0):
     return res
 
 
-@pytest.mark.parametrize('world', [2, 3, 4, 5, 8])
+@pytest.mark.parametrize('world', [2, 3, 4] + ([5, 8] if BIG else []))
 def test_engine_over_multirank_rccl(gpu, world):
     """Every check of the multi-process worker at P ranks over real RCCL communicators."""
     import _mp_gpu_worker
@@ -115,6 +133,6 @@ def test_data_parallelism_example_over_two_rccl_ranks():
 def test_full_size_hash_equals_mpich_over_multirank_rccl(gpu, world):
     """C3 (P = 8, 256 MiB fp32 per rank) and the P = 5 pre-fold at full size through real multi-rank
     RCCL communicators: every rank's output hashes to MPICH 3.3.2's (check_fullsize_mpich_hash)."""
-    res = _run(world, ['check_fullsize_mpich_hash'], timeout=300)
+    res = _run(world, ['check_fullsize_mpich_hash'], timeout=300, hw_queues=2)  # one communicator in use
     for rank, results in res.items():
         assert [n for n, _, _ in results][:1] == ['check_fullsize_mpich_hash'], results
