@@ -1040,7 +1040,7 @@ def multi_gpu(args):
     os.environ.setdefault('MASTER_PORT', '29533')
     dist.init_process_group('gloo', rank=rank, world_size=world)
     lib = CPPBackend.c_api()
-    if args.rehearse:  # every rank on cuda:0, groups over gloo (RCCL refuses two ranks on one GPU)
+    if args.rehearse:  # every rank on cuda:0, groups over gloo (--rehearse-rccl: real RCCL over sockets)
         sys.path.insert(0, os.path.join(ROOT, 'tools'))
         import gloo_transport
         state['callbacks'] = gloo_transport.init_world(lib, dist, torch, rank, world, device=local)

@@ -2,7 +2,8 @@
 as at N > 1 — world communicator, TCP token ring, keyed handler, fusion pipeline, ring / direct /
 one-shot schedules, the autotuner, streams and kernels — with only the point-to-point groups
 carried differently: through gloo on host copies (ddl_init_test_transport), because RCCL
-refuses two ranks on one device. Every check compares with the oracle or an exact sum; every
+refuses two ranks of one host on one device — or, with transport='rccl', over real multi-rank RCCL
+(rccl_sockets_env). Every check compares with the oracle or an exact sum; every
 rank runs the same checks in the same order (they are collectives) and reports
 (name, ok, detail). Test infrastructure only."""
 import contextlib

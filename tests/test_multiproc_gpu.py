@@ -5,7 +5,8 @@ fusion pipeline, cached ids), ring / direct / one-shot schedules, the collective
 broadcast / allgather, the host-resident pipeline and the scripts-level DP wrapper and
 callbacks — checked against the oracle and exact sums (tests/_mp_gpu_worker.py). Only the
 point-to-point groups differ from an RCCL run: they go through gloo on host copies
-(ddl_init_test_transport), because RCCL refuses two ranks on one device."""
+(ddl_init_test_transport), because RCCL refuses two ranks of one host on one device. The same
+worker over real multi-rank RCCL (a host id per rank, RCCL's socket transport): test_multiproc_rccl_gpu.py."""
 import os
 import socket
 

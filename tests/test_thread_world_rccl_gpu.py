@@ -3,7 +3,7 @@ weak #2): the thread world of test_thread_world_gpu.py — P threads, each drivi
 RingExecutor::run_ (what ddl_allreduce runs at N > 1) — with ddl_testing_thread_transport(1), so
 every matched send / receive pair moves through RcclTransport::group (the production transport
 code) as a self send + self receive on a one-rank RCCL communicator, posted on the receiver's
-stream after its wait on the sender's event. RCCL refuses two ranks on one GPU, so this is as close
+stream after its wait on the sender's event. RCCL refuses two ranks of one host on one GPU, so within one process this is as close
 to `RingExecutor` + `RcclTransport` at P > 1 as a one-GPU box allows: the same executor, the same
 transport call, RCCL kernels carrying the data; only the peer (self) and who posts the pair differ.
 
