@@ -201,6 +201,17 @@ def test_product_does_not_reference_oracle():
         assert 'oracle' not in out
 
 
+def test_rccl_channel_bounds_from_the_environment():
+    """DDL_RCCL_MIN_CTAS / DDL_RCCL_MAX_CTAS seed rccl_min_ctas / rccl_max_ctas (clamped to 0..256)
+    for a deployment that sets them per job; read in a fresh process (the config is built once)."""
+    import sys
+    code = ('import ctypes; l = ctypes.CDLL(%r); l.ddl_get_config.restype = ctypes.c_longlong; '
+            'print(l.ddl_get_config(b"rccl_min_ctas"), l.ddl_get_config(b"rccl_max_ctas"))' % LIB)
+    env = dict(os.environ, DDL_RCCL_MIN_CTAS='12', DDL_RCCL_MAX_CTAS='999')
+    out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.split() == ['12', '256'], out
+
+
 def test_python_config_module(lib):
     """ddl.torch.config: every documented key reads back, override() restores, bad keys raise."""
     from ddl.torch import config
