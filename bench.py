@@ -1436,7 +1436,7 @@ def multi_gpu(args):
                 if sz > args.size_sweep_max_mib << 20:
                     break
                 m = sz // 4
-                a = torch.randn(m, device=dev, generator=g)
+                a = torch.full((m,), float(rank + 1), device=dev)  # the replayed sums are checkable
                 b = torch.empty_like(a)
                 per_graph, replays = 16, 10
                 gs = torch.cuda.Stream()
@@ -1453,9 +1453,15 @@ def multi_gpu(args):
                 def replay(graph=graph, gs=gs):
                     with torch.cuda.stream(gs):
                         graph.replay()
+                b.fill_(-1.0)
+                torch.cuda.synchronize()
                 t = timed_fn(replay, replays, 1) / per_graph
+                torch.cuda.synchronize()
+                ok = torch.tensor([int(bool((b == float(world * (world + 1) // 2)).all().item()))])
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank's replayed sums exact
                 gcurve.append({'bytes': sz, 'us': round(t * 1e6, 1), 'algbw_GiBs': round(sz / GiB / t, 3),
-                               'busbw_GBs': round(2 * (world - 1) / world * sz / t / 1e9, 2)})
+                               'busbw_GBs': round(2 * (world - 1) / world * sz / t / 1e9, 2),
+                               'replay_exact': bool(ok.item())})
                 out['size_sweep_graph_fp32'] = gcurve
                 del graph, a, b
     except Exception as e:  # e.g. the rehearsal's host-synchronising transport cannot be captured

@@ -624,6 +624,48 @@ def check_resources(ctx):
     sys.stderr.flush()
 
 
+def check_graph_capture(ctx):
+    """The data plane captured into a hipGraph and replayed over real multi-rank RCCL (the test
+    transport synchronises the host and refuses capture): per capture mode (0 serial, 2 single-stream
+    DAG) and schedule (direct, one-shot, gather-fold), K allreduces of different sizes captured once,
+    then replayed three times on fresh inputs written into the captured buffers — every replay
+    bit-exact vs MPICH's order on every rank."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    sizes = (1000, 70_001, 300_001)
+    for mode in (0, 2):
+        for algo in (1, 2, 3):
+            with h.config(lib, tune=0, algo=algo, reference_order=1, capture_mode=mode, slice_bytes=64 << 10):
+                bufs = [(torch.empty(n, device='cuda'), torch.empty(n, device='cuda')) for n in sizes]
+                gs = torch.cuda.Stream()
+                with torch.cuda.stream(gs):  # warm-up outside the capture (staging, events)
+                    for a, b in bufs:
+                        a.fill_(1.0)
+                        assert lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), a.numel(), h.DT_FLOAT, 0,
+                                                 gs.cuda_stream) == 0, lib.ddl_last_error()
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=gs):
+                    for a, b in bufs:
+                        assert lib.ddl_allreduce(comm.id, a.data_ptr(), b.data_ptr(), a.numel(), h.DT_FLOAT, 0,
+                                                 gs.cuda_stream) == 0, lib.ddl_last_error()
+                for rep in range(3):
+                    wants = []
+                    for i, (a, b) in enumerate(bufs):
+                        xs = [h.random_input(h.DT_FLOAT, a.numel(), 1000 * rep + 100 * i + 10 * algo + mode + q)
+                              for q in range(P)]
+                        a.copy_(torch.from_numpy(xs[r]))
+                        b.fill_(float('nan'))
+                        wants.append(ora.fold_ref_order(h.DT_FLOAT, xs))
+                    torch.cuda.synchronize()
+                    with torch.cuda.stream(gs):
+                        g.replay()
+                    torch.cuda.synchronize()
+                    for (a, b), want in zip(bufs, wants):
+                        assert b.cpu().numpy().tobytes() == want.tobytes(), (mode, algo, rep, a.numel())
+                del g
+
+
 def check_fullsize_mpich_hash(ctx):
     """Full-size parity over the real transport: every rank regenerates its
     64 Mi fp32 input of the golden case at this P (tests/golden/golden_fullsize.json: C3 at P = 8,
@@ -648,7 +690,7 @@ def check_fullsize_mpich_hash(ctx):
 
 
 FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resources': check_resources,
-                'check_fullsize_mpich_hash': check_fullsize_mpich_hash}
+                'check_fullsize_mpich_hash': check_fullsize_mpich_hash, 'check_graph_capture': check_graph_capture}
 
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,

@@ -136,3 +136,12 @@ def test_full_size_hash_equals_mpich_over_multirank_rccl(gpu, world):
     res = _run(world, ['check_fullsize_mpich_hash'], timeout=300, hw_queues=2)  # one communicator in use
     for rank, results in res.items():
         assert [n for n, _, _ in results][:1] == ['check_fullsize_mpich_hash'], results
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_graph_capture_over_multirank_rccl(gpu, world):
+    """hipGraph capture of the data plane with real RCCL kernels between processes, serial and DAG
+    posting, three schedules, replayed on fresh inputs bit-exact (check_graph_capture)."""
+    res = _run(world, ['check_graph_capture'], timeout=240)
+    for rank, results in res.items():
+        assert [n for n, _, _ in results][:1] == ['check_graph_capture'], results
