@@ -1463,9 +1463,17 @@ def multi_gpu(args):
                                'busbw_GBs': round(2 * (world - 1) / world * sz / t / 1e9, 2),
                                'replay_exact': bool(ok.item())})
                 out['size_sweep_graph_fp32'] = gcurve
-                del graph, a, b
+                # every captured graph must be gone before finalize: RCCL keeps a captured
+                # collective's resources until its graph is destroyed, and ncclCommDestroy waits for
+                # them (r06 s18: the replay closure kept the last graph alive and teardown hung)
+                del graph, a, b, replay
     except Exception as e:  # e.g. the rehearsal's host-synchronising transport cannot be captured
         out.setdefault('leg_errors', {})['size_sweep_graph'] = repr(e)[:400]
+    finally:  # also after a failed capture: no graph may outlive this leg
+        import gc
+        graph = replay = None
+        gc.collect()
+        torch.cuda.synchronize()
     state['leg'] = 'finalize'
     if rank == 0:
         emit(out)
