@@ -1258,7 +1258,7 @@ def multi_gpu(args):
                 def sub_step(sub=sub):
                     check(lib.ddl_allreduce(sub.id, send.data_ptr(), recv.data_ptr(), n, DT_FLOAT, 0,
                                             stream.cuda_stream), 'ddl_allreduce (cta split)')
-                t = timed_fn(sub_step, reps, 3)  # the first warmup call tunes the new communicator
+                t = timed_fn(sub_step, reps, 3)  # the first warmup call agrees the config on the split
                 cta.append({'min_ctas': lo, 'max_ctas': hi, 'ms': round(t * 1e3, 4),
                             'busbw_GBs': round(2 * (world - 1) / world * S / t / 1e9, 2),
                             'speedup_vs_default': round(t_world / t, 4)})
