@@ -194,9 +194,17 @@ def check_split_communicators_keyed(ctx):
     comms = {'world': comm, 'pair': pair, 'same': same}
     sizes = [7, 300, 5000, 70_001, 1, 4099]
     dts = [h.DT_FLOAT, h.DT_INT32, h.DT_FLOAT, h.DT_DOUBLE, h.DT_FLOAT, h.DT_INT32]
+    # over real RCCL the three communicators' rounds run one communicator at a time unless
+    # DDL_MP_CONCURRENT_SPLITS=1: concurrent keyed rounds of communicators that share ranks can
+    # meet on one in-order hardware queue in different orders on different ranks
+    serial = ctx.get('transport') == 'rccl' and os.environ.get('DDL_MP_CONCURRENT_SPLITS') != '1'
     for rnd in range(2):  # the second round goes by id-table index on every ring
         handles, wants = [], []
         for ci, (name, c) in enumerate(comms.items()):
+            if serial and handles:
+                for hd, (nm, i, want) in zip(handles, wants):
+                    assert hd.wait(timeout=120).cpu().numpy().tobytes() == want.tobytes(), (rnd, nm, i)
+                handles, wants = [], []
             xs = [[h.random_input(dts[i], n, 1000 * rnd + 100 * ci + 31 * i + q) for q in range(P)]
                   for i, n in enumerate(sizes)]
             mem = members[name]
@@ -759,7 +767,7 @@ def worker(rank, world, port, q, only=None, transport='gloo'):
         check(lib.ddl_set_config(b'pipeline_rounds', int(os.environ.get('DDL_MP_PIPELINE_ROUNDS', 1))),
               'ddl_set_config')
         ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
-               'oracle': h.Oracle()}
+               'oracle': h.Oracle(), 'transport': transport}
         import time
         if os.environ.get('DDL_MP_STACKS_S'):  # soak diagnostics: Python stacks of a hung rank
             import faulthandler
