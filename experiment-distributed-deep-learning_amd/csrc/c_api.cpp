@@ -161,7 +161,8 @@ int ddl_set_config(const char *key, long long value) {
             DDL_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, DDL_STATUS_INVALID_ARGUMENT,
                         "compute_cu_mask must be 0 (all CUs), 2, 4 or 8 (every n-th CU left to RCCL)");
             c.compute_cu_mask = value;
-        } else if (k == "rccl_min_ctas" || k == "rccl_max_ctas") {
+        } else if (k == "queue_isolation") c.queue_isolation = value ? 1 : 0;
+        else if (k == "rccl_min_ctas" || k == "rccl_max_ctas") {
             DDL_REQUIRE(value >= 0 && value <= 256, DDL_STATUS_INVALID_ARGUMENT,
                         k << " must be 0 (RCCL's default) or a channel count in [1, 256]");
             (k == "rccl_min_ctas" ? c.rccl_min_ctas : c.rccl_max_ctas) = value;
@@ -216,6 +217,7 @@ long long ddl_get_config(const char *key) {
     if (k == "capture_mode") return c.capture_mode;
     if (k == "fold_form") return get_fold_form();
     if (k == "compute_cu_mask") return c.compute_cu_mask;
+    if (k == "queue_isolation") return c.queue_isolation;
     if (k == "rccl_min_ctas") return c.rccl_min_ctas;
     if (k == "rccl_max_ctas") return c.rccl_max_ctas;
     return -1;

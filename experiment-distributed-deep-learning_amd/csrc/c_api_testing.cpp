@@ -548,6 +548,19 @@ int ddl_testing_compute_stream_cus(int every, int *enabled, int *total) {
     });
 }
 
+int ddl_testing_stream_priorities(ddl_communicator_id id, int *prio) {
+    return guarded([&] {
+        DDL_REQUIRE(prio, DDL_STATUS_INVALID_ARGUMENT, "null output");
+        auto c = Registry::get().find(id);
+        const RankResources &rr = c->executor().resources();
+        DDL_HIP(hipStreamGetPriority(rr.comm, &prio[0]));
+        DDL_HIP(hipStreamGetPriority(rr.compute, &prio[1]));
+        prio[2] = prio[3] = DDL_TESTING_NO_STREAM;
+        if (RequestHandler *h = c->handler_if_created()) DDL_HIP(hipStreamGetPriority(h->stream(), &prio[2]));
+        if (auto kd = c->keyed_data()) DDL_HIP(hipStreamGetPriority(kd->executor().resources().comm, &prio[3]));
+    });
+}
+
 int ddl_testing_host_chunk_cuts(size_t total_bytes, size_t chunk_bytes, size_t *cuts, size_t cap, size_t *count) {
     return guarded([&] {
         DDL_REQUIRE(count && (cuts || cap == 0), DDL_STATUS_INVALID_ARGUMENT, "null output");

@@ -239,4 +239,7 @@ void free_retired();
 // collectives: config agreement, the tuner's max, split records) — no allocation per call.
 void *thread_scratch(size_t bytes);
 
+// Hardware-queue class of an engine stream (executor.h create_engine_stream).
+enum class QueueClass { kPooled, kHigh, kLow };
+
 }  // namespace ddl

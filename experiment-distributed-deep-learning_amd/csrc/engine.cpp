@@ -80,9 +80,14 @@ DeviceGuard::~DeviceGuard() {
 
 // ---- communicator -----------------------------------------------------------------------------
 Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks,
-                           long long tag, std::vector<int> world_ranks)
+                           long long tag, std::vector<int> world_ranks, QueueClass qc)
     : rank_(rank), size_(size), device_(device), nccl_(nccl), hooks_(std::move(hooks)), tag_(tag),
-      world_ranks_(std::move(world_ranks)) {
+      world_ranks_(std::move(world_ranks)),
+      qclass_(nccl && size > 1 && config().queue_isolation.load() ? qc : QueueClass::kPooled) {
+    // the world (created kPooled) keeps its keyed path apart, at the greatest priority
+    keyed_qclass_ = qclass_ == QueueClass::kPooled && nccl_ && size_ > 1 && config().queue_isolation.load()
+                        ? QueueClass::kHigh
+                        : qclass_;
     DeviceGuard g(device_);
     std::unique_ptr<Transport> t;
     if (size_ > 1) {
@@ -94,7 +99,7 @@ Communicator::Communicator(int rank, int size, int device, ncclComm_t nccl, std:
             t.reset(new RcclTransport(nccl_));
         }
     }
-    exec_.reset(new RingExecutor(rank_, size_, device_, std::move(t)));
+    exec_.reset(new RingExecutor(rank_, size_, device_, std::move(t), qclass_));
 }
 
 Communicator::~Communicator() {
@@ -239,7 +244,7 @@ void Communicator::agree_config(hipStream_t stream) {
         }
         cb_->host_group(ops);
     } else {
-        if (!ctl_stream_) DDL_HIP(hipStreamCreateWithFlags(&ctl_stream_, hipStreamNonBlocking));
+        if (!ctl_stream_) ctl_stream_ = create_engine_stream(qclass_);
         rccl_allgather_u64(nccl_, all.data(), size_, rank_, ctl_stream_);
     }
     check_config_agreement(rank_, all);
@@ -537,9 +542,9 @@ void Communicator::allreduce_host(const void *send, void *recv, size_t n, int dt
     chunk = chunk < 4096 ? 4096 : chunk & ~size_t(255);
     if (chunk > total) chunk = (total + 255) & ~size_t(255);
     if (!h2d_) {
-        DDL_HIP(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
-        DDL_HIP(hipStreamCreateWithFlags(&ring_, hipStreamNonBlocking));
-        DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+        h2d_ = create_engine_stream(qclass_);
+        ring_ = create_engine_stream(qclass_);
+        d2h_ = create_engine_stream(qclass_);
     }
     if (slot_bytes_ < chunk) {
         for (void *&sl : slots_) {  // outgrown: kept until ddl_finalize (retire_device)
@@ -690,7 +695,10 @@ std::shared_ptr<Communicator> Communicator::split(int color, int key, bool keyed
         DDL_REQUIRE(nc != nullptr, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
         DDL_REQUIRE(r == me && n == s, DDL_STATUS_COMM_ERROR,
                     "ncclCommSplit gave rank " << r << " of " << n << ", the split exchange " << me << " of " << s);
-        c = new_communicator(r, n, device_, nc);
+        // queue class (executor.h QueueClass): a user split the least priority's pool; a private
+        // keyed communicator (keyed == false, made by enable_keyed) its owner's keyed class
+        const QueueClass qc = keyed ? QueueClass::kLow : keyed_qclass_;
+        c = new_communicator(r, n, device_, nc, nullptr, 0, std::vector<int>{}, qc);
     } else {
         DDL_REQUIRE(color >= 0, DDL_STATUS_INVALID_ARGUMENT, "negative color: rank is in no communicator");
         c = new_communicator(0, 1, device_, nullptr);

@@ -132,6 +132,12 @@ struct Config {
     // mismatched RCCL kernels.
     std::atomic<long long> rccl_min_ctas{0};
     std::atomic<long long> rccl_max_ctas{0};
+    // 1 (default): the engine's streams are created in hardware-queue classes (executor.h
+    // QueueClass): the world's user streams, its keyed path and the splits each in a priority
+    // pool of HIP's hardware queues of their own;
+    // 0: every stream in HIP's default pool (the r05 behaviour). Read when a stream is created;
+    // local.
+    std::atomic<long long> queue_isolation{1};
     // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'
@@ -174,14 +180,23 @@ public:
     // `hooks` (test harness only, ddl_init_test_transport): groups go to host callbacks, `tag`
     // names this communicator to them, `world_ranks[i]` is the world rank of rank i (empty: the
     // world itself); nullptr = RCCL on `nccl`.
+    // `qc`: the hardware-queue class of the communicator's own streams (executor, control, host
+    // pipeline; executor.h QueueClass), decided by who creates it: the world kPooled, the world's
+    // private keyed communicator kHigh, splits and theirs kLow (RCCL only, config
+    // queue_isolation 1).
     Communicator(int rank, int size, int device, ncclComm_t nccl, std::shared_ptr<TestHooks> hooks = nullptr,
-                 long long tag = 0, std::vector<int> world_ranks = {});
+                 long long tag = 0, std::vector<int> world_ranks = {}, QueueClass qc = QueueClass::kPooled);
     ~Communicator();
 
     long long id() const { return reinterpret_cast<long long>(this); }
     int rank() const { return rank_; }
     int size() const { return size_; }
     int device() const { return device_; }
+    QueueClass queue_class() const { return qclass_; }
+    // the class of the streams of this communicator's keyed path (handler, fusion pipe, private
+    // data-plane communicator): apart from the world's user streams (kHigh) for the world, its
+    // split's (kLow) for a split; fixed at creation like queue_class()
+    QueueClass keyed_queue_class() const { return keyed_qclass_; }
     ncclComm_t nccl() const { return nccl_; }
 
     // Communicator::allreduce (reference Communicator.h:45-48), device buffers, stream-ordered.
@@ -309,6 +324,7 @@ private:
     // the tuner's scratch buckets (grow-only, retired on growth: no hipFree while others run)
     void *tune_a_ = nullptr, *tune_b_ = nullptr;
     size_t tune_cap_ = 0;
+    QueueClass qclass_ = QueueClass::kPooled, keyed_qclass_ = QueueClass::kPooled;
 };
 
 // Set on a request handler's engine and completion threads. The last reference to a communicator

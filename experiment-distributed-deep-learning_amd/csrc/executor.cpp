@@ -55,6 +55,18 @@ void RcclTransport::allgather(const GatherOp &g, hipStream_t stream) {
     if (dep::on()) dep::op(stream, "rccl allgather", {dep::rd(g.send, g.bytes), dep::wr(g.recv, g.bytes)});
 }
 
+hipStream_t create_engine_stream(QueueClass qc, int cu_mask_every) {
+    if (cu_mask_every >= 2 || qc == QueueClass::kPooled) {
+        // a CU-masked stream already has a hardware queue of its own
+        return create_compute_stream(cu_mask_every);
+    }
+    int least = 0, greatest = 0;
+    DDL_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    DDL_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, qc == QueueClass::kHigh ? greatest : least));
+    return s;
+}
+
 hipStream_t create_compute_stream(int every) {
     hipStream_t s = nullptr;
     int ncu = device_cu_count();
@@ -75,9 +87,9 @@ hipStream_t create_compute_stream(int every) {
     return s;
 }
 
-RankResources::RankResources(int dev, int cu_mask_every) : device(dev) {
-    DDL_HIP(hipStreamCreateWithFlags(&comm, hipStreamNonBlocking));
-    compute = create_compute_stream(cu_mask_every);
+RankResources::RankResources(int dev, int cu_mask_every, QueueClass qc) : device(dev) {
+    comm = create_engine_stream(qc);
+    compute = create_engine_stream(qc, cu_mask_every);
     DDL_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     DDL_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     DDL_HIP(hipEventCreateWithFlags(&join_cp_ev, hipEventDisableTiming));
@@ -199,8 +211,9 @@ int last_reduce_at_or_before(const RingProgram &p, int w) {
     return -1;
 }
 
-RingExecutor::RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport)
-    : rank_(rank), size_(size), transport_(std::move(transport)), res_(device, size > 1 ? config_compute_cu_mask() : 0) {}
+RingExecutor::RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport, QueueClass qc)
+    : rank_(rank), size_(size), transport_(std::move(transport)),
+      res_(device, size > 1 ? config_compute_cu_mask() : 0, qc) {}
 
 RingExecutor::~RingExecutor() {
     for (auto *v : {&timed_, &free_pairs_})

@@ -53,6 +53,24 @@ int config_compute_cu_mask();
 // A non-blocking stream whose kernels avoid every `every`-th CU (every >= 2; otherwise, or where
 // the runtime refuses CU masks, an ordinary non-blocking stream).
 hipStream_t create_compute_stream(int every);
+// Hardware-queue isolation of the engine's streams (r06). HIP maps a process's
+// streams of one priority onto a small pool of in-order hardware queues (tools/queue_probe.hip:
+// the 8th ordinary stream shares the 1st one's queue, profiles/r06/s24), so two communicators'
+// RCCL kernels — or their stream waits — can land on one queue and run in posting order; ranks
+// that posted them in different orders then wait for each other forever (three communicators
+// running keyed rounds at once over real RCCL, profiles/r06/s23). Each priority has a pool of
+// its own (s24), so the engine spreads its communicators over the three:
+//  kPooled  the default priority: the world's own executor (the user's direct collectives,
+//           ordered by the user and, against keyed rounds, by §6) and the test harness;
+//  kHigh    the greatest priority: the world's keyed data plane (handler, fusion pipe, its
+//           private communicator) — apart from the user's streams, and communication first;
+//  kLow     the least priority: every stream of a split communicator and of its keyed path.
+// Splits still share the least priority's pool with each other: keyed rounds on two splits that
+// share ranks are not isolated. All three are non-blocking streams (a CU-masked
+// stream would get a queue of its own but is ordered with the legacy NULL stream).
+// Config "queue_isolation" 0 makes every stream kPooled (the r05 behaviour).
+// (enum QueueClass { kPooled, kHigh, kLow } lives in common.h)
+hipStream_t create_engine_stream(QueueClass qc, int cu_mask_every = 0);
 
 // Posts a program's ops on its logical streams (each rank's comm / compute stream, a transport
 // stream) with event records and waits between them, in one of three ways:
@@ -126,7 +144,7 @@ class RankResources {
 public:
     // cu_mask_every >= 2: the compute stream (reduce / fold kernels) is created with every
     // cu_mask_every-th CU masked off (config "compute_cu_mask"), leaving those to RCCL's kernels
-    RankResources(int device, int cu_mask_every = 0);
+    RankResources(int device, int cu_mask_every = 0, QueueClass qc = QueueClass::kPooled);
     ~RankResources();
     RankResources(const RankResources &) = delete;
     RankResources &operator=(const RankResources &) = delete;
@@ -162,7 +180,8 @@ struct KernelStats {
 // Single-rank executor over a Transport (RCCL in production).
 class RingExecutor {
 public:
-    RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport);
+    RingExecutor(int rank, int size, int device, std::unique_ptr<Transport> transport,
+                 QueueClass qc = QueueClass::kPooled);
     ~RingExecutor();
     void allreduce(const void *in, void *out, size_t n, int dtype, hipStream_t user,
                    const RingConfig &cfg);
@@ -177,6 +196,7 @@ public:
     int size() const { return size_; }
     void set_timing(bool on);
     KernelStats collect_stats();  // synchronises the recorded timing events, then resets
+    const RankResources &resources() const { return res_; }
 
 private:
     // posts prog_ on the streams, forked from / joined to user (graph-safe when user is captured)

@@ -90,7 +90,7 @@ void FusionPipe::run(const std::vector<const void *> &srcs, const std::vector<vo
     size_t maxflat = 0;
     for (const Sub &sb : subs) maxflat = sb.flat > maxflat ? sb.flat : maxflat;
     void *buf[2] = {ensure(0, maxflat, stream), ensure(1, maxflat, stream)};
-    if (!side_) DDL_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    if (!side_) side_ = create_engine_stream(qc);
     const size_t J = subs.size();
     last_subplans_ = J;
     // events: [0] fork, [1 + 2j] pack j done, [2 + 2j] allreduce j done, [1 + 2J] join

@@ -31,8 +31,8 @@ public:
     FusionPipe(const FusionPipe &) = delete;
     FusionPipe &operator=(const FusionPipe &) = delete;
 
-    // Fusion buffer i (0 or 1) of at least `need` bytes; a regrow first synchronises `stream`
-    // (every earlier use of the buffer, the side stream's included, is ordered before it there).
+    // Fusion buffer i (0 or 1) of at least `need` bytes; an outgrown buffer is retired, not freed
+    // (common.h retire_device): earlier uses of it may still be in flight.
     void *ensure(int i, size_t need, hipStream_t stream);
     // elems of the plan's dtype in `buf`, reduced in place on the pipe's stream; `message_bytes`
     // = the whole plan's unpadded bytes (the reference's MPI_Allreduce message)
@@ -44,6 +44,8 @@ public:
     size_t subplans() const { return last_subplans_; }  // of the last run
 
     SegmentCopier copier;
+    // hardware-queue class of the side stream (executor.h QueueClass; set by the owning handler)
+    QueueClass qc = QueueClass::kPooled;
 
 private:
     hipEvent_t event_(size_t i);

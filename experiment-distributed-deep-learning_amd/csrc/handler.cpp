@@ -353,7 +353,9 @@ RequestHandler::RequestHandler(Communicator *owner) : owner_(owner) {
     // the fusion pack / unpack kernels overlap other plans' RCCL kernels at size > 1: the same CU
     // mask as the executors' compute streams (config compute_cu_mask; pack / unpack keep their
     // rate on it, tools/cu_mask_probe.py)
-    stream_ = create_compute_stream(owner_->size() > 1 ? config_compute_cu_mask() : 0);
+    // its hardware-queue class (executor.h QueueClass): apart from the user's streams
+    stream_ = create_engine_stream(owner_->keyed_queue_class(), owner_->size() > 1 ? config_compute_cu_mask() : 0);
+    fp_.qc = owner_->keyed_queue_class();
     done_thread_ = std::thread(&RequestHandler::completer_, this);
     thread_ = std::thread(&RequestHandler::main_, this);
 }
@@ -972,8 +974,8 @@ size_t RequestHandler::host_slots_(size_t total) {
         host_slot_bytes_ = chunk;
     }
     if (!h2d_) {
-        DDL_HIP(hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
-        DDL_HIP(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+        h2d_ = create_engine_stream(owner_->keyed_queue_class());
+        d2h_ = create_engine_stream(owner_->keyed_queue_class());
         for (hipEvent_t &e : hev_) DDL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return chunk;

@@ -198,6 +198,7 @@ class RequestHandler {
 public:
     explicit RequestHandler(Communicator *owner);
     ~RequestHandler();
+    hipStream_t stream() const { return stream_; }  // the engine thread's (pack / unpack)
 
     void submit(Request r);
     // Unregisters every range of the host registration cache (ddl_set_config

@@ -20,7 +20,7 @@ from ddl.torch.cpp_backend import CPPBackend, check
 KEYS = ('algo', 'slice_bytes', 'rings', 'max_slices', 'fusion_threshold_bytes', 'log_level', 'cycle_time_us',
         'host_chunk_bytes', 'host_copy_threads', 'host_zero_copy', 'tune', 'fusion_pipeline_bytes', 'one_rank_shortcut',
         'pipeline_rounds', 'reference_order', 'host_register_cache_bytes', 'capture_mode',
-        'fold_form', 'compute_cu_mask', 'host_numa_bind', 'rccl_min_ctas', 'rccl_max_ctas')
+        'fold_form', 'compute_cu_mask', 'host_numa_bind', 'rccl_min_ctas', 'rccl_max_ctas', 'queue_isolation')
 SHARED = ('algo', 'slice_bytes', 'rings', 'max_slices', 'fusion_threshold_bytes', 'tune', 'fusion_pipeline_bytes',
           'reference_order', 'host_chunk_bytes', 'rccl_min_ctas', 'rccl_max_ctas')
 

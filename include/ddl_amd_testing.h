@@ -192,6 +192,13 @@ int ddl_testing_dep_check(long long *counts, char *report, size_t len);
 /* The CUs enabled on an executor compute stream created with every `every`-th CU masked off
  * (config "compute_cu_mask"; 0 = unmasked), read back with hipExtStreamGetCUMask. */
 int ddl_testing_compute_stream_cus(int every, int *enabled, int *total);
+/* The stream priorities of a communicator's engine streams (config "queue_isolation", executor.h
+ * QueueClass): prio[0] / prio[1] its executor's comm / compute stream, prio[2] its keyed
+ * handler's stream, prio[3] its private keyed data-plane communicator's comm stream
+ * (DDL_TESTING_NO_STREAM where that object does not exist yet). hipDeviceGetStreamPriorityRange
+ * gives the meaning: lower is more urgent, 0 is the default. */
+#define DDL_TESTING_NO_STREAM (-1000)
+int ddl_testing_stream_priorities(ddl_communicator_id id, int *prio);
 /* The chunk boundaries of a host-staged transfer (ddl_allreduce_host, the keyed handler's host
  * plans): whole chunks of chunk_bytes, the last one short. Writes min(count, cap) boundaries
  * cut[0] = 0 < ... < cut[count - 1] = total_bytes into cuts and sets *count. Pure host arithmetic

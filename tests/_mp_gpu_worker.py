@@ -194,14 +194,18 @@ def check_split_communicators_keyed(ctx):
     comms = {'world': comm, 'pair': pair, 'same': same}
     sizes = [7, 300, 5000, 70_001, 1, 4099]
     dts = [h.DT_FLOAT, h.DT_INT32, h.DT_FLOAT, h.DT_DOUBLE, h.DT_FLOAT, h.DT_INT32]
-    # over real RCCL the three communicators' rounds run one communicator at a time unless
-    # DDL_MP_CONCURRENT_SPLITS=1: concurrent keyed rounds of communicators that share ranks can
-    # meet on one in-order hardware queue in different orders on different ranks
-    serial = ctx.get('transport') == 'rccl' and os.environ.get('DDL_MP_CONCURRENT_SPLITS') != '1'
+    # over real RCCL, keyed rounds of two SPLITS that share ranks can meet on one in-order
+    # hardware queue (both in the least priority's pool, config queue_isolation) in different
+    # orders on different ranks: the world's rounds run beside the pair's, the
+    # same-size split's after them (queue_isolation 0: one communicator at a time);
+    # DDL_MP_CONCURRENT_SPLITS=1 runs all three at once
+    flush_before = set()
+    if ctx.get('transport') == 'rccl' and os.environ.get('DDL_MP_CONCURRENT_SPLITS') != '1':
+        flush_before = {'same'} if lib.ddl_get_config(b'queue_isolation') == 1 else {'pair', 'same'}
     for rnd in range(2):  # the second round goes by id-table index on every ring
         handles, wants = [], []
         for ci, (name, c) in enumerate(comms.items()):
-            if serial and handles:
+            if name in flush_before and handles:
                 for hd, (nm, i, want) in zip(handles, wants):
                     assert hd.wait(timeout=120).cpu().numpy().tobytes() == want.tobytes(), (rnd, nm, i)
                 handles, wants = [], []
@@ -226,6 +230,45 @@ def check_split_communicators_keyed(ctx):
             assert np.array_equal(got, want), name
     pair.detach()
     same.detach()
+
+
+def check_queue_classes(ctx):
+    """Config queue_isolation: over RCCL the world's executor streams sit at the
+    default priority, its keyed data plane (handler stream, private communicator) at the greatest
+    and a split's streams at the least — three pools of HIP's in-order hardware queues; with the
+    key at 0, or over the test transport (no RCCL kernels), every stream at the default. A keyed
+    batch on the split and on the world stays bit-exact vs MPICH's order."""
+    import _helpers as h
+    torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
+    from ddl.torch.tensor_communicate import allreduce_async_batch
+    rccl = ctx.get('transport') == 'rccl'
+
+    def prios(c):
+        out = (ctypes.c_int * 4)()
+        assert lib.ddl_testing_stream_priorities(ctypes.c_longlong(c.id), out) == 0, lib.ddl_last_error()
+        return list(out)
+
+    def keyed(c, tag):
+        xs = [[h.random_input(h.DT_FLOAT, 3000 + 7 * i, 400 + 10 * i + q) for q in range(P)] for i in range(2)]
+        hs = allreduce_async_batch([torch.from_numpy(x[r]).cuda() for x in xs], [f'{tag}_a', f'{tag}_b'], c)
+        gb = sum(x[0].nbytes for x in xs)
+        for hd, x in zip(hs, xs):
+            assert hd.wait(timeout=120).cpu().numpy().tobytes() == ora.fold_ref_order(h.DT_FLOAT, x, gb).tobytes()
+
+    # HIP's range on gfx950 is least 1, greatest -1, default 0 (torch's Stream.priority_range
+    # reports (0, -1): it clamps the least to the default), so: more urgent < 0 < less urgent
+    keyed(comm, 'qc_world')
+    w = prios(comm)
+    assert w[:2] == [0, 0] and w[2] == w[3] and (w[2] < 0 if rccl else w[2] == 0), w
+    for iso in (1, 0):
+        with h.config(lib, queue_isolation=iso):
+            sub = comm.split_communicator(0, r)
+        try:
+            keyed(sub, f'qc_split{iso}')
+            p = prios(sub)
+            assert len(set(p)) == 1 and (p[0] > 0 if rccl and iso else p[0] == 0), (iso, p)
+        finally:
+            sub.detach()
 
 
 def check_rccl_channel_bounds(ctx):
@@ -703,7 +746,7 @@ FAULT_CHECKS = {'check_control_link_lost': check_control_link_lost, 'check_resou
 
 CHECKS = [check_reference_known_answers, check_schedules_vs_oracle, check_allreduce_batch, check_tuned_exact,
           check_keyed_fusion,
-          check_keyed_reference_order, check_split_communicators_keyed, check_rccl_channel_bounds,
+          check_keyed_reference_order, check_split_communicators_keyed, check_queue_classes, check_rccl_channel_bounds,
           check_keyed_host_requests,
           check_keyed_broadcast_allgather, check_host_resident, check_dp_training, check_dp_training_cpu_model,
           check_dp_training_overlap, check_config_mismatch, check_keyed_round_order]

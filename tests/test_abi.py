@@ -181,6 +181,10 @@ def test_config_roundtrip(lib):
         assert lib.ddl_set_config(key, -1) == 3 and lib.ddl_set_config(key, 257) == 3
         for v in (1, 32, 256, 0):
             assert lib.ddl_set_config(key, v) == 0 and lib.ddl_get_config(key) == v
+    # hardware-queue classes of multi-rank communicators' streams: on by default, local, 0 / 1
+    assert lib.ddl_get_config(b'queue_isolation') == 1
+    for v in (0, 1):
+        assert lib.ddl_set_config(b'queue_isolation', v) == 0 and lib.ddl_get_config(b'queue_isolation') == v
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
     assert lib.ddl_set_config(b'fold_form', 3) == 3
