@@ -33,6 +33,7 @@ Config &config() {
         // RCCL channel bounds for a deployment that sets them per job (0..256, as ddl_set_config)
         if (const char *e = std::getenv("DDL_RCCL_MIN_CTAS")) cfg->rccl_min_ctas = std::max(0ll, std::min(256ll, std::atoll(e)));
         if (const char *e = std::getenv("DDL_RCCL_MAX_CTAS")) cfg->rccl_max_ctas = std::max(0ll, std::min(256ll, std::atoll(e)));
+        if (const char *e = std::getenv("DDL_QUEUE_ISOLATION")) cfg->queue_isolation = std::atoll(e) ? 1 : 0;
         if (const char *e = std::getenv("DDL_LOG_LEVEL")) cfg->log_level = std::atoll(e);
         if (const char *e = std::getenv("DDL_CYCLE_TIME_US")) cfg->cycle_time_us = std::atoll(e);
         if (const char *e = std::getenv("DDL_TUNE")) cfg->tune = std::atoll(e);

@@ -132,12 +132,13 @@ struct Config {
     // mismatched RCCL kernels.
     std::atomic<long long> rccl_min_ctas{0};
     std::atomic<long long> rccl_max_ctas{0};
-    // 1 (default): the engine's streams are created in hardware-queue classes (executor.h
-    // QueueClass): the world's user streams, its keyed path and the splits each in a priority
-    // pool of HIP's hardware queues of their own;
-    // 0: every stream in HIP's default pool (the r05 behaviour). Read when a stream is created;
+    // 1: the engine's streams are created in hardware-queue classes (executor.h QueueClass): the
+    // world's user streams, its keyed path and the splits each in a priority pool of HIP's
+    // hardware queues of their own; 0 (default; env DDL_QUEUE_ISOLATION seeds it): every stream
+    // in HIP's default pool. Off by default: the extra queues crawled the 8-rank one-GPU rehearsal
+    // (profiles/r06/s29) and no node has measured them yet. Read when a communicator is created;
     // local.
-    std::atomic<long long> queue_isolation{1};
+    std::atomic<long long> queue_isolation{0};
     // bumped by every ddl_set_config
     std::atomic<long long> epoch{0};
     // Hash of the tunables every rank of a communicator must share (they shape the collectives'

@@ -68,7 +68,7 @@ hipStream_t create_compute_stream(int every);
 // Splits still share the least priority's pool with each other: keyed rounds on two splits that
 // share ranks are not isolated. All three are non-blocking streams (a CU-masked
 // stream would get a queue of its own but is ordered with the legacy NULL stream).
-// Config "queue_isolation" 0 makes every stream kPooled (the r05 behaviour).
+// Config "queue_isolation" 0 (the default) makes every stream kPooled.
 // (enum QueueClass { kPooled, kHigh, kLow } lives in common.h)
 hipStream_t create_engine_stream(QueueClass qc, int cu_mask_every = 0);
 

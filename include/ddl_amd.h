@@ -156,12 +156,12 @@ int ddl_is_initialized(void);
  * communicator created afterwards — ddl_init's ncclCommInitRankConfig, ddl_comm_split's and the
  * keyed data plane's ncclCommSplit — bounding its channel count and with it the p2p channels the
  * direct schedule's concurrent sends and receives spread over; shared tunables),
- * "queue_isolation" (1, default: the streams of multi-rank RCCL communicators are created in
- * three stream-priority classes, each of which HIP maps to a pool of in-order hardware queues of
- * its own — the world's direct collectives at the default priority, the world's keyed data
- * plane at the greatest, split communicators at the least — so one communicator's queued RCCL
- * kernels cannot hold another's behind them; 0: every stream at the default priority; read when
- * a communicator is created; local),
+ * "queue_isolation" (0, default: every engine stream at the default priority; 1: the streams of
+ * multi-rank RCCL communicators are created in three stream-priority classes, each of which HIP
+ * maps to a pool of in-order hardware queues of its own — the world's direct collectives at the
+ * default priority, the world's keyed data plane at the greatest, split communicators at the
+ * least — so one communicator's queued RCCL kernels cannot hold another's behind them; env
+ * DDL_QUEUE_ISOLATION seeds it; read when a communicator is created; local),
  * "fusion_pipeline_bytes" (keyed fusion plans above this run as a pack / allreduce / unpack
  * pipeline of sub-plans of at most this size; 0 = unpipelined), "one_rank_shortcut" (1: a
  * one-rank world skips the keyed data plane; 0: runs it, for tests), "pipeline_rounds" (1,

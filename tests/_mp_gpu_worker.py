@@ -233,10 +233,11 @@ def check_split_communicators_keyed(ctx):
 
 
 def check_queue_classes(ctx):
-    """Config queue_isolation: over RCCL the world's executor streams sit at the
-    default priority, its keyed data plane (handler stream, private communicator) at the greatest
-    and a split's streams at the least — three pools of HIP's in-order hardware queues; with the
-    key at 0, or over the test transport (no RCCL kernels), every stream at the default. A keyed
+    """Config queue_isolation: with it on, over RCCL the world's executor streams sit
+    at the default priority, its keyed data plane (handler stream, private communicator) at the
+    greatest and a split's streams at the least — three pools of HIP's in-order hardware queues;
+    with the key at 0 (default), or over the test transport (no RCCL kernels), every stream at the
+    default. A keyed
     batch on the split and on the world stays bit-exact vs MPICH's order."""
     import _helpers as h
     torch, lib, comm, P, r, ora = ctx['torch'], ctx['lib'], ctx['comm'], ctx['P'], ctx['rank'], ctx['oracle']
@@ -258,8 +259,8 @@ def check_queue_classes(ctx):
     # HIP's range on gfx950 is least 1, greatest -1, default 0 (torch's Stream.priority_range
     # reports (0, -1): it clamps the least to the default), so: more urgent < 0 < less urgent
     keyed(comm, 'qc_world')
-    w = prios(comm)
-    assert w[:2] == [0, 0] and w[2] == w[3] and (w[2] < 0 if rccl else w[2] == 0), w
+    w = prios(comm)  # the world's class was fixed at ddl_init (default 0, DDL_QUEUE_ISOLATION)
+    assert w[:2] == [0, 0] and w[2] == w[3] and (w[2] < 0 if rccl and ctx['queue_isolation'] else w[2] == 0), w
     for iso in (1, 0):
         with h.config(lib, queue_isolation=iso):
             sub = comm.split_communicator(0, r)
@@ -789,7 +790,8 @@ def worker(rank, world, port, q, only=None, transport='gloo'):
         lib = CPPBackend.c_api()
         import gloo_transport
         # engine placement knobs for A/B runs (read when the executors / handlers are created)
-        for env, key in (('DDL_MP_NUMA_BIND', b'host_numa_bind'), ('DDL_MP_CU_MASK', b'compute_cu_mask')):
+        for env, key in (('DDL_MP_NUMA_BIND', b'host_numa_bind'), ('DDL_MP_CU_MASK', b'compute_cu_mask'),
+                         ('DDL_MP_QUEUE_ISOLATION', b'queue_isolation')):
             if os.environ.get(env):
                 check(lib.ddl_set_config(key, int(os.environ[env])), 'ddl_set_config')
         if transport == 'rccl':
@@ -810,7 +812,8 @@ def worker(rank, world, port, q, only=None, transport='gloo'):
         check(lib.ddl_set_config(b'pipeline_rounds', int(os.environ.get('DDL_MP_PIPELINE_ROUNDS', 1))),
               'ddl_set_config')
         ctx = {'torch': torch, 'dist': dist, 'lib': lib, 'comm': comm, 'P': world, 'rank': rank,
-               'oracle': h.Oracle(), 'transport': transport}
+               'oracle': h.Oracle(), 'transport': transport,
+               'queue_isolation': lib.ddl_get_config(b'queue_isolation')}
         import time
         if os.environ.get('DDL_MP_STACKS_S'):  # soak diagnostics: Python stacks of a hung rank
             import faulthandler

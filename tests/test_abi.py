@@ -181,9 +181,9 @@ def test_config_roundtrip(lib):
         assert lib.ddl_set_config(key, -1) == 3 and lib.ddl_set_config(key, 257) == 3
         for v in (1, 32, 256, 0):
             assert lib.ddl_set_config(key, v) == 0 and lib.ddl_get_config(key) == v
-    # hardware-queue classes of multi-rank communicators' streams: on by default, local, 0 / 1
-    assert lib.ddl_get_config(b'queue_isolation') == 1
-    for v in (0, 1):
+    # hardware-queue classes of multi-rank communicators' streams: off by default, local, 0 / 1
+    assert lib.ddl_get_config(b'queue_isolation') == 0
+    for v in (1, 0):
         assert lib.ddl_set_config(b'queue_isolation', v) == 0 and lib.ddl_get_config(b'queue_isolation') == v
     # the fold's form: 0 auto (default), 1 tile, 2 run
     assert lib.ddl_get_config(b'fold_form') == 0
@@ -206,14 +206,15 @@ def test_product_does_not_reference_oracle():
 
 
 def test_rccl_channel_bounds_from_the_environment():
-    """DDL_RCCL_MIN_CTAS / DDL_RCCL_MAX_CTAS seed rccl_min_ctas / rccl_max_ctas (clamped to 0..256)
-    for a deployment that sets them per job; read in a fresh process (the config is built once)."""
+    """DDL_RCCL_MIN_CTAS / DDL_RCCL_MAX_CTAS seed rccl_min_ctas / rccl_max_ctas (clamped to 0..256),
+    DDL_QUEUE_ISOLATION queue_isolation, for a deployment that sets them per job; read in a fresh process (the config is built once)."""
     import sys
     code = ('import ctypes; l = ctypes.CDLL(%r); l.ddl_get_config.restype = ctypes.c_longlong; '
-            'print(l.ddl_get_config(b"rccl_min_ctas"), l.ddl_get_config(b"rccl_max_ctas"))' % LIB)
-    env = dict(os.environ, DDL_RCCL_MIN_CTAS='12', DDL_RCCL_MAX_CTAS='999')
+            'print(l.ddl_get_config(b"rccl_min_ctas"), l.ddl_get_config(b"rccl_max_ctas"), '
+            'l.ddl_get_config(b"queue_isolation"))' % LIB)
+    env = dict(os.environ, DDL_RCCL_MIN_CTAS='12', DDL_RCCL_MAX_CTAS='999', DDL_QUEUE_ISOLATION='1')
     out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, check=True).stdout
-    assert out.split() == ['12', '256'], out
+    assert out.split() == ['12', '256', '1'], out
 
 
 def test_python_config_module(lib):

@@ -80,6 +80,18 @@ def test_engine_over_multirank_rccl(gpu, world):
 
 
 @pytest.mark.parametrize('world', [2, 3])
+def test_queue_isolation_over_rccl(gpu, world, monkeypatch):
+    """Config queue_isolation = 1 from ddl_init on (the worker sets it before the world exists):
+    the world's keyed data plane at the greatest stream priority, splits at the least, read back;
+    the world's keyed rounds beside a split's stay bit-exact vs MPICH's order."""
+    monkeypatch.setenv('DDL_MP_QUEUE_ISOLATION', '1')  # spawned children inherit it
+    names = ['check_split_communicators_keyed', 'check_queue_classes']
+    res = _run(world, names, timeout=180)
+    for rank, results in res.items():
+        assert [n for n, _, _ in results] == names, results
+
+
+@pytest.mark.parametrize('world', [2, 3])
 def test_control_link_lost_mid_round_over_rccl(gpu, world):
     """ADVICE r3's fault case over real RCCL communicators: a control link lost after a member froze
     its user collectives for a keyed round stops every rank's handler; keyed requests complete with
