@@ -4,7 +4,8 @@
 // finishes while the long one still runs tells whether the two streams sit on different hardware
 // queues (an in-order queue runs its packets one after another). Streams: 8 ordinary non-blocking
 // ones (HIP pools a process's streams onto GPU_MAX_HW_QUEUES queues), then non-blocking streams at
-// the greatest and least priority, then a full-CU-mask stream.
+// the greatest and least priority, then a full-CU-mask stream; then, within each priority's own
+// pool of 8 streams, which share the pool's first stream's queue.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/queue_probe.hip -o tools/bin/queue_probe
 #include <hip/hip_runtime.h>
@@ -45,15 +46,18 @@ int main() {
         CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
         s.push_back({"pooled_" + std::to_string(i), x});
     }
-    for (int i = 0; i < 2; ++i) {
+    std::vector<hipStream_t> hi, lo;  // the priority pools' own sizes: 8 streams each (second pass)
+    for (int i = 0; i < 8; ++i) {
         hipStream_t x;
         CK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, greatest));
-        s.push_back({"greatest_priority_" + std::to_string(i), x});
+        if (i < 2) s.push_back({"greatest_priority_" + std::to_string(i), x});
+        hi.push_back(x);
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 8; ++i) {
         hipStream_t x;
         CK(hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least));
-        s.push_back({"least_priority_" + std::to_string(i), x});
+        if (i < 2) s.push_back({"least_priority_" + std::to_string(i), x});
+        lo.push_back(x);
     }
     {
         int ncu = 0;
@@ -85,6 +89,24 @@ int main() {
         std::printf("{\"stream\": \"%s\", \"short_kernel_ms\": %.3f, \"shares_queue_with_pooled_0\": %s}\n",
                     s[i].first.c_str(), short_ms, short_ms > 150.0 ? "true" : "false");
         std::fflush(stdout);
+    }
+    // second pass: within each priority pool, which streams share the pool's first stream's queue
+    for (auto *pool : {&hi, &lo}) {
+        const char *name = pool == &hi ? "greatest" : "least";
+        for (size_t i = 1; i < pool->size(); ++i) {
+            hipLaunchKernelGGL(k_busy, dim3(1), dim3(64), 0, (*pool)[0], cycles, flag);
+            const clk::time_point t0 = clk::now();
+            while (std::chrono::duration<double>(clk::now() - t0).count() < 0.02) {
+            }
+            hipLaunchKernelGGL(k_busy, dim3(1), dim3(64), 0, (*pool)[i], 1000LL, flag + 1);
+            const clk::time_point t1 = clk::now();
+            CK(hipStreamSynchronize((*pool)[i]));
+            const double short_ms = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
+            CK(hipStreamSynchronize((*pool)[0]));
+            std::printf("{\"pool\": \"%s\", \"stream\": %zu, \"short_kernel_ms\": %.3f, \"shares_queue_with_pool_0\": %s}\n",
+                        name, i, short_ms, short_ms > 150.0 ? "true" : "false");
+            std::fflush(stdout);
+        }
     }
     CK(hipFree(flag));
     return 0;
